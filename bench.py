@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DRN-D-22 segmentation of 1024x2048 frames on MI355X (BASELINE.json).
+
+A step = one pass of the seg_video hot loop (reference seg_video_old_no_plot.py:157-169:
+normalise -> model(img)[0] -> torch.max(final, 1)) over a batch of synthetic uint8 RGB
+frames already resident in HBM: frame ingest -> 22 fused conv launches -> seg -> up x8 +
+log-softmax + argmax, producing uint8 label maps.  Frames shard across ranks (one process
+per GPU, weak scaling, no collective on the data path; the only collectives are the
+timing barrier and the max-over-ranks of the elapsed time).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "video-seg-model-compress_amd"))
+sys.path.insert(0, REPO)
+
+METRIC = "frames/sec @1024x2048 DRN-D-22 on 1/2/4/8 MI355X; mIoU vs ref; %HBM roofline"
+DOMINANT_T = "conv_igemm_kernel<{}, 128, 128, 2, 2, 3>"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4, help="frames per GPU per step")
+    ap.add_argument("--arch", default="drn_d_22")
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--width", type=int, default=2048)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true")
+    return ap.parse_args()
+
+
+def tile_of(cout):
+    return 0 if cout > 64 else 1 if cout > 32 else 2 if cout > 16 else 3
+
+
+def kernel_name(nd, prec):
+    t = ["128, 128, 2, 2", "128, 64, 2, 2", "256, 32, 4, 1", "256, 16, 4, 1"][tile_of(nd.conv.out_channels)]
+    return f"conv_igemm_kernel<{'bf16' if prec == 'bf16' else 'f32'}, {t}, {nd.conv.kernel_size[0]}>"
+
+
+def cpu_baseline(args, seconds):
+    """Reference seg_video CPU loop restated by the oracle (fp32 NCHW torch CPU, batch 1)."""
+    import numpy as np
+    import torch
+
+    from drnmi.drnseg import DRNSeg
+    from drnmi.weights import synth_frames, synth_state_dict
+    from oracle import drn_oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    m = DRNSeg(args.arch, 19, pretrained=False)
+    sd = synth_state_dict(m, 0)
+    frames = synth_frames(7, 2, args.height, args.width)
+
+    def one(i):
+        x = O.preprocess_u8(frames[i % 2:i % 2 + 1])
+        lp, _, _ = O.drnseg_forward(sd, args.arch, x)
+        return torch.max(lp, 1)[1].cpu().numpy()
+
+    one(0)                                   # warm-up frame (untimed)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one(n)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and n >= 2) or n >= 64:
+            break
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": n / el, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} frames of {args.height}x{args.width} after 1 warm-up frame, batch 1, "
+                      f"oracle/drn_oracle.py fp32 NCHW torch-CPU ({threads} threads, {cpu_model})"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from drnmi import _lib
+    from drnmi.drnseg import INFO_MEAN, INFO_STD, build
+    from drnmi.roofline import MFMA_PEAK, network_roofline, node_work
+
+    model = build(args.arch, 19, seed=0, device=dev, precision=args.precision)
+    B, H, W = args.batch, args.height, args.width
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    frames = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
+    plan = model.plan(B, H, W, device=dev)
+    oh, ow = plan.out_hw
+    labels = torch.empty(B, oh, ow, dtype=torch.uint8, device=dev)
+    up_plane = model._up_plane(dev)
+    stream = _lib.stream_ptr(dev)
+    nodes = plan.packed.graph.nodes
+    works = node_work(plan)
+    dominant = DOMINANT_T.format("bf16" if args.precision == "bf16" else "f32")
+    dom_idx = {i for i, nd in enumerate(nodes) if kernel_name(nd, args.precision) == dominant}
+
+    events = []
+
+    def hook(i, nd, before):
+        if i in dom_idx:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            events.append((i, before, ev))
+
+    def step(timed):
+        plan.ingest_u8(frames, INFO_MEAN, INFO_STD, False, stream)
+        plan.run_backbone(stream, hook if (timed and not args.no_kernel_events) else None)
+        plan.head(up_plane, stream, None, labels)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = t.item()
+
+    # dominant-kernel durations from the events recorded inside the timed region
+    durs, flops = [], []
+    pend = {}
+    for i, before, ev in events:
+        if before:
+            pend[i] = ev
+        else:
+            durs.append(pend.pop(i).elapsed_time(ev) * 1e-3)
+            flops.append(works[i][1])
+    nr = network_roofline(plan)
+    total_frames = world * B * args.steps
+    out = {
+        "metric": METRIC,
+        "value": total_frames / el,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.precision,
+        "data": "synthetic uint8 RGB frames resident in HBM; hash-initialised DRN-D-22 weights (no checkpoint)",
+        "config": {"workload": f"{args.arch} dense inference, seg_video loop (uint8 frame -> uint8 labels) "
+                               f"{H}x{W}, {B} frames/GPU/step",
+                   "arch": args.arch, "height": H, "width": W, "frames_per_gpu_step": B,
+                   "global_batch": B * world, "parallelism": f"dp{world} (frames sharded, no data-path collective)"},
+    }
+    if durs:
+        avg_d = sum(durs) / len(durs)
+        avg_f = sum(flops) / len(flops)
+        ach = avg_f / avg_d / 1e12
+        peak = MFMA_PEAK[args.precision] / 1e12
+        out["roofline"] = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 2), "peak": peak,
+                           "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+                           "launches": len(durs), "avg_launch_us": round(avg_d * 1e6, 2),
+                           "avg_launch_gflop": round(avg_f / 1e9, 3)}
+    out["network_roofline"] = {"t_star_ms_per_frame": nr["t_star_s"] / B * 1e3,
+                               "measured_ms_per_frame": el / args.steps / B * 1e3,
+                               "frac": nr["t_star_s"] / (el / args.steps),
+                               "gflop_per_frame": nr["flops"] / B / 1e9, "gb_per_frame": nr["bytes"] / B / 1e9,
+                               "achieved_tflops": nr["flops"] * args.steps / el / 1e12}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

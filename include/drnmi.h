@@ -1,0 +1,118 @@
+/*
+ * drnmi.h — C-ABI of the MI355X-native DRN-D segmentation hot path.
+ *
+ * Every entry point takes device pointers, plain sizes and a hipStream_t (passed
+ * as void*), launches asynchronously on that stream and returns 0 on success or
+ * a negative drnmi_status on a rejected argument / a positive hipError_t on a
+ * launch failure.  No torch or C++ types cross this boundary; the Python host
+ * layer (drnmi/_lib.py) binds it with ctypes, and any other FFI (cgo, JNI,
+ * N-API) can bind it the same way.
+ *
+ * The reference (thejasvi-konduru/video-seg-model-compress) has no native code
+ * and no FFI: its hot path is PyTorch ATen ops called from Python.  Each entry
+ * point below names the reference code it replaces (file:line in the reference).
+ *
+ * Layouts: activations are NHWC with a power-of-two channel stride >= 8;
+ * weights are packed [cout_pad][k_pad] with k = (kh*ks + kw)*cin + ci.
+ * dtype codes: DRNMI_F32 (fp32 parity mode), DRNMI_BF16 (bf16 perf mode).
+ */
+#ifndef DRNMI_H
+#define DRNMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum drnmi_dtype { DRNMI_F32 = 0, DRNMI_BF16 = 1, DRNMI_U8 = 2, DRNMI_I64 = 3 };
+
+enum drnmi_status {
+  DRNMI_OK = 0,
+  DRNMI_EINVAL = -1,     /* bad shape / stride / dtype combination */
+  DRNMI_ENOTSUP = -2,    /* no kernel instantiated for this configuration */
+};
+
+/* One fused convolution: y = act(conv(x, w) * scale + shift [+ res]).
+ * Replaces conv3x3 + BatchNorm2d + ReLU (+ residual add) of the reference:
+ *   lmodels/drn.py:27-29   conv3x3
+ *   lmodels/drn.py:49-65   BasicBlock.forward (conv-bn-relu, conv-bn, += residual, relu)
+ *   lmodels/drn.py:86-106  Bottleneck.forward (1x1 / 3x3 / 1x1 + residual)
+ *   lmodels/drn.py:132-137 layer0 (7x7 stem) ; :181-186 downsample (1x1 stride s + BN)
+ *   lmodels/drn.py:201-211 _make_conv_layers (conv-bn-relu stacks, layer1/2/7/8)
+ *   lmodels/drnseg.py:278-284 seg (1x1 conv + bias, scale = 1, shift = bias)
+ * Output addressing: y[img*y_sn + pixel*y_sp + c*y_sc] (pixel = oh*wo + ow), so
+ * the same kernel writes NHWC activations or the NCHW fp32 logits tensor. */
+typedef struct drnmi_conv_args {
+  const void* x;       /* NHWC input [n][h][w][cin]                                   */
+  const void* wgt;     /* packed weights [cout_pad][k_pad]                            */
+  const float* scale;  /* [cout_pad] folded BN scale                                  */
+  const float* shift;  /* [cout_pad] folded BN shift (or conv bias)                   */
+  const void* res;     /* optional NHWC residual [n*ho*wo][cout] in x's dtype, or NULL */
+  void* y;             /* output                                                      */
+  int64_t y_sn, y_sp, y_sc; /* output strides in elements                          */
+  int32_t n, h, w, cin;     /* cin: channel stride of x, power of two >= 8          */
+  int32_t ho, wo, cout, cout_pad;
+  int32_t ks, stride, pad, dil;
+  int32_t k, k_pad;         /* k = ks*ks*cin ; k_pad = round_up(k, 32)              */
+  int32_t relu;             /* 1: ReLU after the (optional) residual add            */
+  int32_t dtype;            /* DRNMI_BF16 or DRNMI_F32: x, w, res                   */
+  int32_t out_dtype;        /* DRNMI_BF16 or DRNMI_F32: y                           */
+  int32_t tile;             /* tile id (drnmi_conv_tile_name), -1 = auto            */
+} drnmi_conv_args;
+
+int drnmi_conv2d_bn_act(const drnmi_conv_args* args, void* stream);
+
+/* Name of a tile configuration ("128x128", ...) or NULL; count via drnmi_conv_num_tiles. */
+const char* drnmi_conv_tile_name(int tile);
+int drnmi_conv_num_tiles(void);
+
+/* Frame ingest: uint8 HWC frames -> normalised NHWC (channel stride 8, c>=3 zero).
+ * Replaces ToTensorVideoImage + Normalize (data_transforms.py:256-281, :109-125;
+ * constants info.json:1): v = (u8 / 255 - mean[c]) / std[c] in fp32, then cast.
+ * bgr != 0 swaps channel order on read (seg_video_old_no_plot.py:125 feeds cv2's
+ * BGR frames as "RGB"; bgr = 0 reproduces that quirk when given cv2 frames). */
+/* mean3 / std3 are HOST pointers to 3 floats (passed by value to the kernel). */
+int drnmi_frame_ingest_u8(const uint8_t* frames, void* out, int32_t n, int32_t h, int32_t w,
+                          const float* mean3, const float* std3, int32_t bgr,
+                          int32_t out_dtype, void* stream);
+
+/* fp32 NCHW [n][c][h][w] -> NHWC [n][h][w][c_pad] in out_dtype, zero-filling c..c_pad-1.
+ * The boundary conversion for DRNSeg.forward(x) (lmodels/drnseg.py:295-299 takes NCHW fp32). */
+int drnmi_nchw_to_nhwc(const float* x, void* out, int32_t n, int32_t c, int32_t h, int32_t w,
+                       int32_t c_pad, int32_t out_dtype, void* stream);
+
+/* NHWC [n][h][w][c_stride] (first c channels) -> fp32 NCHW [n][c][h][w]. Debug/parity taps. */
+int drnmi_nhwc_to_nchw(const void* x, float* out, int32_t n, int32_t c, int32_t h, int32_t w,
+                       int32_t c_stride, int32_t in_dtype, void* stream);
+
+/* Fused up x8 + LogSoftmax(dim=1) + argmax over classes.
+ * Replaces the depthwise ConvTranspose2d(c, c, 16, stride 8, pad 4, groups=c) with the
+ * bilinear fill_up_weights kernel, the LogSoftmax and torch.max(final, 1):
+ *   lmodels/drnseg.py:257-266, :285-299 ; semantic_seg.py:445 ; seg_video_old_no_plot.py:166
+ * logits: fp32 NCHW [n][c][h][w]; up_w: fp32 [16][16] (one depthwise plane, all planes equal);
+ * logprobs: fp32 NCHW [n][c][8h][8w] or NULL; labels: [n][8h][8w] uint8 or int64 (label_dtype)
+ * or NULL.  Ties in argmax resolve to the lowest class index. */
+int drnmi_up8_logsoftmax_argmax(const float* logits, const float* up_w, float* logprobs,
+                                void* labels, int32_t label_dtype, int32_t n, int32_t c,
+                                int32_t h, int32_t w, void* stream);
+
+/* Multi-tensor in-place mask apply: w[t][i] *= m[t][i] for every tensor t.
+ * Replaces Pruner.apply_masks (pruners/Pruner.py:17-20, same body BlockPruner.py:27-30,
+ * SRMBRepMasker.py:20-23): one launch for all masked layers instead of one ATen mul_ per
+ * layer plus a state_dict() rebuild per layer. */
+int drnmi_mask_apply_f32(int32_t ntensors, float* const* weights, const float* const* masks,
+                         const int64_t* numels, void* stream);
+
+/* Same, with bit-packed masks: bit i of word i/32 of masks[t] keeps element i. */
+int drnmi_mask_apply_bits_f32(int32_t ntensors, float* const* weights,
+                              const uint32_t* const* mask_bits, const int64_t* numels,
+                              void* stream);
+
+/* Library version string, e.g. "drnmi 0.1.0 gfx950". */
+const char* drnmi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRNMI_H */

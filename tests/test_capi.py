@@ -1,0 +1,50 @@
+"""The C-ABI library loads without a GPU and exports every symbol include/drnmi.h declares."""
+import ctypes
+import os
+import re
+import subprocess
+
+from drnmi import _lib
+from drnmi.build import LIB_PATH, build
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "drnmi.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(drnmi_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_and_binding_agree():
+    assert declared_functions() == sorted(_lib.SIGNATURES)
+
+
+def test_library_exports_every_symbol():
+    path = build(verbose=False)
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (drnmi_[a-z0-9_]+)", out))
+    missing = set(declared_functions()) - exported
+    assert not missing, missing
+
+
+def test_library_loads_and_reports():
+    lib = _lib.load()
+    assert lib.drnmi_version().decode().startswith("drnmi ")
+    n = lib.drnmi_conv_num_tiles()
+    assert n >= 4
+    names = [lib.drnmi_conv_tile_name(i).decode() for i in range(n)]
+    assert names[0] == "128x128"
+    assert lib.drnmi_conv_tile_name(n) is None
+
+
+def test_argument_validation_without_gpu():
+    """Rejected arguments return DRNMI_EINVAL before any HIP call (safe with no device)."""
+    lib = _lib.load()
+    a = _lib.ConvArgs()
+    a.cin = 12          # not a power of two
+    assert lib.drnmi_conv2d_bn_act(ctypes.byref(a), None) == -1
+    assert lib.drnmi_conv2d_bn_act(None, None) == -1
+    assert lib.drnmi_up8_logsoftmax_argmax(None, None, None, None, 2, 1, 19, 8, 8, None) == -1
+    assert lib.drnmi_mask_apply_f32(-1, None, None, None, None) == -1
+    assert lib.drnmi_mask_apply_f32(0, None, None, None, None) == 0

@@ -1,0 +1,178 @@
+"""Per-kernel parity on the GPU: HIP kernels vs the CPU fp32 oracle (torch CPU ops).
+
+Tolerances (written here, per precision):
+  fp32 parity mode: |y - ref| <= 2e-5 * max|ref| + 1e-6   (exact-fp32 MFMA, different sum order)
+  bf16 perf mode  : reference computed on bf16-rounded operands; |y - ref| <= 1.5e-2 * max|ref|
+                    (bf16 output rounding 2^-9 plus fp32 accumulation-order differences)
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from drnmi import ops
+from oracle import drn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+CONV_CASES = [
+    # cin, cout, ks, stride, dil, h, w, residual, relu
+    (16, 16, 3, 1, 1, 37, 45, False, True),
+    (16, 32, 3, 2, 1, 40, 52, False, True),
+    (32, 64, 3, 2, 1, 33, 31, False, True),
+    (64, 64, 3, 1, 1, 20, 24, True, True),
+    (32, 64, 1, 2, 1, 33, 31, False, False),
+    (128, 256, 3, 1, 2, 16, 20, False, True),
+    (256, 256, 3, 1, 2, 12, 16, True, True),
+    (256, 512, 3, 1, 4, 16, 16, False, True),
+    (512, 512, 3, 1, 4, 11, 13, True, True),
+    (512, 512, 3, 1, 2, 16, 32, False, True),
+    (512, 19, 1, 1, 1, 16, 32, False, False),
+    (64, 256, 1, 1, 1, 15, 17, True, True),    # bottleneck conv3
+    (256, 64, 1, 1, 1, 15, 17, False, True),   # bottleneck conv1
+]
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+def _ref_conv(x, w, sc, sh, res, stride, pad, dil, relu):
+    y = F.conv2d(x, w, stride=stride, padding=pad, dilation=dil)
+    y = y * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", range(len(CONV_CASES)))
+def test_conv_bn_act(case, prec):
+    cin, cout, ks, stride, dil, h, w, has_res, relu = CONV_CASES[case]
+    n = 2
+    pad = dil * (ks // 2)
+    x = _rand((n, cin, h, w), 1 + case)
+    wt = _rand((cout, cin, ks, ks), 100 + case, (2.0 / (ks * ks * cout)) ** 0.5)
+    sc = torch.rand(cout, generator=torch.Generator().manual_seed(7)) + 0.5
+    sh = torch.rand(cout, generator=torch.Generator().manual_seed(8)) - 0.5
+    ho = (h + 2 * pad - dil * (ks - 1) - 1) // stride + 1
+    wo = (w + 2 * pad - dil * (ks - 1) - 1) // stride + 1
+    res = _rand((n, cout, ho, wo), 200 + case) if has_res else None
+    dt = torch.float32 if prec == "fp32" else torch.bfloat16
+    if prec == "bf16":
+        x, wt = x.bfloat16().float(), wt.bfloat16().float()
+        res = res.bfloat16().float() if res is not None else None
+    ref = _ref_conv(x, wt, sc, sh, res, stride, pad, dil, relu)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV, dt)
+    rd = res.permute(0, 2, 3, 1).contiguous().to(DEV, dt) if res is not None else None
+    y = ops.conv2d_bn_act(xd, wt.to(DEV), sc.to(DEV), sh.to(DEV), rd, stride, pad, dil, relu)
+    torch.cuda.synchronize()
+    got = y.float().permute(0, 3, 1, 2).cpu()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    tol = (2e-5 * scale + 1e-6) if prec == "fp32" else 1.5e-2 * scale
+    assert err <= tol, f"max err {err} (scale {scale})"
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3])
+def test_conv_all_tiles(tile):
+    n, cin, cout, h, w = 1, 64, 128, 19, 23
+    x = _rand((n, cin, h, w), 5)
+    wt = _rand((cout, cin, 3, 3), 6, 0.05)
+    ref = F.conv2d(x, wt, padding=2, dilation=2)
+    y = ops.conv2d_bn_act(x.permute(0, 2, 3, 1).contiguous().to(DEV), wt.to(DEV), padding=2, dilation=2,
+                          tile=tile)
+    got = y.permute(0, 3, 1, 2).cpu()
+    assert (got - ref).abs().max().item() <= 2e-5 * ref.abs().max().item() + 1e-6
+
+
+def test_stem_7x7_padded_input():
+    """layer0: 7x7 conv over 3 channels stored with channel stride 8 (zero pad)."""
+    x = _rand((2, 3, 41, 67), 9)
+    wt = _rand((16, 3, 7, 7), 10, 0.1)
+    ref = F.conv2d(x, wt, padding=3)
+    xd = ops.nchw_to_nhwc(x.to(DEV), 8, torch.float32)
+    y = ops.conv2d_bn_act(xd, wt.to(DEV), padding=3)
+    got = y.permute(0, 3, 1, 2).cpu()
+    assert (got - ref).abs().max().item() <= 2e-5 * ref.abs().max().item() + 1e-6
+
+
+def test_seg_conv_writes_nchw_fp32_logits():
+    x = _rand((2, 512, 9, 14), 11)
+    wt = _rand((19, 512, 1, 1), 12, 0.05)
+    b = _rand((19,), 13, 0.1)
+    ref = F.conv2d(x, wt, b)
+    y = ops.conv2d_bn_act(x.permute(0, 2, 3, 1).contiguous().to(DEV), wt.to(DEV), None, b.to(DEV),
+                          out_nchw_fp32=True)
+    assert y.shape == (2, 19, 9, 14)
+    assert (y.cpu() - ref).abs().max().item() <= 2e-5 * ref.abs().max().item() + 1e-6
+
+
+def test_frame_ingest_bit_exact(golden_forward):
+    for case in ["d22_1x64x128", "d22_1x300x300"]:
+        frames = torch.from_numpy(golden_forward[case + "/frames"]).to(DEV)
+        out = ops.frame_ingest(frames, O.INFO_MEAN, O.INFO_STD, dtype=torch.float32)
+        got = out[..., :3].permute(0, 3, 1, 2).cpu().numpy()
+        np.testing.assert_array_equal(got, golden_forward[case + "/input"])
+        assert torch.count_nonzero(out[..., 3:]).item() == 0
+
+
+def test_frame_ingest_bgr_swap():
+    fr = torch.randint(0, 256, (1, 5, 7, 3), dtype=torch.uint8)
+    a = ops.frame_ingest(fr.to(DEV), O.INFO_MEAN, O.INFO_STD, bgr=True)
+    b = ops.frame_ingest(fr.flip(-1).contiguous().to(DEV), O.INFO_MEAN, O.INFO_STD, bgr=False)
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("h,w", [(8, 16), (38, 38), (5, 3), (1, 1)])
+def test_up8_logsoftmax_argmax(h, w):
+    from drnmi.weights import bilinear_up_kernel
+    c = 19
+    logits = _rand((2, c, h, w), 21, 3.0)
+    upw = torch.from_numpy(bilinear_up_kernel(16))
+    sd = {"up.weight": upw.expand(c, 1, 16, 16).contiguous()}
+    ref = O.up_logsoftmax(sd, logits)
+    lp, lab = ops.up8_logsoftmax_argmax(logits.to(DEV), upw.to(DEV))
+    assert lp.shape == ref.shape
+    assert (lp.cpu() - ref).abs().max().item() <= 2e-5
+    ref_lab = O.labels_of(ref)
+    srt = ref.sort(dim=1).values
+    margin = srt[:, -1] - srt[:, -2]
+    diff = lab.cpu() != ref_lab
+    assert not bool((diff & (margin > 1e-5)).any())
+    _, lab8 = ops.up8_logsoftmax_argmax(logits.to(DEV), upw.to(DEV), want_logprobs=False,
+                                        label_dtype=torch.uint8)
+    assert torch.equal(lab8.cpu().long(), lab.cpu())
+
+
+@pytest.mark.parametrize("use_bits", [False, True])
+def test_mask_apply_bit_exact(use_bits, tmp_path):
+    """Pruner.apply_masks through the HIP kernel == w * m on the CPU, bit for bit (incl. -0.0)."""
+    import json
+    from drnmi import pruners as P
+    from drnmi.drnseg import DRNSeg
+    from drnmi.weights import synth_state_dict
+    m = DRNSeg("drn_d_22", 19, pretrained=False)
+    m.load_state_dict(synth_state_dict(m, 0))
+    layers = ["layer.0.0.weight", "layer.3.0.conv2.weight", "layer.6.1.conv2.weight", "seg.weight"]
+    cfg = {"pruner_type": "block", "configs": [{"layer_set": layers, "sparsity": 0.5, "block_height": 4,
+           "block_width": 4, "sub_rows": -1, "sub_cols": -1, "collapse_tensor": True}]}
+    jp = tmp_path / "c.json"
+    jp.write_text(json.dumps(cfg))
+    pr = P.BlockPruner(str(jp), on_gpu=True)
+    pr.generate_masks(m)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    ref = O.apply_masks({k: before[k] for k in layers}, {k: pr.mask_dict[k].cpu() for k in layers})
+    m = m.to(DEV)
+    pr.apply_masks(m, use_bits=use_bits)
+    torch.cuda.synchronize()
+    sd = m.state_dict()
+    for k in layers:
+        a = sd[k].cpu().view(torch.int32)
+        b = ref[k].contiguous().view(torch.int32)
+        assert torch.equal(a, b), k
+    for k, v in before.items():
+        if k not in layers:
+            assert torch.equal(sd[k].cpu(), v), k

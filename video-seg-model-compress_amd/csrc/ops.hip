@@ -1,0 +1,350 @@
+// HBM-bound kernels around the convolutions:
+//   * frame ingest (u8 HWC -> normalised NHWC8)      data_transforms.py:109-125, :256-281
+//   * NCHW fp32 -> NHWC boundary conversion          lmodels/drnseg.py:295-299 input
+//   * fused up x8 + LogSoftmax + argmax             lmodels/drnseg.py:257-299, semantic_seg.py:445
+//   * multi-tensor mask apply (float / bit masks)    pruners/Pruner.py:17-20
+#include "common.h"
+
+namespace drnmi {
+namespace {
+
+template <typename T>
+__device__ __forceinline__ T from_f32(float v);
+template <>
+__device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <>
+__device__ __forceinline__ bf16_t from_f32<bf16_t>(float v) { return f32_to_bf16(v); }
+
+// ---------------------------------------------------------------- frame ingest
+// One thread per pixel: 3 bytes in, 8 channels out (16 B bf16 / 32 B fp32).
+template <typename T>
+__global__ void __launch_bounds__(256)
+frame_ingest_kernel(const uint8_t* __restrict__ frames, T* __restrict__ out, int64_t npix,
+                    float m0, float m1, float m2, float s0, float s1, float s2, int bgr) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= npix) return;
+  const uint8_t* px = frames + i * 3;
+  float c0 = static_cast<float>(px[0]);
+  float c1 = static_cast<float>(px[1]);
+  float c2 = static_cast<float>(px[2]);
+  if (bgr) { const float t = c0; c0 = c2; c2 = t; }
+  // Same fp32 op sequence as ToTensorVideoImage (x / 255) then Normalize (sub_, div_).
+  const float v0 = (c0 / 255.0f - m0) / s0;
+  const float v1 = (c1 / 255.0f - m1) / s1;
+  const float v2 = (c2 / 255.0f - m2) / s2;
+  T* o = out + i * 8;
+  Vec8<T> r = Vec8<T>::zero();
+  T tmp[8] = {from_f32<T>(v0), from_f32<T>(v1), from_f32<T>(v2), T(0), T(0), T(0), T(0), T(0)};
+  r = Vec8<T>::load(tmp);
+  r.store(o);
+}
+
+// ---------------------------------------------------------------- layout conversion
+template <typename T>
+__global__ void __launch_bounds__(256)
+nchw_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ out, int c, int64_t hw,
+                    int c_pad, int64_t total_pix) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= total_pix) return;
+  const int64_t n = i / hw;
+  const int64_t q = i - n * hw;
+  const float* src = x + n * c * hw + q;
+  T* dst = out + i * c_pad;
+  for (int ch = 0; ch < c_pad; ++ch) {
+    dst[ch] = ch < c ? from_f32<T>(src[ch * hw]) : T(0);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+nhwc_to_nchw_kernel(const T* __restrict__ x, float* __restrict__ out, int c, int64_t hw,
+                    int c_stride, int64_t total) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= total) return;  // i indexes the NCHW output
+  const int64_t n = i / (c * hw);
+  const int64_t r = i - n * c * hw;
+  const int64_t ch = r / hw;
+  const int64_t q = r - ch * hw;
+  out[i] = Elem<T>::to_f32(x[(n * hw + q) * c_stride + ch]);
+}
+
+// ---------------------------------------------------------------- up x8 + log-softmax + argmax
+// Output pixel (oy, ox) of ConvTranspose2d(k16, s8, p4) receives input rows
+// i1 = (oy+4)>>3 (tap ky = oy+4-8*i1 in [0,8)) and i0 = i1-1 (tap ky+8), likewise for
+// columns: 4 taps per class.  The 16x16 kernel is shared by every class plane
+// (fill_up_weights copies plane 0 into all planes, lmodels/drnseg.py:265-266).
+constexpr int kMaxClasses = 32;
+
+template <int LABEL_DTYPE>
+__global__ void __launch_bounds__(256)
+up8_lsm_kernel(const float* __restrict__ logits, const float* __restrict__ up_w,
+               float* __restrict__ logprobs, void* __restrict__ labels, int c, int h, int w) {
+  __shared__ float wk[256];
+  wk[threadIdx.x] = up_w[threadIdx.x];
+  __syncthreads();
+
+  const int H = h * 8, W = w * 8;
+  const int ox = blockIdx.x * blockDim.x + threadIdx.x;
+  const int oy = blockIdx.y;
+  const int n = blockIdx.z;
+  if (ox >= W) return;
+
+  const int i1 = (oy + 4) >> 3, i0 = i1 - 1;
+  const int ky1 = oy + 4 - 8 * i1, ky0 = ky1 + 8;
+  const int j1 = (ox + 4) >> 3, j0 = j1 - 1;
+  const int kx1 = ox + 4 - 8 * j1, kx0 = kx1 + 8;
+  const bool vi0 = i0 >= 0, vi1 = i1 < h, vj0 = j0 >= 0, vj1 = j1 < w;
+  const float w00 = (vi0 && vj0) ? wk[ky0 * 16 + kx0] : 0.f;
+  const float w01 = (vi0 && vj1) ? wk[ky0 * 16 + kx1] : 0.f;
+  const float w10 = (vi1 && vj0) ? wk[ky1 * 16 + kx0] : 0.f;
+  const float w11 = (vi1 && vj1) ? wk[ky1 * 16 + kx1] : 0.f;
+  const int ci0 = vi0 ? i0 : 0, ci1 = vi1 ? i1 : 0, cj0 = vj0 ? j0 : 0, cj1 = vj1 ? j1 : 0;
+
+  const int64_t plane = static_cast<int64_t>(h) * w;
+  const float* src = logits + static_cast<int64_t>(n) * c * plane;
+  float v[kMaxClasses];
+  float vmax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kMaxClasses; ++k) {
+    if (k < c) {
+      const float* s = src + k * plane;
+      float a = s[ci0 * w + cj0] * w00;
+      a = fmaf(s[ci0 * w + cj1], w01, a);
+      a = fmaf(s[ci1 * w + cj0], w10, a);
+      a = fmaf(s[ci1 * w + cj1], w11, a);
+      v[k] = a;
+      vmax = fmaxf(vmax, a);
+    }
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxClasses; ++k) {
+    if (k < c) sum += expf(v[k] - vmax);
+  }
+  const float lse = logf(sum);
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int64_t pix = static_cast<int64_t>(oy) * W + ox;
+  float best = -INFINITY;
+  int arg = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxClasses; ++k) {
+    if (k < c) {
+      const float lp = (v[k] - vmax) - lse;
+      if (logprobs != nullptr) logprobs[(static_cast<int64_t>(n) * c + k) * HW + pix] = lp;
+      if (lp > best) { best = lp; arg = k; }
+    }
+  }
+  if (labels != nullptr) {
+    if (LABEL_DTYPE == DRNMI_U8) {
+      reinterpret_cast<uint8_t*>(labels)[static_cast<int64_t>(n) * HW + pix] = static_cast<uint8_t>(arg);
+    } else {
+      reinterpret_cast<int64_t*>(labels)[static_cast<int64_t>(n) * HW + pix] = arg;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- mask apply
+constexpr int kMaskBatch = 32;
+
+struct MaskBatchF32 {
+  float* w[kMaskBatch];
+  const float* m[kMaskBatch];
+  int64_t numel[kMaskBatch];
+};
+
+struct MaskBatchBits {
+  float* w[kMaskBatch];
+  const uint32_t* m[kMaskBatch];
+  int64_t numel[kMaskBatch];
+};
+
+// blockIdx.y = tensor; grid-stride over float4 groups, scalar tail.
+__global__ void __launch_bounds__(256) mask_apply_f32_kernel(const MaskBatchF32 b) {
+  const int t = blockIdx.y;
+  float* __restrict__ w = b.w[t];
+  const float* __restrict__ m = b.m[t];
+  const int64_t n = b.numel[t];
+  const int64_t n4 = n >> 2;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 wv = reinterpret_cast<float4*>(w)[i];
+    const float4 mv = reinterpret_cast<const float4*>(m)[i];
+    wv.x *= mv.x; wv.y *= mv.y; wv.z *= mv.z; wv.w *= mv.w;
+    reinterpret_cast<float4*>(w)[i] = wv;
+  }
+  if (blockIdx.x == 0) {
+    for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += blockDim.x) w[i] *= m[i];
+  }
+}
+
+// One thread per 32-element group: one mask word, 8 float4 loads/stores.  The multiply
+// by 1.0f / 0.0f keeps the reference's exact result (including -0.0 for negative w).
+__global__ void __launch_bounds__(256) mask_apply_bits_kernel(const MaskBatchBits b) {
+  const int t = blockIdx.y;
+  float* __restrict__ w = b.w[t];
+  const uint32_t* __restrict__ m = b.m[t];
+  const int64_t n = b.numel[t];
+  const int64_t groups = (n + 31) >> 5;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < groups; g += stride) {
+    const uint32_t bits = m[g];
+    const int64_t e0 = g << 5;
+    if (e0 + 32 <= n) {
+      float4* p = reinterpret_cast<float4*>(w + e0);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float4 v = p[q];
+        v.x *= static_cast<float>((bits >> (4 * q + 0)) & 1u);
+        v.y *= static_cast<float>((bits >> (4 * q + 1)) & 1u);
+        v.z *= static_cast<float>((bits >> (4 * q + 2)) & 1u);
+        v.w *= static_cast<float>((bits >> (4 * q + 3)) & 1u);
+        p[q] = v;
+      }
+    } else {
+      for (int q = 0; e0 + q < n; ++q) w[e0 + q] *= static_cast<float>((bits >> q) & 1u);
+    }
+  }
+}
+
+inline unsigned grid1d(int64_t n, int block = 256) {
+  return static_cast<unsigned>((n + block - 1) / block);
+}
+
+}  // namespace
+}  // namespace drnmi
+
+using namespace drnmi;
+
+extern "C" int drnmi_frame_ingest_u8(const uint8_t* frames, void* out, int32_t n, int32_t h, int32_t w,
+                                     const float* mean3, const float* std3, int32_t bgr,
+                                     int32_t out_dtype, void* stream) {
+  if (frames == nullptr || out == nullptr || mean3 == nullptr || std3 == nullptr) return DRNMI_EINVAL;
+  if (n <= 0 || h <= 0 || w <= 0) return DRNMI_EINVAL;
+  const int64_t npix = static_cast<int64_t>(n) * h * w;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (out_dtype == DRNMI_BF16) {
+    hipLaunchKernelGGL(frame_ingest_kernel<bf16_t>, dim3(grid1d(npix)), dim3(256), 0, s, frames,
+                       reinterpret_cast<bf16_t*>(out), npix, mean3[0], mean3[1], mean3[2], std3[0],
+                       std3[1], std3[2], bgr);
+  } else if (out_dtype == DRNMI_F32) {
+    hipLaunchKernelGGL(frame_ingest_kernel<float>, dim3(grid1d(npix)), dim3(256), 0, s, frames,
+                       reinterpret_cast<float*>(out), npix, mean3[0], mean3[1], mean3[2], std3[0],
+                       std3[1], std3[2], bgr);
+  } else {
+    return DRNMI_EINVAL;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_nchw_to_nhwc(const float* x, void* out, int32_t n, int32_t c, int32_t h, int32_t w,
+                                  int32_t c_pad, int32_t out_dtype, void* stream) {
+  if (x == nullptr || out == nullptr || n <= 0 || c <= 0 || h <= 0 || w <= 0 || c_pad < c) return DRNMI_EINVAL;
+  const int64_t hw = static_cast<int64_t>(h) * w;
+  const int64_t total = static_cast<int64_t>(n) * hw;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (out_dtype == DRNMI_BF16) {
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, s, x,
+                       reinterpret_cast<bf16_t*>(out), c, hw, c_pad, total);
+  } else if (out_dtype == DRNMI_F32) {
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid1d(total)), dim3(256), 0, s, x,
+                       reinterpret_cast<float*>(out), c, hw, c_pad, total);
+  } else {
+    return DRNMI_EINVAL;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_nhwc_to_nchw(const void* x, float* out, int32_t n, int32_t c, int32_t h, int32_t w,
+                                  int32_t c_stride, int32_t in_dtype, void* stream) {
+  if (x == nullptr || out == nullptr || n <= 0 || c <= 0 || h <= 0 || w <= 0 || c_stride < c) return DRNMI_EINVAL;
+  const int64_t hw = static_cast<int64_t>(h) * w;
+  const int64_t total = static_cast<int64_t>(n) * c * hw;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (in_dtype == DRNMI_BF16) {
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, s,
+                       reinterpret_cast<const bf16_t*>(x), out, c, hw, c_stride, total);
+  } else if (in_dtype == DRNMI_F32) {
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, dim3(grid1d(total)), dim3(256), 0, s,
+                       reinterpret_cast<const float*>(x), out, c, hw, c_stride, total);
+  } else {
+    return DRNMI_EINVAL;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_up8_logsoftmax_argmax(const float* logits, const float* up_w, float* logprobs,
+                                           void* labels, int32_t label_dtype, int32_t n, int32_t c,
+                                           int32_t h, int32_t w, void* stream) {
+  if (logits == nullptr || up_w == nullptr || n <= 0 || h <= 0 || w <= 0) return DRNMI_EINVAL;
+  if (c <= 0 || c > kMaxClasses) return DRNMI_ENOTSUP;
+  if (labels != nullptr && label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64) return DRNMI_EINVAL;
+  if (static_cast<int64_t>(h) * 8 > 65535 || n > 65535) return DRNMI_EINVAL;
+  const int W = w * 8;
+  dim3 grid(static_cast<unsigned>((W + 255) / 256), static_cast<unsigned>(h * 8), static_cast<unsigned>(n));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (label_dtype == DRNMI_I64) {
+    hipLaunchKernelGGL(up8_lsm_kernel<DRNMI_I64>, grid, dim3(256), 0, s, logits, up_w, logprobs, labels, c, h, w);
+  } else {
+    hipLaunchKernelGGL(up8_lsm_kernel<DRNMI_U8>, grid, dim3(256), 0, s, logits, up_w, logprobs, labels, c, h, w);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_mask_apply_f32(int32_t ntensors, float* const* weights, const float* const* masks,
+                                    const int64_t* numels, void* stream) {
+  if (ntensors < 0 || (ntensors > 0 && (weights == nullptr || masks == nullptr || numels == nullptr)))
+    return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (int t0 = 0; t0 < ntensors; t0 += kMaskBatch) {
+    MaskBatchF32 b{};
+    const int cnt = ntensors - t0 < kMaskBatch ? ntensors - t0 : kMaskBatch;
+    int64_t maxn = 0;
+    for (int i = 0; i < cnt; ++i) {
+      b.w[i] = weights[t0 + i];
+      b.m[i] = masks[t0 + i];
+      b.numel[i] = numels[t0 + i];
+      if (b.numel[i] < 0) return DRNMI_EINVAL;
+      if (b.numel[i] > 0 && (b.w[i] == nullptr || b.m[i] == nullptr)) return DRNMI_EINVAL;
+      if ((reinterpret_cast<uintptr_t>(b.w[i]) | reinterpret_cast<uintptr_t>(b.m[i])) & 15) return DRNMI_EINVAL;
+      maxn = b.numel[i] > maxn ? b.numel[i] : maxn;
+    }
+    if (maxn == 0) continue;
+    unsigned gx = grid1d((maxn + 3) / 4);
+    gx = gx > 1024 ? 1024 : (gx == 0 ? 1 : gx);
+    hipLaunchKernelGGL(mask_apply_f32_kernel, dim3(gx, cnt), dim3(256), 0, s, b);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  return DRNMI_OK;
+}
+
+extern "C" int drnmi_mask_apply_bits_f32(int32_t ntensors, float* const* weights,
+                                         const uint32_t* const* mask_bits, const int64_t* numels,
+                                         void* stream) {
+  if (ntensors < 0 || (ntensors > 0 && (weights == nullptr || mask_bits == nullptr || numels == nullptr)))
+    return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (int t0 = 0; t0 < ntensors; t0 += kMaskBatch) {
+    MaskBatchBits b{};
+    const int cnt = ntensors - t0 < kMaskBatch ? ntensors - t0 : kMaskBatch;
+    int64_t maxn = 0;
+    for (int i = 0; i < cnt; ++i) {
+      b.w[i] = weights[t0 + i];
+      b.m[i] = mask_bits[t0 + i];
+      b.numel[i] = numels[t0 + i];
+      if (b.numel[i] < 0) return DRNMI_EINVAL;
+      if (b.numel[i] > 0 && (b.w[i] == nullptr || b.m[i] == nullptr)) return DRNMI_EINVAL;
+      if (reinterpret_cast<uintptr_t>(b.w[i]) & 15) return DRNMI_EINVAL;
+      maxn = b.numel[i] > maxn ? b.numel[i] : maxn;
+    }
+    if (maxn == 0) continue;
+    unsigned gx = grid1d((maxn + 31) / 32);
+    gx = gx > 1024 ? 1024 : (gx == 0 ? 1 : gx);
+    hipLaunchKernelGGL(mask_apply_bits_kernel, dim3(gx, cnt), dim3(256), 0, s, b);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  return DRNMI_OK;
+}
+
+extern "C" const char* drnmi_version(void) { return "drnmi 0.1.0 gfx950"; }

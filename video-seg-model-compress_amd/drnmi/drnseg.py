@@ -1,0 +1,207 @@
+"""DRNSeg — drop-in for the reference segmentation module, run on HIP kernels.
+
+Reference API (kept): semantic_seg.py:126-164 / lmodels/drnseg.py:268-305
+  DRNSeg(model_name, classes, pretrained_model=None, pretrained=True, use_torch_up=False)
+  forward(x: fp32 [B,3,H,W]) -> (log_probs fp32 [B,C,8h,8w], logits fp32 [B,C,h,w])
+  optim_parameters()  -> layer + seg params (up excluded)
+  state_dict keys     layer.{0..8}.*, seg.weight, seg.bias, up.weight
+                      (load_state_dict also accepts the seg_video "base." prefix,
+                       log.txt:18-170, and a DataParallel/DDP "module." prefix)
+
+Differences by design:
+  * forward runs the fused HIP plan (drnmi.engine) on a ROCm device.  It never falls
+    back to ATen; on CPU, or in train mode, it raises.
+  * precision: "fp32" (default; the reference's arithmetic, parity mode, exact-fp32
+    MFMA) or "bf16" (perf mode, fp32 accumulation) via set_precision().
+  * segment(frames_u8) is the fused seg_video path (seg_video_old_no_plot.py:157-169:
+    normalise -> model(img)[0] -> torch.max(final, 1)) producing uint8 labels without
+    materialising the 19-plane log-prob tensor.
+  * model_name is honoured (lmodels/drnseg.py:272 always builds D-22; semantic_seg.py
+    :130-131 builds model_name — we follow the driver copy).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+
+import torch
+import torch.nn as nn
+
+from . import _lib, drn
+from .engine import PackedNet, Plan, lower_drnseg
+from .weights import bilinear_up_kernel
+
+# info.json:1 (Cityscapes normalisation used by every reference driver)
+INFO_MEAN = (0.29010095242892997, 0.32808144844279574, 0.28696394422942517)
+INFO_STD = (0.1829540508368939, 0.18656561047509476, 0.18447508988480435)
+
+
+def fill_up_weights(up: nn.ConvTranspose2d) -> None:
+    """Bilinear kernel into every depthwise plane (lmodels/drnseg.py:257-266)."""
+    k = up.weight.shape[2]
+    w = torch.from_numpy(bilinear_up_kernel(k))
+    with torch.no_grad():
+        up.weight.copy_(w.expand_as(up.weight))
+
+
+class DRNSeg(nn.Module):
+    def __init__(self, model_name, classes, pretrained_model=None, pretrained=True,
+                 use_torch_up=False):
+        super().__init__()
+        if use_torch_up:
+            raise NotImplementedError(
+                "use_torch_up=True (nn.UpsamplingBilinear2d) is not on the north-star path; "
+                "the fused kernel implements the ConvTranspose2d 'up' (lmodels/drnseg.py:288-293)")
+        factory = getattr(drn, model_name, None)
+        if factory is None:
+            raise KeyError(f"unknown model {model_name!r}; known: {drn.ARCHS}")
+        model = factory(pretrained=pretrained, num_classes=1000)
+        if pretrained_model is not None:
+            model.load_state_dict(pretrained_model)
+        self.layer = nn.Sequential(*list(model.children())[:-2])
+        self.seg = nn.Conv2d(model.out_dim, classes, kernel_size=1, bias=True)
+        self.softmax = nn.LogSoftmax(dim=1)
+        n = self.seg.kernel_size[0] * self.seg.kernel_size[1] * self.seg.out_channels
+        self.seg.weight.data.normal_(0, math.sqrt(2.0 / n))
+        self.seg.bias.data.zero_()
+        up = nn.ConvTranspose2d(classes, classes, 16, stride=8, padding=4, output_padding=0,
+                                groups=classes, bias=False)
+        fill_up_weights(up)
+        up.weight.requires_grad = False
+        self.up = up
+        self.model_name = model_name
+        self.classes = classes
+        self.precision = "fp32"
+        self._graph = lower_drnseg(self.layer, self.seg)
+        self._packed = {}
+        self._plans = {}
+        self._pack_key = None
+
+    # ----------------------------------------------------------------- reference API
+    def optim_parameters(self, memo=None):
+        for param in self.layer.parameters():
+            yield param
+        for param in self.seg.parameters():
+            yield param
+
+    def forward(self, x: torch.Tensor):
+        plan, stream = self._prepare(x.shape[0], x.shape[2], x.shape[3], x.device)
+        if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError("DRNSeg.forward expects fp32 [B,3,H,W]")
+        x = x.contiguous()
+        plan.ingest_nchw(x, stream)
+        plan.run_backbone(stream)
+        oh, ow = plan.out_hw
+        logprobs = torch.empty(x.shape[0], self.classes, oh, ow, dtype=torch.float32, device=x.device)
+        plan.head(self._up_plane(x.device), stream, logprobs, None)
+        logits = plan.bufs["logits"].clone()
+        return logprobs, logits
+
+    # ----------------------------------------------------------------- fused paths
+    def predict(self, x: torch.Tensor) -> torch.Tensor:
+        """torch.max(model(x)[0], 1)[1] (semantic_seg.py:444-445) as one fused pass: int64 labels."""
+        plan, stream = self._prepare(x.shape[0], x.shape[2], x.shape[3], x.device)
+        plan.ingest_nchw(x.contiguous(), stream)
+        plan.run_backbone(stream)
+        oh, ow = plan.out_hw
+        labels = torch.empty(x.shape[0], oh, ow, dtype=torch.int64, device=x.device)
+        plan.head(self._up_plane(x.device), stream, None, labels)
+        return labels
+
+    def segment(self, frames_u8: torch.Tensor, mean=INFO_MEAN, std=INFO_STD, bgr: bool = False,
+                labels: torch.Tensor | None = None) -> torch.Tensor:
+        """Video path: uint8 HWC frames [B,H,W,3] on the GPU -> uint8 label maps [B,8h,8w].
+
+        Fuses ToTensorVideoImage + Normalize (data_transforms.py:256-281, :109-125) into the
+        ingest kernel and model(img)[0] + torch.max(final,1) into the head kernel."""
+        if frames_u8.dtype != torch.uint8 or frames_u8.dim() != 4 or frames_u8.shape[3] != 3:
+            raise ValueError("segment expects uint8 [B,H,W,3] frames")
+        plan, stream = self._prepare(frames_u8.shape[0], frames_u8.shape[1], frames_u8.shape[2],
+                                     frames_u8.device)
+        plan.ingest_u8(frames_u8.contiguous(), mean, std, bgr, stream)
+        plan.run_backbone(stream)
+        oh, ow = plan.out_hw
+        if labels is None:
+            labels = torch.empty(frames_u8.shape[0], oh, ow, dtype=torch.uint8, device=frames_u8.device)
+        plan.head(self._up_plane(frames_u8.device), stream, None, labels)
+        return labels
+
+    # ----------------------------------------------------------------- configuration
+    def set_precision(self, precision: str) -> "DRNSeg":
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
+        self.precision = precision
+        return self
+
+    def plan(self, n, h, w, device=None, keep_all=False) -> Plan:
+        device = device or next(self.parameters()).device
+        plan, _ = self._prepare(n, h, w, torch.device(device), keep_all=keep_all)
+        return plan
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        fixed = {}
+        for k, v in state_dict.items():
+            if k.startswith("module."):
+                k = k[len("module."):]
+            if k.startswith("base."):
+                k = "layer." + k[len("base."):]
+            fixed[k] = v
+        return super().load_state_dict(fixed, strict=strict, assign=assign)
+
+    # ----------------------------------------------------------------- internals
+    def _up_plane(self, device):
+        return self.up.weight[0, 0].detach().to(device, torch.float32).contiguous()
+
+    def _state_key(self):
+        key = [self.precision]
+        for t in list(self.parameters()) + list(self.buffers()):
+            key.append((t.data_ptr(), t._version, str(t.device)))
+        return tuple(key)
+
+    def _prepare(self, n, h, w, device, keep_all=False):
+        if device.type != "cuda":
+            raise RuntimeError("drnmi.DRNSeg runs on the HIP engine only: move the model and input "
+                               "to a ROCm device (no CPU fallback by design)")
+        if self.training:
+            raise NotImplementedError("train-mode forward (batch-stat BN + autograd) is the "
+                                      "fine-tune path, not built yet; call .eval()")
+        _lib.load()
+        key = self._state_key()
+        if key != self._pack_key:
+            if self.precision in self._packed:
+                self._packed[self.precision].pack()
+                for (p, *_), plan in self._plans.items():
+                    if p == self.precision:
+                        plan.refresh_weight_ptrs()
+            self._pack_key = key
+        pk = self._packed.get(self.precision)
+        if pk is None:
+            pk = PackedNet(self._graph, self.precision, device)
+            self._packed[self.precision] = pk
+        pkey = (self.precision, n, h, w, keep_all)
+        plan = self._plans.get(pkey)
+        if plan is None:
+            plan = Plan(pk, n, h, w, keep_all=keep_all)
+            self._plans[pkey] = plan
+        return plan, _lib.stream_ptr(device)
+
+
+def load_info(path: str):
+    with open(path) as f:
+        info = json.load(f)
+    return tuple(info["mean"]), tuple(info["std"])
+
+
+def build(model_name: str = "drn_d_22", classes: int = 19, seed: int | None = 0, device="cuda",
+          precision: str = "fp32") -> DRNSeg:
+    """DRNSeg with hash-initialised weights (drnmi.weights), in eval mode, on `device`."""
+    from .weights import synth_state_dict
+    m = DRNSeg(model_name, classes, pretrained=False)
+    if seed is not None:
+        m.load_state_dict(synth_state_dict(m, seed))
+    return m.to(device).eval().set_precision(precision)
+
+
+__all__ = ["DRNSeg", "fill_up_weights", "build", "INFO_MEAN", "INFO_STD", "load_info",
+           "os"]

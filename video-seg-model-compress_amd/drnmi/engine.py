@@ -1,0 +1,339 @@
+"""Execution engine: packs a DRN-D + seg head into HIP-kernel launch plans.
+
+The reference runs DRNSeg.forward as ~70 ATen ops per frame (lmodels/drnseg.py:
+295-299 -> lmodels/drn.py:213-259).  Here the same network is lowered once into a
+list of fused launches on the C-ABI (include/drnmi.h):
+
+  ingest / NCHW->NHWC  -> stem conv7x7+BN+ReLU -> conv3x3+BN+ReLU ... ->
+  [block: conv+BN+ReLU, (1x1 downsample+BN), conv+BN+residual+ReLU] ... ->
+  seg 1x1+bias (fp32 NCHW logits) -> up x8 + log-softmax + argmax
+
+Activations are NHWC in HBM (channel stride = a power of two >= 8), in bf16 (perf
+mode) or fp32 (parity mode).  BN is folded into per-channel scale/shift applied in
+the conv epilogue (eval semantics, lmodels/drn.py:7 BatchNorm2d in .eval()).
+Weights are re-packed lazily whenever any parameter/buffer changes (tracked by the
+tensors' version counters), so Pruner.apply_masks or a load_state_dict is picked up.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .drn import BasicBlock, Bottleneck
+
+BN_EPS_DEFAULT = 1e-5
+K_ALIGN = 32
+COUT_ALIGN = 128
+
+DTYPES = {"fp32": (torch.float32, _lib.DRNMI_F32), "bf16": (torch.bfloat16, _lib.DRNMI_BF16)}
+
+
+def _pow2_at_least(c: int, lo: int = 8) -> int:
+    p = lo
+    while p < c:
+        p *= 2
+    return p
+
+
+def _round_up(v: int, a: int) -> int:
+    return (v + a - 1) // a * a
+
+
+@dataclass
+class ConvNode:
+    """One fused conv launch: y = act(conv(x) * scale + shift [+ res])."""
+    name: str                    # state_dict prefix of the conv weight (e.g. "layer.3.0.conv1")
+    conv: nn.Conv2d
+    bn: nn.BatchNorm2d | None    # None -> bias (seg) or identity scale
+    src: str                     # value names in the plan
+    dst: str
+    res: str | None = None
+    relu: bool = True
+    out_fp32_nchw: bool = False  # seg logits
+    cin_stride: int = 0          # filled by packing
+    # packed device tensors
+    wpk: torch.Tensor | None = None
+    scale: torch.Tensor | None = None
+    shift: torch.Tensor | None = None
+    k: int = 0
+    k_pad: int = 0
+    cout_pad: int = 0
+
+
+@dataclass
+class Graph:
+    nodes: list = field(default_factory=list)
+    stage_outputs: dict = field(default_factory=dict)   # "layer0".."layer8" -> value name
+    channels: dict = field(default_factory=dict)        # value -> logical channels
+
+
+def lower_drnseg(layer: nn.Sequential, seg: nn.Conv2d, prefix: str = "layer") -> Graph:
+    """Walk DRNSeg.layer (= DRN children[:-2]) and emit ConvNodes.
+
+    Follows lmodels/drn.py forward order (:213-259): layer0 .. layer8, with
+    BasicBlock (:49-65) / Bottleneck (:86-106) residual structure."""
+    g = Graph()
+    cur = "input"
+    g.channels[cur] = 3
+    vid = [0]
+
+    def new(c):
+        vid[0] += 1
+        name = f"v{vid[0]}"
+        g.channels[name] = c
+        return name
+
+    for li, stage in enumerate(layer):
+        sname = f"{prefix}.{li}"
+        mods = list(stage)
+        if mods and isinstance(mods[0], nn.Conv2d):
+            # conv-bn-relu triples (layer0 stem, _make_conv_layers)
+            for j in range(0, len(mods), 3):
+                conv, bn = mods[j], mods[j + 1]
+                dst = new(conv.out_channels)
+                g.nodes.append(ConvNode(f"{sname}.{j}", conv, bn, cur, dst, relu=True))
+                cur = dst
+        else:
+            for bi, blk in enumerate(mods):
+                bname = f"{sname}.{bi}"
+                if isinstance(blk, BasicBlock) or type(blk).__name__ == "BasicBlock":
+                    t = new(blk.conv1.out_channels)
+                    g.nodes.append(ConvNode(f"{bname}.conv1", blk.conv1, blk.bn1, cur, t, relu=True))
+                    res = None
+                    if blk.residual:
+                        res = cur
+                        if blk.downsample is not None:
+                            res = new(blk.downsample[0].out_channels)
+                            g.nodes.append(ConvNode(f"{bname}.downsample.0", blk.downsample[0],
+                                                    blk.downsample[1], cur, res, relu=False))
+                    out = new(blk.conv2.out_channels)
+                    g.nodes.append(ConvNode(f"{bname}.conv2", blk.conv2, blk.bn2, t, out, res=res, relu=True))
+                    cur = out
+                elif isinstance(blk, Bottleneck) or type(blk).__name__ == "Bottleneck":
+                    t1 = new(blk.conv1.out_channels)
+                    g.nodes.append(ConvNode(f"{bname}.conv1", blk.conv1, blk.bn1, cur, t1, relu=True))
+                    t2 = new(blk.conv2.out_channels)
+                    g.nodes.append(ConvNode(f"{bname}.conv2", blk.conv2, blk.bn2, t1, t2, relu=True))
+                    res = cur
+                    if blk.downsample is not None:
+                        res = new(blk.downsample[0].out_channels)
+                        g.nodes.append(ConvNode(f"{bname}.downsample.0", blk.downsample[0],
+                                                blk.downsample[1], cur, res, relu=False))
+                    out = new(blk.conv3.out_channels)
+                    g.nodes.append(ConvNode(f"{bname}.conv3", blk.conv3, blk.bn3, t2, out, res=res, relu=True))
+                    cur = out
+                else:
+                    raise TypeError(f"unsupported block {type(blk)} at {bname}")
+        g.stage_outputs[f"layer{li}"] = cur
+    logits = "logits"
+    g.channels[logits] = seg.out_channels
+    g.nodes.append(ConvNode("seg", seg, None, cur, logits, relu=False, out_fp32_nchw=True))
+    return g
+
+
+def _fold_bn(bn: nn.BatchNorm2d):
+    """Eval-mode BatchNorm as y = x*scale + shift (lmodels/drn.py:7)."""
+    invstd = torch.rsqrt(bn.running_var.float() + bn.eps)
+    w = bn.weight.float() if bn.weight is not None else torch.ones_like(invstd)
+    b = bn.bias.float() if bn.bias is not None else torch.zeros_like(invstd)
+    scale = w * invstd
+    shift = b - bn.running_mean.float() * scale
+    return scale, shift
+
+
+class PackedNet:
+    """Device-resident packed weights for one precision."""
+
+    def __init__(self, graph: Graph, precision: str, device):
+        self.graph = graph
+        self.precision = precision
+        self.tdtype, self.code = DTYPES[precision]
+        self.device = device
+        self.cstride = {"input": 8}
+        for v, c in graph.channels.items():
+            if v != "input":
+                self.cstride[v] = _pow2_at_least(c)
+        self.pack()
+
+    def pack(self):
+        with torch.no_grad():
+            for nd in self.graph.nodes:
+                conv = nd.conv
+                w = conv.weight.detach().to(self.device, torch.float32)
+                cout, cin, kh, kw = w.shape
+                if kh != kw:
+                    raise NotImplementedError("square kernels only")
+                cs = self.cstride[nd.src]
+                nd.cin_stride = cs
+                wp = torch.zeros(cout, kh, kw, cs, device=self.device, dtype=torch.float32)
+                wp[..., :cin] = w.permute(0, 2, 3, 1)
+                nd.k = kh * kw * cs
+                nd.k_pad = _round_up(nd.k, K_ALIGN)
+                nd.cout_pad = _round_up(cout, COUT_ALIGN)
+                full = torch.zeros(nd.cout_pad, nd.k_pad, device=self.device, dtype=torch.float32)
+                full[:cout, :nd.k] = wp.reshape(cout, nd.k)
+                nd.wpk = full.to(self.tdtype).contiguous()
+                scale = torch.ones(nd.cout_pad, device=self.device)
+                shift = torch.zeros(nd.cout_pad, device=self.device)
+                if nd.bn is not None:
+                    s, b = _fold_bn(nd.bn)
+                    scale[:cout] = s.to(self.device)
+                    shift[:cout] = b.to(self.device)
+                elif conv.bias is not None:
+                    shift[:cout] = conv.bias.detach().to(self.device, torch.float32)
+                nd.scale, nd.shift = scale.contiguous(), shift.contiguous()
+
+
+def _conv_out(h, k, s, p, d):
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+class Plan:
+    """Launch plan for one (batch, H, W, precision): shapes, buffers, C-ABI arg structs."""
+
+    def __init__(self, packed: PackedNet, n: int, h: int, w: int, keep_all: bool = False):
+        self.packed = packed
+        self.n, self.h, self.w = n, h, w
+        dev = packed.device
+        g = packed.graph
+        self.shapes = {"input": (h, w)}
+        for nd in g.nodes:
+            c = nd.conv
+            ih, iw = self.shapes[nd.src]
+            self.shapes[nd.dst] = (_conv_out(ih, c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0]),
+                                   _conv_out(iw, c.kernel_size[1], c.stride[1], c.padding[1], c.dilation[1]))
+        lh, lw = self.shapes["logits"]
+        self.out_hw = (8 * lh, 8 * lw)
+
+        # Liveness-based buffer reuse (exact-size pool).
+        last_use = {}
+        for i, nd in enumerate(g.nodes):
+            last_use[nd.src] = i
+            if nd.res:
+                last_use[nd.res] = i
+        self.bufs = {}
+        pool = {}
+        esz = torch.tensor([], dtype=packed.tdtype).element_size()
+        self.bufs["input"] = torch.empty(n * h * w * 8, dtype=packed.tdtype, device=dev)
+        for i, nd in enumerate(g.nodes):
+            if nd.out_fp32_nchw:
+                oh, ow = self.shapes[nd.dst]
+                self.bufs[nd.dst] = torch.empty(n, nd.conv.out_channels, oh, ow, dtype=torch.float32, device=dev)
+            else:
+                oh, ow = self.shapes[nd.dst]
+                numel = n * oh * ow * packed.cstride[nd.dst]
+                key = numel * esz
+                lst = pool.get(key)
+                self.bufs[nd.dst] = lst.pop() if lst else torch.empty(numel, dtype=packed.tdtype, device=dev)
+            if not keep_all:
+                for v in {nd.src, nd.res} - {None, "input"}:
+                    if last_use.get(v) == i and v in self.bufs and v != nd.dst:
+                        t = self.bufs[v]
+                        pool.setdefault(t.numel() * esz, []).append(t)
+        self.keep_all = keep_all
+        self.args = [self._conv_args(nd) for nd in g.nodes]
+
+    def _conv_args(self, nd: ConvNode) -> _lib.ConvArgs:
+        pk = self.packed
+        c = nd.conv
+        ih, iw = self.shapes[nd.src]
+        oh, ow = self.shapes[nd.dst]
+        a = _lib.ConvArgs()
+        a.x = self.bufs[nd.src].data_ptr()
+        a.wgt = nd.wpk.data_ptr()
+        a.scale = nd.scale.data_ptr()
+        a.shift = nd.shift.data_ptr()
+        a.res = self.bufs[nd.res].data_ptr() if nd.res else None
+        a.y = self.bufs[nd.dst].data_ptr()
+        cout = c.out_channels
+        if nd.out_fp32_nchw:
+            a.y_sn, a.y_sp, a.y_sc = cout * oh * ow, 1, oh * ow
+            a.out_dtype = _lib.DRNMI_F32
+        else:
+            cs = pk.cstride[nd.dst]
+            if nd.res and pk.cstride[nd.res] != cout:
+                raise NotImplementedError("residual channel stride must equal cout")
+            a.y_sn, a.y_sp, a.y_sc = oh * ow * cs, cs, 1
+            a.out_dtype = pk.code
+            if cs != cout:
+                raise NotImplementedError("activation channel padding beyond the stem input")
+        a.n, a.h, a.w, a.cin = self.n, ih, iw, nd.cin_stride
+        a.ho, a.wo, a.cout, a.cout_pad = oh, ow, cout, nd.cout_pad
+        a.ks, a.stride, a.pad, a.dil = c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0]
+        a.k, a.k_pad = nd.k, nd.k_pad
+        a.relu = 1 if nd.relu else 0
+        a.dtype = pk.code
+        a.tile = -1
+        return a
+
+    def refresh_weight_ptrs(self):
+        for a, nd in zip(self.args, self.packed.graph.nodes):
+            a.wgt = nd.wpk.data_ptr()
+            a.scale = nd.scale.data_ptr()
+            a.shift = nd.shift.data_ptr()
+
+    # ------------------------------------------------------------------ execution
+    def run_backbone(self, stream: int, timing_hook=None):
+        lib = _lib.load()
+        for i, (a, nd) in enumerate(zip(self.args, self.packed.graph.nodes)):
+            if timing_hook is not None:
+                timing_hook(i, nd, True)
+            _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), f"conv {nd.name}")
+            if timing_hook is not None:
+                timing_hook(i, nd, False)
+
+    def ingest_nchw(self, x: torch.Tensor, stream: int):
+        lib = _lib.load()
+        n, c, h, w = x.shape
+        _lib.check(lib.drnmi_nchw_to_nhwc(x.data_ptr(), self.bufs["input"].data_ptr(), n, c, h, w, 8,
+                                          self.packed.code, ctypes.c_void_p(stream)), "nchw_to_nhwc")
+
+    def ingest_u8(self, frames: torch.Tensor, mean, std, bgr: bool, stream: int):
+        lib = _lib.load()
+        n, h, w, _ = frames.shape
+        m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+        s = (ctypes.c_float * 3)(*[float(v) for v in std])
+        _lib.check(lib.drnmi_frame_ingest_u8(frames.data_ptr(), self.bufs["input"].data_ptr(), n, h, w,
+                                             m, s, 1 if bgr else 0, self.packed.code,
+                                             ctypes.c_void_p(stream)), "frame_ingest_u8")
+
+    def head(self, up_w: torch.Tensor, stream: int, logprobs: torch.Tensor | None,
+             labels: torch.Tensor | None):
+        lib = _lib.load()
+        logits = self.bufs["logits"]
+        n, c, lh, lw = logits.shape
+        lab_dtype = _lib.DRNMI_U8
+        if labels is not None and labels.dtype == torch.int64:
+            lab_dtype = _lib.DRNMI_I64
+        _lib.check(lib.drnmi_up8_logsoftmax_argmax(
+            logits.data_ptr(), up_w.data_ptr(),
+            logprobs.data_ptr() if logprobs is not None else None,
+            labels.data_ptr() if labels is not None else None,
+            lab_dtype, n, c, lh, lw, ctypes.c_void_p(stream)), "up8_logsoftmax_argmax")
+
+    def stage_nchw(self, value: str) -> torch.Tensor:
+        """fp32 NCHW copy of an intermediate activation (parity taps; keep_all plans)."""
+        lib = _lib.load()
+        c = self.packed.graph.channels[value]
+        oh, ow = self.shapes[value]
+        out = torch.empty(self.n, c, oh, ow, dtype=torch.float32, device=self.packed.device)
+        _lib.check(lib.drnmi_nhwc_to_nchw(self.bufs[value].data_ptr(), out.data_ptr(), self.n, c, oh, ow,
+                                          self.packed.cstride[value], self.packed.code,
+                                          ctypes.c_void_p(_lib.stream_ptr())), "nhwc_to_nchw")
+        return out
+
+
+def conv_flops(plan: Plan):
+    """Per-node algorithmic FLOPs (2*M*N*K with the logical Cin, no padding)."""
+    out = []
+    for nd in plan.packed.graph.nodes:
+        c = nd.conv
+        oh, ow = plan.shapes[nd.dst]
+        m = plan.n * oh * ow
+        k = c.in_channels * c.kernel_size[0] * c.kernel_size[1]
+        out.append(2.0 * m * c.out_channels * k)
+    return out

@@ -1,0 +1,110 @@
+"""Functional host wrappers of the C-ABI (one call = one HIP launch on the current stream).
+
+These are the per-op entry points (the engine prebuilds the same argument structs once
+per plan).  Tensors must already live on the ROCm device; nothing here computes on the
+host or falls back to ATen.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .engine import COUT_ALIGN, K_ALIGN, _round_up
+
+_CODE = {torch.float32: _lib.DRNMI_F32, torch.bfloat16: _lib.DRNMI_BF16}
+
+
+def pack_conv_weight(weight: torch.Tensor, cin_stride: int, dtype: torch.dtype):
+    """[cout, cin, k, k] fp32 -> [cout_pad][k_pad] with k = (kh*ks + kw)*cin_stride + ci."""
+    cout, cin, kh, kw = weight.shape
+    k = kh * kw * cin_stride
+    wp = torch.zeros(cout, kh, kw, cin_stride, device=weight.device, dtype=torch.float32)
+    wp[..., :cin] = weight.float().permute(0, 2, 3, 1)
+    full = torch.zeros(_round_up(cout, COUT_ALIGN), _round_up(k, K_ALIGN), device=weight.device,
+                       dtype=torch.float32)
+    full[:cout, :k] = wp.reshape(cout, k)
+    return full.to(dtype).contiguous(), k
+
+
+def conv2d_bn_act(x_nhwc: torch.Tensor, weight: torch.Tensor, scale=None, shift=None, residual=None,
+                  stride=1, padding=0, dilation=1, relu=False, out_nchw_fp32=False, tile=-1,
+                  packed=None):
+    """y = act(conv(x) * scale + shift [+ residual]) on NHWC x (channel stride = x.shape[3])."""
+    n, h, w, cs = x_nhwc.shape
+    cout, cin, ks, _ = weight.shape
+    dt = x_nhwc.dtype
+    if packed is None:
+        wpk, k = pack_conv_weight(weight, cs, dt)
+    else:
+        wpk, k = packed
+    cout_pad = wpk.shape[0]
+    dev = x_nhwc.device
+    sc = torch.ones(cout_pad, device=dev)
+    sh = torch.zeros(cout_pad, device=dev)
+    if scale is not None:
+        sc[:cout] = scale.float()
+    if shift is not None:
+        sh[:cout] = shift.float()
+    ho = (h + 2 * padding - dilation * (ks - 1) - 1) // stride + 1
+    wo = (w + 2 * padding - dilation * (ks - 1) - 1) // stride + 1
+    if out_nchw_fp32:
+        y = torch.empty(n, cout, ho, wo, device=dev, dtype=torch.float32)
+        strides = (cout * ho * wo, 1, ho * wo)
+        out_code = _lib.DRNMI_F32
+    else:
+        y = torch.empty(n, ho, wo, cout, device=dev, dtype=dt)
+        strides = (ho * wo * cout, cout, 1)
+        out_code = _CODE[dt]
+    a = _lib.ConvArgs()
+    a.x, a.wgt, a.scale, a.shift = x_nhwc.data_ptr(), wpk.data_ptr(), sc.data_ptr(), sh.data_ptr()
+    a.res = residual.data_ptr() if residual is not None else None
+    a.y = y.data_ptr()
+    a.y_sn, a.y_sp, a.y_sc = strides
+    a.n, a.h, a.w, a.cin = n, h, w, cs
+    a.ho, a.wo, a.cout, a.cout_pad = ho, wo, cout, cout_pad
+    a.ks, a.stride, a.pad, a.dil = ks, stride, padding, dilation
+    a.k, a.k_pad = k, wpk.shape[1]
+    a.relu = 1 if relu else 0
+    a.dtype, a.out_dtype = _CODE[dt], out_code
+    a.tile = tile
+    lib = _lib.load()
+    _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr(dev))), "conv2d_bn_act")
+    return y
+
+
+def nchw_to_nhwc(x: torch.Tensor, c_pad: int, dtype=torch.float32):
+    n, c, h, w = x.shape
+    out = torch.empty(n, h, w, c_pad, device=x.device, dtype=dtype)
+    lib = _lib.load()
+    _lib.check(lib.drnmi_nchw_to_nhwc(x.contiguous().data_ptr(), out.data_ptr(), n, c, h, w, c_pad, _CODE[dtype],
+                                      ctypes.c_void_p(_lib.stream_ptr(x.device))), "nchw_to_nhwc")
+    return out
+
+
+def frame_ingest(frames_u8: torch.Tensor, mean, std, bgr=False, dtype=torch.float32):
+    n, h, w, _ = frames_u8.shape
+    out = torch.empty(n, h, w, 8, device=frames_u8.device, dtype=dtype)
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    lib = _lib.load()
+    _lib.check(lib.drnmi_frame_ingest_u8(frames_u8.contiguous().data_ptr(), out.data_ptr(), n, h, w, m, s,
+                                         1 if bgr else 0, _CODE[dtype],
+                                         ctypes.c_void_p(_lib.stream_ptr(frames_u8.device))), "frame_ingest")
+    return out
+
+
+def up8_logsoftmax_argmax(logits: torch.Tensor, up_plane: torch.Tensor, want_logprobs=True,
+                          label_dtype=torch.int64):
+    n, c, h, w = logits.shape
+    dev = logits.device
+    lp = torch.empty(n, c, 8 * h, 8 * w, device=dev, dtype=torch.float32) if want_logprobs else None
+    lab = torch.empty(n, 8 * h, 8 * w, device=dev, dtype=label_dtype) if label_dtype is not None else None
+    code = _lib.DRNMI_I64 if label_dtype == torch.int64 else _lib.DRNMI_U8
+    lib = _lib.load()
+    _lib.check(lib.drnmi_up8_logsoftmax_argmax(
+        logits.contiguous().data_ptr(), up_plane.float().contiguous().data_ptr(),
+        lp.data_ptr() if lp is not None else None, lab.data_ptr() if lab is not None else None,
+        code, n, c, h, w, ctypes.c_void_p(_lib.stream_ptr(dev))), "up8_logsoftmax_argmax")
+    return lp, lab

@@ -1,0 +1,57 @@
+"""Algorithmic work and the per-layer roofline of a DRN-D plan.
+
+Per conv node l:  F_l = 2 * M * Cout * (Cin * k * k)       (M = output pixels)
+                  B_l = in + weights + out (+ residual)    (activations/weights at the
+                        plan's element size; the stem reads the uint8 frame; the seg
+                        logits are fp32 and the head writes uint8 labels)
+t_l = max(F_l / P_mfma, B_l / BW_hbm),  T* = sum_l t_l,  network fraction = T* / T_measured.
+Peaks from /opt/skills/guides/MI355X_MICROARCH.md: HBM 8.0 TB/s, dense bf16 MFMA 2.5 PFLOP/s,
+f32-input MFMA 157.3 TFLOP/s.
+"""
+from __future__ import annotations
+
+HBM_PEAK_BPS = 8.0e12
+MFMA_PEAK = {"bf16": 2.5e15, "fp32": 157.3e12}
+
+
+def node_work(plan):
+    """[(name, flops, bytes)] for every conv node, plus the head (up+argmax)."""
+    pk = plan.packed
+    esz = 2 if pk.precision == "bf16" else 4
+    out = []
+    for nd in pk.graph.nodes:
+        c = nd.conv
+        ih, iw = plan.shapes[nd.src]
+        oh, ow = plan.shapes[nd.dst]
+        m = plan.n * oh * ow
+        cin, cout, k = c.in_channels, c.out_channels, c.kernel_size[0]
+        flops = 2.0 * m * cout * cin * k * k
+        if nd.src == "input":
+            in_b = plan.n * ih * iw * 3 * 1          # uint8 frame
+        else:
+            in_b = plan.n * ih * iw * cin * esz
+        w_b = cout * cin * k * k * esz
+        out_b = m * cout * (4 if nd.out_fp32_nchw else esz)
+        res_b = m * cout * esz if nd.res else 0
+        out.append((nd.name, flops, float(in_b + w_b + out_b + res_b)))
+    lh, lw = plan.shapes["logits"]
+    c = pk.graph.channels["logits"]
+    H, W = plan.out_hw
+    head_b = plan.n * c * lh * lw * 4 + plan.n * H * W * 1
+    head_f = plan.n * H * W * c * 8.0             # 4 MAC per class per output pixel
+    out.append(("head", head_f, float(head_b)))
+    return out
+
+
+def network_roofline(plan):
+    prec = plan.packed.precision
+    peak = MFMA_PEAK[prec]
+    rows = node_work(plan)
+    t_star = sum(max(f / peak, b / HBM_PEAK_BPS) for _, f, b in rows)
+    return {
+        "flops": sum(f for _, f, _ in rows),
+        "bytes": sum(b for _, _, b in rows),
+        "t_star_s": t_star,
+        "t_mfma_s": sum(f for _, f, _ in rows) / peak,
+        "t_hbm_s": sum(b for _, _, b in rows) / HBM_PEAK_BPS,
+    }
