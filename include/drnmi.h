@@ -59,7 +59,26 @@ typedef struct drnmi_conv_args {
   int32_t dtype;            /* DRNMI_BF16 or DRNMI_F32: x, w, res                   */
   int32_t out_dtype;        /* DRNMI_BF16 or DRNMI_F32: y                           */
   int32_t tile;             /* tile id (drnmi_conv_tile_name), -1 = auto            */
+  int32_t algo;             /* DRNMI_ALGO_IGEMM or DRNMI_ALGO_PATCH (see below)     */
+  int32_t src_u8;           /* PATCH only: x is uint8 HWC3 frames, normalised on load */
+  int32_t bgr;              /* src_u8: swap channel 0 and 2 on read                  */
+  float mean[3], std[3];    /* src_u8: (u8 / 255 - mean[c]) / std[c], fp32          */
 } drnmi_conv_args;
+
+/* Algorithms behind drnmi_conv2d_bn_act:
+ *  DRNMI_ALGO_IGEMM  generic NHWC implicit GEMM (any power-of-two cin >= 8, any ks/stride/dil;
+ *                    bf16 or fp32).
+ *  DRNMI_ALGO_PATCH  bf16-only small-channel direct conv for the full-resolution layers
+ *                    (lmodels/drn.py:132-137 layer0, :201-211 layer1/layer2): the input tile
+ *                    plus halo is staged once in LDS and reused by all ks*ks taps; weights stay
+ *                    in registers; the MFMA puts output channels on rows so each lane stores 4
+ *                    contiguous channels (coalesced NHWC stores).  Supports dil = 1,
+ *                    (cin, cout, ks, stride) in {(8,16,7,1), (16,16,3,1), (16,32,3,2), (32,64,3,2)},
+ *                    no residual, packed NHWC output; and the
+ *                    fused stem src_u8 = 1 with (cin = 4, cout = 16, ks = 7, stride = 1): weights
+ *                    packed [cout_pad][224] with k = kh*32 + kw*4 + c (kw < 8, c < 4; kw = 7 and
+ *                    c = 3 are zero), which also replaces the frame-ingest kernel. */
+enum drnmi_algo { DRNMI_ALGO_IGEMM = 0, DRNMI_ALGO_PATCH = 1 };
 
 int drnmi_conv2d_bn_act(const drnmi_conv_args* args, void* stream);
 

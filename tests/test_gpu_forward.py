@@ -114,3 +114,19 @@ def test_weights_repack_after_mask_apply(golden_forward, tmp_path):
     _, ref, _ = O.drnseg_forward(sd, "drn_d_22", x.cpu())
     assert (l1.cpu() - ref).abs().max().item() <= 1e-3
     assert (l1 - l0).abs().max().item() > 1e-3
+
+
+def test_bf16_segment_matches_bf16_forward_labels(golden_forward):
+    """bf16 video path (fused u8 stem) vs bf16 NCHW path: same network, near-identical labels."""
+    case = "d22_2x128x256"
+    m = model(case, golden_forward).set_precision("bf16")
+    frames = torch.from_numpy(golden_forward[case + "/frames"]).to(DEV)
+    x = torch.from_numpy(golden_forward[case + "/input"]).to(DEV)
+    lab_seg = m.segment(frames).long()
+    lab_fwd = m.predict(x)
+    m.set_precision("fp32")
+    agree = (lab_seg == lab_fwd).float().mean().item()
+    ref = torch.from_numpy(golden_forward[case + "/labels"]).long().to(DEV)
+    agree_ref = (lab_seg == ref).float().mean().item()
+    print(f"bf16 segment vs predict agreement {agree:.4f}, vs reference {agree_ref:.4f}")
+    assert agree >= 0.98 and agree_ref >= 0.95

@@ -176,3 +176,48 @@ def test_mask_apply_bit_exact(use_bits, tmp_path):
     for k, v in before.items():
         if k not in layers:
             assert torch.equal(sd[k].cpu(), v), k
+
+
+PATCH_CASES = [  # cin(stored), cout, ks, stride, h, w  — the bf16 LDS-patch kernel shapes
+    (16, 16, 3, 1, 37, 131),
+    (16, 32, 3, 2, 41, 133),
+    (32, 64, 3, 2, 19, 70),
+    (8, 16, 7, 1, 23, 77),
+]
+
+
+@pytest.mark.parametrize("case", range(len(PATCH_CASES)))
+def test_patch_conv_bf16(case):
+    from drnmi import _lib
+    cin, cout, ks, stride, h, w = PATCH_CASES[case]
+    n, pad = 2, ks // 2
+    x = _rand((n, cin, h, w), 31 + case).bfloat16().float()
+    wt = _rand((cout, cin, ks, ks), 41 + case, (2.0 / (ks * ks * cout)) ** 0.5).bfloat16().float()
+    sc = torch.rand(cout, generator=torch.Generator().manual_seed(1)) + 0.5
+    sh = torch.rand(cout, generator=torch.Generator().manual_seed(2)) - 0.5
+    ref = _ref_conv(x, wt, sc, sh, None, stride, pad, 1, True)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV, torch.bfloat16)
+    y = ops.conv2d_bn_act(xd, wt.to(DEV), sc.to(DEV), sh.to(DEV), None, stride, pad, 1, True,
+                          algo=_lib.ALGO_PATCH)
+    got = y.float().permute(0, 3, 1, 2).cpu()
+    y2 = ops.conv2d_bn_act(xd, wt.to(DEV), sc.to(DEV), sh.to(DEV), None, stride, pad, 1, True)
+    scale = ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= 1.5e-2 * scale
+    # the two bf16 algorithms agree to bf16 output rounding
+    assert (got - y2.float().permute(0, 3, 1, 2).cpu()).abs().max().item() <= 1e-2 * scale
+
+
+def test_stem_u8_fused_ingest():
+    frames = torch.randint(0, 256, (2, 45, 83, 3), dtype=torch.uint8,
+                           generator=torch.Generator().manual_seed(3))
+    wt = _rand((16, 3, 7, 7), 50, 0.1).bfloat16().float()
+    sc = torch.rand(16, generator=torch.Generator().manual_seed(4)) + 0.5
+    sh = torch.rand(16, generator=torch.Generator().manual_seed(5)) - 0.5
+    x = O.preprocess_u8(frames.numpy()).bfloat16().float()
+    ref = _ref_conv(x, wt, sc, sh, None, 1, 3, 1, True)
+    y = ops.stem_u8(frames.to(DEV), wt, sc.to(DEV), sh.to(DEV), O.INFO_MEAN, O.INFO_STD)
+    got = y.float().permute(0, 3, 1, 2).cpu()
+    assert (got - ref).abs().max().item() <= 1.5e-2 * ref.abs().max().item()
+    yb = ops.stem_u8(frames.flip(-1).contiguous().to(DEV), wt, sc.to(DEV), sh.to(DEV), O.INFO_MEAN,
+                     O.INFO_STD, bgr=True)
+    assert torch.equal(yb, y)

@@ -20,6 +20,7 @@
 // (blocks b and b+8 share an XCD) so the blocks that share an input row-band and a
 // weight panel run under one L2.
 #include "common.h"
+#include "kernels.h"
 
 namespace drnmi {
 
@@ -307,6 +308,16 @@ extern "C" const char* drnmi_conv_tile_name(int tile) {
 extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (a == nullptr) return DRNMI_EINVAL;
   const drnmi_conv_args& p = *a;
+  if (p.algo == DRNMI_ALGO_PATCH) {
+    if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.scale == nullptr || p.shift == nullptr ||
+        p.n <= 0 || p.h <= 0 || p.w <= 0 || p.cout > p.cout_pad)
+      return DRNMI_EINVAL;
+    if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
+        p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
+      return DRNMI_EINVAL;
+    return patch_conv_dispatch(p, reinterpret_cast<hipStream_t>(stream));
+  }
+  if (p.algo != DRNMI_ALGO_IGEMM || p.src_u8) return DRNMI_EINVAL;
   const bool pow2 = p.cin >= 8 && (p.cin & (p.cin - 1)) == 0;
   if (!pow2 || p.n <= 0 || p.h <= 0 || p.w <= 0 || p.ho <= 0 || p.wo <= 0) return DRNMI_EINVAL;
   if (p.cout <= 0 || p.cout > p.cout_pad || p.k != p.ks * p.ks * p.cin) return DRNMI_EINVAL;

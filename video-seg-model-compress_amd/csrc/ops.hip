@@ -143,6 +143,108 @@ up8_lsm_kernel(const float* __restrict__ logits, const float* __restrict__ up_w,
   }
 }
 
+// Fast path for a compile-time class count: each thread owns 4 consecutive output pixels
+// of one row.  Output columns [4q, 4q+4) all read input columns j0 = j1-1, j1 = (q+1)>>1,
+// so the 4 taps per class are loaded once for 4 pixels (19 loads per pixel -> ~5), the
+// labels go out as one 4-byte store and each log-prob plane as one 16-byte store.
+// Same per-pixel arithmetic (and summation order) as up8_lsm_kernel.
+template <int NC, int LABEL_DTYPE>
+__global__ void __launch_bounds__(256)
+up8_lsm_quad_kernel(const float* __restrict__ logits, const float* __restrict__ up_w,
+                    float* __restrict__ logprobs, void* __restrict__ labels, int h, int w) {
+  __shared__ float wk[256];
+  wk[threadIdx.x] = up_w[threadIdx.x];
+  __syncthreads();
+
+  const int H = h * 8, W = w * 8;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int oy = blockIdx.y;
+  const int n = blockIdx.z;
+  if (4 * q >= W) return;
+
+  const int i1 = (oy + 4) >> 3, i0 = i1 - 1;
+  const int ky1 = oy + 4 - 8 * i1, ky0 = ky1 + 8;
+  const int j1 = (q + 1) >> 1, j0 = j1 - 1;
+  const bool vi0 = i0 >= 0, vi1 = i1 < h, vj0 = j0 >= 0, vj1 = j1 < w;
+  float w00[4], w01[4], w10[4], w11[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int ox = 4 * q + p;
+    const int kx1 = ox + 4 - 8 * j1, kx0 = kx1 + 8;
+    w00[p] = (vi0 && vj0) ? wk[ky0 * 16 + kx0] : 0.f;
+    w01[p] = (vi0 && vj1) ? wk[ky0 * 16 + kx1] : 0.f;
+    w10[p] = (vi1 && vj0) ? wk[ky1 * 16 + kx0] : 0.f;
+    w11[p] = (vi1 && vj1) ? wk[ky1 * 16 + kx1] : 0.f;
+  }
+  const int ci0 = vi0 ? i0 : 0, ci1 = vi1 ? i1 : 0, cj0 = vj0 ? j0 : 0, cj1 = vj1 ? j1 : 0;
+  const int64_t plane = static_cast<int64_t>(h) * w;
+  const float* src = logits + static_cast<int64_t>(n) * NC * plane;
+  float v[NC][4];
+  float vmax[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const float* s = src + k * plane;
+    const float s00 = s[ci0 * w + cj0], s01 = s[ci0 * w + cj1];
+    const float s10 = s[ci1 * w + cj0], s11 = s[ci1 * w + cj1];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float a = s00 * w00[p];
+      a = fmaf(s01, w01[p], a);
+      a = fmaf(s10, w10[p], a);
+      a = fmaf(s11, w11[p], a);
+      v[k][p] = a;
+      vmax[p] = fmaxf(vmax[p], a);
+    }
+  }
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int64_t pix = static_cast<int64_t>(oy) * W + 4 * q;
+  int arg[4] = {0, 0, 0, 0};
+  if (logprobs == nullptr) {
+    // Labels only: lp_c = (v_c - max) - lse is a monotone map of v_c, so the argmax of the
+    // up-sampled logits is the argmax of the log-probs (a tie created by the rounding of that
+    // map needs two logits within ~1 ulp of lse: below fp32 summation-order noise).
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float best = v[0][p];
+#pragma unroll
+      for (int k = 1; k < NC; ++k)
+        if (v[k][p] > best) { best = v[k][p]; arg[p] = k; }
+    }
+  } else {
+    float lse[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) sum += expf(v[k][p] - vmax[p]);
+      lse[p] = logf(sum);
+    }
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      float lp[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        lp[p] = (v[k][p] - vmax[p]) - lse[p];
+        if (lp[p] > best[p]) { best[p] = lp[p]; arg[p] = k; }
+      }
+      *reinterpret_cast<float4*>(logprobs + (static_cast<int64_t>(n) * NC + k) * HW + pix) =
+          make_float4(lp[0], lp[1], lp[2], lp[3]);
+    }
+  }
+  if (labels != nullptr) {
+    if (LABEL_DTYPE == DRNMI_U8) {
+      const uint32_t packed = static_cast<uint32_t>(arg[0]) | (static_cast<uint32_t>(arg[1]) << 8) |
+                              (static_cast<uint32_t>(arg[2]) << 16) | (static_cast<uint32_t>(arg[3]) << 24);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(labels) + static_cast<int64_t>(n) * HW + pix) = packed;
+    } else {
+      int64_t* o = reinterpret_cast<int64_t*>(labels) + static_cast<int64_t>(n) * HW + pix;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) o[p] = arg[p];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- mask apply
 constexpr int kMaskBatch = 32;
 
@@ -282,6 +384,15 @@ extern "C" int drnmi_up8_logsoftmax_argmax(const float* logits, const float* up_
   const int W = w * 8;
   dim3 grid(static_cast<unsigned>((W + 255) / 256), static_cast<unsigned>(h * 8), static_cast<unsigned>(n));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (c == 19) {   // Cityscapes classes: quad kernel
+    dim3 gq(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h * 8), static_cast<unsigned>(n));
+    if (label_dtype == DRNMI_I64) {
+      hipLaunchKernelGGL((up8_lsm_quad_kernel<19, DRNMI_I64>), gq, dim3(256), 0, s, logits, up_w, logprobs, labels, h, w);
+    } else {
+      hipLaunchKernelGGL((up8_lsm_quad_kernel<19, DRNMI_U8>), gq, dim3(256), 0, s, logits, up_w, logprobs, labels, h, w);
+    }
+    return static_cast<int>(hipGetLastError());
+  }
   if (label_dtype == DRNMI_I64) {
     hipLaunchKernelGGL(up8_lsm_kernel<DRNMI_I64>, grid, dim3(256), 0, s, logits, up_w, logprobs, labels, c, h, w);
   } else {

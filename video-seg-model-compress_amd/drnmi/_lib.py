@@ -11,6 +11,7 @@ import os
 from .build import LIB_PATH
 
 DRNMI_F32, DRNMI_BF16, DRNMI_U8, DRNMI_I64 = 0, 1, 2, 3
+ALGO_IGEMM, ALGO_PATCH = 0, 1
 
 _STATUS = {-1: "DRNMI_EINVAL (bad shape/stride/dtype)", -2: "DRNMI_ENOTSUP (no kernel for this config)"}
 
@@ -32,6 +33,11 @@ class ConvArgs(ctypes.Structure):
         ("relu", ctypes.c_int32),
         ("dtype", ctypes.c_int32), ("out_dtype", ctypes.c_int32),
         ("tile", ctypes.c_int32),
+        ("algo", ctypes.c_int32),
+        ("src_u8", ctypes.c_int32),
+        ("bgr", ctypes.c_int32),
+        ("mean", ctypes.c_float * 3),
+        ("std", ctypes.c_float * 3),
     ]
 
 

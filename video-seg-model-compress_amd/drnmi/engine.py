@@ -31,6 +31,10 @@ COUT_ALIGN = 128
 
 DTYPES = {"fp32": (torch.float32, _lib.DRNMI_F32), "bf16": (torch.bfloat16, _lib.DRNMI_BF16)}
 
+# (cin_stride, cout, ks, stride, dil) served by the LDS-patch kernel (bf16 only; include/drnmi.h)
+PATCH_SHAPES = {(8, 16, 7, 1, 1), (16, 16, 3, 1, 1), (16, 32, 3, 2, 1), (32, 64, 3, 2, 1)}
+STEM_U8_K = 224     # fused u8 stem: k = kh*32 + kw*4 + c
+
 
 def _pow2_at_least(c: int, lo: int = 8) -> int:
     p = lo
@@ -186,6 +190,16 @@ class PackedNet:
                 elif conv.bias is not None:
                     shift[:cout] = conv.bias.detach().to(self.device, torch.float32)
                 nd.scale, nd.shift = scale.contiguous(), shift.contiguous()
+            # fused-ingest stem weights (bf16 patch kernel reads uint8 frames directly)
+            self.stem_u8_w = None
+            stem = self.graph.nodes[0]
+            w = stem.conv.weight.detach().to(self.device, torch.float32)
+            if self.precision == "bf16" and tuple(w.shape[1:]) == (3, 7, 7):
+                wp = torch.zeros(w.shape[0], 7, 8, 4, device=self.device, dtype=torch.float32)
+                wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+                full = torch.zeros(stem.cout_pad, STEM_U8_K, device=self.device, dtype=torch.float32)
+                full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
+                self.stem_u8_w = full.to(self.tdtype).contiguous()
 
 
 def _conv_out(h, k, s, p, d):
@@ -236,6 +250,8 @@ class Plan:
                         pool.setdefault(t.numel() * esz, []).append(t)
         self.keep_all = keep_all
         self.args = [self._conv_args(nd) for nd in g.nodes]
+        self.stem_u8 = self._stem_u8_args()
+        self.src = "nchw"
 
     def _conv_args(self, nd: ConvNode) -> _lib.ConvArgs:
         pk = self.packed
@@ -268,6 +284,23 @@ class Plan:
         a.relu = 1 if nd.relu else 0
         a.dtype = pk.code
         a.tile = -1
+        shape = (nd.cin_stride, cout, c.kernel_size[0], c.stride[0], c.dilation[0])
+        use_patch = (pk.precision == "bf16" and shape in PATCH_SHAPES and nd.res is None
+                     and not nd.out_fp32_nchw)
+        a.algo = _lib.ALGO_PATCH if use_patch else _lib.ALGO_IGEMM
+        return a
+
+    def _stem_u8_args(self) -> _lib.ConvArgs | None:
+        pk = self.packed
+        if pk.stem_u8_w is None:
+            return None
+        a = _lib.ConvArgs()
+        ctypes.pointer(a)[0] = self.args[0]
+        a.algo = _lib.ALGO_PATCH
+        a.src_u8 = 1
+        a.cin = 4
+        a.k = a.k_pad = STEM_U8_K
+        a.wgt = pk.stem_u8_w.data_ptr()
         return a
 
     def refresh_weight_ptrs(self):
@@ -275,11 +308,18 @@ class Plan:
             a.wgt = nd.wpk.data_ptr()
             a.scale = nd.scale.data_ptr()
             a.shift = nd.shift.data_ptr()
+        if self.stem_u8 is not None:
+            nd = self.packed.graph.nodes[0]
+            self.stem_u8.wgt = self.packed.stem_u8_w.data_ptr()
+            self.stem_u8.scale = nd.scale.data_ptr()
+            self.stem_u8.shift = nd.shift.data_ptr()
 
     # ------------------------------------------------------------------ execution
     def run_backbone(self, stream: int, timing_hook=None):
         lib = _lib.load()
         for i, (a, nd) in enumerate(zip(self.args, self.packed.graph.nodes)):
+            if i == 0 and self.src == "u8":
+                a = self.stem_u8
             if timing_hook is not None:
                 timing_hook(i, nd, True)
             _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), f"conv {nd.name}")
@@ -287,14 +327,29 @@ class Plan:
                 timing_hook(i, nd, False)
 
     def ingest_nchw(self, x: torch.Tensor, stream: int):
+        self.src = "nchw"
         lib = _lib.load()
         n, c, h, w = x.shape
         _lib.check(lib.drnmi_nchw_to_nhwc(x.data_ptr(), self.bufs["input"].data_ptr(), n, c, h, w, 8,
                                           self.packed.code, ctypes.c_void_p(stream)), "nchw_to_nhwc")
 
     def ingest_u8(self, frames: torch.Tensor, mean, std, bgr: bool, stream: int):
-        lib = _lib.load()
+        """uint8 HWC frames in.  bf16: the stem kernel reads them directly (normalise fused);
+        fp32: a separate ingest kernel writes the normalised NHWC8 input."""
         n, h, w, _ = frames.shape
+        if (n, h, w) != (self.n, self.h, self.w):
+            raise ValueError("frames shape does not match the plan")
+        if self.stem_u8 is not None:
+            a = self.stem_u8
+            a.x = frames.data_ptr()
+            a.bgr = 1 if bgr else 0
+            for i in range(3):
+                a.mean[i] = float(mean[i])
+                a.std[i] = float(std[i])
+            self.src = "u8"
+            return
+        self.src = "nchw"
+        lib = _lib.load()
         m = (ctypes.c_float * 3)(*[float(v) for v in mean])
         s = (ctypes.c_float * 3)(*[float(v) for v in std])
         _lib.check(lib.drnmi_frame_ingest_u8(frames.data_ptr(), self.bufs["input"].data_ptr(), n, h, w,

@@ -30,7 +30,7 @@ def pack_conv_weight(weight: torch.Tensor, cin_stride: int, dtype: torch.dtype):
 
 def conv2d_bn_act(x_nhwc: torch.Tensor, weight: torch.Tensor, scale=None, shift=None, residual=None,
                   stride=1, padding=0, dilation=1, relu=False, out_nchw_fp32=False, tile=-1,
-                  packed=None):
+                  packed=None, algo=_lib.ALGO_IGEMM):
     """y = act(conv(x) * scale + shift [+ residual]) on NHWC x (channel stride = x.shape[3])."""
     n, h, w, cs = x_nhwc.shape
     cout, cin, ks, _ = weight.shape
@@ -69,6 +69,7 @@ def conv2d_bn_act(x_nhwc: torch.Tensor, weight: torch.Tensor, scale=None, shift=
     a.relu = 1 if relu else 0
     a.dtype, a.out_dtype = _CODE[dt], out_code
     a.tile = tile
+    a.algo = algo
     lib = _lib.load()
     _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr(dev))), "conv2d_bn_act")
     return y
@@ -108,3 +109,40 @@ def up8_logsoftmax_argmax(logits: torch.Tensor, up_plane: torch.Tensor, want_log
         lp.data_ptr() if lp is not None else None, lab.data_ptr() if lab is not None else None,
         code, n, c, h, w, ctypes.c_void_p(_lib.stream_ptr(dev))), "up8_logsoftmax_argmax")
     return lp, lab
+
+
+def stem_u8(frames_u8: torch.Tensor, weight: torch.Tensor, scale, shift, mean, std, bgr=False, relu=True):
+    """Fused ingest + 7x7 stem (bf16 patch kernel): uint8 [N,H,W,3] -> bf16 NHWC [N,H,W,cout]."""
+    from .engine import STEM_U8_K
+    n, h, w, _ = frames_u8.shape
+    cout = weight.shape[0]
+    dev = frames_u8.device
+    wp = torch.zeros(cout, 7, 8, 4, device=dev)
+    wp[:, :, :7, :3] = weight.float().to(dev).permute(0, 2, 3, 1)
+    full = torch.zeros(_round_up(cout, COUT_ALIGN), STEM_U8_K, device=dev)
+    full[:cout] = wp.reshape(cout, STEM_U8_K)
+    wpk = full.to(torch.bfloat16).contiguous()
+    sc = torch.ones(wpk.shape[0], device=dev)
+    sh = torch.zeros(wpk.shape[0], device=dev)
+    sc[:cout] = scale.float()
+    sh[:cout] = shift.float()
+    y = torch.empty(n, h, w, cout, device=dev, dtype=torch.bfloat16)
+    a = _lib.ConvArgs()
+    a.x, a.wgt, a.scale, a.shift, a.res, a.y = frames_u8.data_ptr(), wpk.data_ptr(), sc.data_ptr(), \
+        sh.data_ptr(), None, y.data_ptr()
+    a.y_sn, a.y_sp, a.y_sc = h * w * cout, cout, 1
+    a.n, a.h, a.w, a.cin = n, h, w, 4
+    a.ho, a.wo, a.cout, a.cout_pad = h, w, cout, wpk.shape[0]
+    a.ks, a.stride, a.pad, a.dil = 7, 1, 3, 1
+    a.k = a.k_pad = STEM_U8_K
+    a.relu = 1 if relu else 0
+    a.dtype = a.out_dtype = _lib.DRNMI_BF16
+    a.tile = -1
+    a.algo = _lib.ALGO_PATCH
+    a.src_u8 = 1
+    a.bgr = 1 if bgr else 0
+    for i in range(3):
+        a.mean[i], a.std[i] = float(mean[i]), float(std[i])
+    lib = _lib.load()
+    _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr(dev))), "stem_u8")
+    return y
