@@ -26,7 +26,6 @@ sys.path.insert(0, os.path.join(REPO, "video-seg-model-compress_amd"))
 sys.path.insert(0, REPO)
 
 METRIC = "frames/sec @1024x2048 DRN-D-22 on 1/2/4/8 MI355X; mIoU vs ref; %HBM roofline"
-DOMINANT_T = "conv_igemm_kernel<{}, 128, 128, 2, 2, 3>"
 
 
 def parse():
@@ -43,15 +42,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
     return ap.parse_args()
-
-
-def tile_of(cout):
-    return 0 if cout > 64 else 1 if cout > 32 else 2 if cout > 16 else 3
-
-
-def kernel_name(nd, prec):
-    t = ["128, 128, 2, 2", "128, 64, 2, 2", "256, 32, 4, 1", "256, 16, 4, 1"][tile_of(nd.conv.out_channels)]
-    return f"conv_igemm_kernel<{'bf16' if prec == 'bf16' else 'f32'}, {t}, {nd.conv.kernel_size[0]}>"
 
 
 def cpu_baseline(args, seconds):
@@ -122,18 +112,22 @@ def main():
     labels = torch.empty(B, oh, ow, dtype=torch.uint8, device=dev)
     up_plane = model._up_plane(dev)
     stream = _lib.stream_ptr(dev)
-    nodes = plan.packed.graph.nodes
     works = node_work(plan)
-    dominant = DOMINANT_T.format("bf16" if args.precision == "bf16" else "f32")
-    dom_idx = {i for i, nd in enumerate(nodes) if kernel_name(nd, args.precision) == dominant}
+    lib = _lib.load()
+    import ctypes
 
+    def launched_name(i):
+        a = plan.stem_u8 if (i == 0 and plan.stem_u8 is not None) else plan.args[i]
+        return lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
+
+    names = [launched_name(i) for i in range(len(plan.args))]
     events = []
+    pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * len(names) * args.steps)]
 
     def hook(i, nd, before):
-        if i in dom_idx:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record()
-            events.append((i, before, ev))
+        ev = pool[len(events)]
+        ev.record()
+        events.append((i, before, ev))
 
     def step(timed):
         plan.ingest_u8(frames, INFO_MEAN, INFO_STD, False, stream)
@@ -158,15 +152,21 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
 
-    # dominant-kernel durations from the events recorded inside the timed region
-    durs, flops = [], []
+    # per-kernel durations from the events recorded inside the timed region; the dominant
+    # kernel is the template instance (as rocprofv3 names it) with the largest total time
+    per = {}
     pend = {}
     for i, before, ev in events:
         if before:
             pend[i] = ev
         else:
-            durs.append(pend.pop(i).elapsed_time(ev) * 1e-3)
-            flops.append(works[i][1])
+            g_ = per.setdefault(names[i], {"d": [], "f": [], "b": []})
+            g_["d"].append(pend.pop(i).elapsed_time(ev) * 1e-3)
+            g_["f"].append(works[i][1])
+            g_["b"].append(works[i][2])
+    dominant = max(per, key=lambda k: sum(per[k]["d"])) if per else None
+    durs = per[dominant]["d"] if dominant else []
+    flops = per[dominant]["f"] if dominant else []
     nr = network_roofline(plan)
     total_frames = world * B * args.steps
     out = {
@@ -195,7 +195,12 @@ def main():
         out["roofline"] = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 2), "peak": peak,
                            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
                            "launches": len(durs), "avg_launch_us": round(avg_d * 1e6, 2),
-                           "avg_launch_gflop": round(avg_f / 1e9, 3)}
+                           "avg_launch_gflop": round(avg_f / 1e9, 3),
+                           "share_of_step": round(sum(durs) / el, 3)}
+        out["kernels"] = {k: {"launches": len(v["d"]), "avg_us": round(sum(v["d"]) / len(v["d"]) * 1e6, 1),
+                              "tflops": round(sum(v["f"]) / sum(v["d"]) / 1e12, 1),
+                              "gbps": round(sum(v["b"]) / sum(v["d"]) / 1e9, 1)}
+                          for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]["d"]))}
     out["network_roofline"] = {"t_star_ms_per_frame": nr["t_star_s"] / B * 1e3,
                                "measured_ms_per_frame": el / args.steps / B * 1e3,
                                "frac": nr["t_star_s"] / (el / args.steps),

@@ -66,8 +66,10 @@ typedef struct drnmi_conv_args {
 } drnmi_conv_args;
 
 /* Algorithms behind drnmi_conv2d_bn_act:
- *  DRNMI_ALGO_IGEMM  generic NHWC implicit GEMM (any power-of-two cin >= 8, any ks/stride/dil;
- *                    bf16 or fp32).
+ *  DRNMI_ALGO_IGEMM  NHWC implicit GEMM (any power-of-two cin >= 8, any ks/stride/dil; bf16 or
+ *                    fp32).  tile -1 picks the bf16 LDS-DMA kernel (tiles 4..7: 128/256/64/32
+ *                    output channels x 256 pixels; cin >= 64, ks 1 or 3) when it applies, else a
+ *                    register-staged tile 0..3 by cout.
  *  DRNMI_ALGO_PATCH  bf16-only small-channel direct conv for the full-resolution layers
  *                    (lmodels/drn.py:132-137 layer0, :201-211 layer1/layer2): the input tile
  *                    plus halo is staged once in LDS and reused by all ks*ks taps; weights stay
@@ -81,6 +83,11 @@ typedef struct drnmi_conv_args {
 enum drnmi_algo { DRNMI_ALGO_IGEMM = 0, DRNMI_ALGO_PATCH = 1 };
 
 int drnmi_conv2d_bn_act(const drnmi_conv_args* args, void* stream);
+
+/* Name of the kernel (template instance) drnmi_conv2d_bn_act would launch for these
+ * arguments, e.g. "conv_big_kernel<3, 128, 2, 2>"; NULL if none.  No launch, no GPU needed.
+ * (Used by bench.py to attribute timed launches to kernels as rocprofv3 names them.) */
+const char* drnmi_conv_kernel_name(const drnmi_conv_args* args);
 
 /* Name of a tile configuration ("128x128", ...) or NULL; count via drnmi_conv_num_tiles. */
 const char* drnmi_conv_tile_name(int tile);

@@ -221,3 +221,35 @@ def test_stem_u8_fused_ingest():
     yb = ops.stem_u8(frames.flip(-1).contiguous().to(DEV), wt, sc.to(DEV), sh.to(DEV), O.INFO_MEAN,
                      O.INFO_STD, bgr=True)
     assert torch.equal(yb, y)
+
+
+@pytest.mark.parametrize("shape", [(64, 128, 3, 2, 1, 37, 51), (128, 256, 3, 1, 2, 33, 40),
+                                   (512, 512, 3, 1, 4, 24, 40), (256, 512, 1, 1, 1, 20, 30),
+                                   (64, 128, 1, 2, 1, 37, 51)])
+def test_dma_conv_matches_register_staged(shape):
+    """bf16 LDS-DMA kernel (tile 4) vs the register-staged bf16 tile 0 on the same inputs."""
+    cin, cout, ks, stride, dil, h, w = shape
+    pad = dil * (ks // 2)
+    x = _rand((3, cin, h, w), 61).bfloat16()
+    wt = _rand((cout, cin, ks, ks), 62, (2.0 / (ks * ks * cout)) ** 0.5)
+    sc = torch.rand(cout, generator=torch.Generator().manual_seed(63)) + 0.5
+    sh = torch.rand(cout, generator=torch.Generator().manual_seed(64)) - 0.5
+    ho = (h + 2 * pad - dil * (ks - 1) - 1) // stride + 1
+    wo = (w + 2 * pad - dil * (ks - 1) - 1) // stride + 1
+    res = _rand((3, ho, wo, cout), 65).bfloat16().to(DEV)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    outs = [ops.conv2d_bn_act(xd, wt.to(DEV), sc.to(DEV), sh.to(DEV), res, stride, pad, dil, True, tile=t)
+            for t in (0, 4)]
+    a, b = outs[0].float(), outs[1].float()
+    assert (a - b).abs().max().item() <= 1e-2 * a.abs().max().item()
+    ref = _ref_conv(x.float(), wt.bfloat16().float(), sc, sh, res.float().permute(0, 3, 1, 2).cpu(), stride,
+                    pad, dil, True)
+    assert (b.permute(0, 3, 1, 2).cpu() - ref).abs().max().item() <= 1.5e-2 * ref.abs().max().item()
+
+
+def test_forced_tile_larger_than_weights_is_rejected():
+    """A 256-channel tile over a 128-row packed weight must be refused, not read past it."""
+    x = torch.randn(1, 16, 16, 128, device=DEV).bfloat16()
+    wt = torch.randn(128, 128, 3, 3, device=DEV) * 0.05
+    with pytest.raises(RuntimeError, match="EINVAL"):
+        ops.conv2d_bn_act(x, wt, padding=1, tile=5)

@@ -22,6 +22,8 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdio>
+
 namespace drnmi {
 
 namespace {
@@ -253,6 +255,11 @@ constexpr TileDesc kTiles[] = {
     {128, 64, "128x64"},
     {256, 32, "256x32"},
     {256, 16, "256x16"},
+    // conv_big.hip (bf16, LDS-DMA, cin >= 64, ks 1/3): cout tile x 256 pixels
+    {128, 128, "dma128x256"},   // 4 waves, 3 stages
+    {256, 256, "dma256x256"},   // 8 waves, 2 stages
+    {64, 64, "dma64x256"},      // 4 waves, 3 stages
+    {32, 32, "dma32x256"},      // 4 waves, 3 stages (seg 1x1)
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -331,12 +338,29 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
       p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
     return DRNMI_EINVAL;
+  if (p.tile >= 4 || (p.tile < 0 && big_conv_supported(p)))
+    return big_conv_dispatch(p, p.tile < 0 ? -1 : p.tile - 4, reinterpret_cast<hipStream_t>(stream));
   const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;
-  if (tile >= kNumTiles || p.cout_pad % kTiles[tile].bn != 0) return DRNMI_EINVAL;
+  if (tile >= 4 || p.cout_pad % kTiles[tile].bn != 0) return DRNMI_EINVAL;
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   if (M >= (int64_t(1) << 31) / 2) return DRNMI_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipError_t e = p.dtype == DRNMI_BF16 ? dispatch_ks<bf16_t>(p, tile, s) : dispatch_ks<float>(p, tile, s);
   if (e == hipErrorInvalidValue) return DRNMI_ENOTSUP;
   return static_cast<int>(e);
+}
+
+extern "C" const char* drnmi_conv_kernel_name(const drnmi_conv_args* a) {
+  if (a == nullptr) return nullptr;
+  const drnmi_conv_args& p = *a;
+  if (p.algo == DRNMI_ALGO_PATCH) return patch_conv_name(p);
+  if (p.tile >= 4 || (p.tile < 0 && big_conv_supported(p))) return big_conv_name(p, p.tile < 0 ? -1 : p.tile - 4);
+  const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;
+  if (tile > 3 || (p.ks != 1 && p.ks != 3 && p.ks != 7)) return nullptr;
+  static const char* tn[4] = {"128, 128, 2, 2", "128, 64, 2, 2", "256, 32, 4, 1", "256, 16, 4, 1"};
+  static char buf[8][96];
+  static int slot = 0;
+  char* b = buf[slot++ & 7];
+  snprintf(b, 96, "conv_igemm_kernel<%s, %s, %d>", p.dtype == DRNMI_BF16 ? "bf16" : "f32", tn[tile], p.ks);
+  return b;
 }

@@ -5,4 +5,9 @@
 namespace drnmi {
 // Small-channel LDS-patch conv (patch_conv.hip); returns drnmi_status / hipError_t.
 int patch_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
+// bf16 LDS-DMA implicit GEMM for cin >= 64, cout % 128 == 0 (conv_big.hip).
+bool big_conv_supported(const drnmi_conv_args& p);
+int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s);  // variant -1 = auto
+const char* big_conv_name(const drnmi_conv_args& p, int variant);
+const char* patch_conv_name(const drnmi_conv_args& p);
 }  // namespace drnmi

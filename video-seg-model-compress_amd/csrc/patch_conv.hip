@@ -209,4 +209,13 @@ int patch_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   return static_cast<int>(e);
 }
 
+const char* patch_conv_name(const drnmi_conv_args& p) {
+  if (p.src_u8) return "patch_conv_kernel<4, 16, 7, 1, 4, 64, true>";
+  if (p.cin == 8 && p.cout == 16 && p.ks == 7) return "patch_conv_kernel<8, 16, 7, 1, 4, 64, false>";
+  if (p.cin == 16 && p.cout == 16 && p.ks == 3 && p.stride == 1) return "patch_conv_kernel<16, 16, 3, 1, 4, 64, false>";
+  if (p.cin == 16 && p.cout == 32 && p.ks == 3 && p.stride == 2) return "patch_conv_kernel<16, 32, 3, 2, 4, 64, false>";
+  if (p.cin == 32 && p.cout == 64 && p.ks == 3 && p.stride == 2) return "patch_conv_kernel<32, 64, 3, 2, 2, 64, false>";
+  return nullptr;
+}
+
 }  // namespace drnmi

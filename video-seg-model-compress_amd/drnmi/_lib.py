@@ -46,6 +46,7 @@ _VP, _I32, _I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
 SIGNATURES = {
     "drnmi_conv2d_bn_act": (ctypes.c_int, [ctypes.POINTER(ConvArgs), _VP]),
     "drnmi_conv_tile_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "drnmi_conv_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(ConvArgs)]),
     "drnmi_conv_num_tiles": (ctypes.c_int, []),
     "drnmi_frame_ingest_u8": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _VP, _VP, _I32, _I32, _VP]),
     "drnmi_nchw_to_nhwc": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _I32, _I32, _I32, _VP]),
