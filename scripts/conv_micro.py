@@ -10,7 +10,7 @@ import torch  # noqa: E402
 from drnmi import ops  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-TILES = [int(t) for t in os.environ.get("TILES", "0,4,5").split(",")]
+TILES = [int(t) for t in os.environ.get("TILES", "10,11,12,13").split(",")]
 SHAPES = [  # name, cin, cout, ks, stride, dil, H(in), W(in), residual
     ("l8 512x512 d1", 512, 512, 3, 1, 1, 128, 256, False),
     ("l6 512x512 d4 +res", 512, 512, 3, 1, 4, 128, 256, True),
@@ -19,9 +19,15 @@ SHAPES = [  # name, cin, cout, ks, stride, dil, H(in), W(in), residual
     ("l4 128x128 +res", 128, 128, 3, 1, 1, 128, 256, True),
     ("l4.0c1 64->128 s2", 64, 128, 3, 2, 1, 256, 512, False),
     ("l6 ds 256->512 1x1", 256, 512, 1, 1, 1, 128, 256, False),
+    ("l3 64x64 +res", 64, 64, 3, 1, 1, 256, 512, True),
+    ("l3.0c1 32->64 s2", 32, 64, 3, 2, 1, 512, 1024, False),
+    ("l3.0ds 32->64 1x1 s2", 32, 64, 1, 2, 1, 512, 1024, False),
 ]
 dev = "cuda"
+ONLY = os.environ.get("ONLY")
 for name, cin, cout, ks, st, dil, h, w, has_res in SHAPES:
+    if ONLY and not name.startswith(ONLY):
+        continue
     pad = dil * (ks // 2)
     x = torch.randn(B, h, w, cin, device=dev).bfloat16()
     wt = torch.randn(cout, cin, ks, ks, device=dev) * 0.05
@@ -32,6 +38,8 @@ for name, cin, cout, ks, st, dil, h, w, has_res in SHAPES:
     flops = 2.0 * B * ho * wo * cout * cin * ks * ks
     line = f"{name:22s}"
     times = {}
+    if ONLY == "l3" and cin == 32:
+        pass
     for rep in range(3):
         for t in TILES:
             try:

@@ -260,6 +260,15 @@ constexpr TileDesc kTiles[] = {
     {256, 256, "dma256x256"},   // 8 waves, 2 stages
     {64, 64, "dma64x256"},      // 4 waves, 3 stages
     {32, 32, "dma32x256"},      // 4 waves, 3 stages (seg 1x1)
+    {256, 256, "dma256x256k32"}, // 8 waves, 4 stages of K 32
+    {128, 128, "dma128x256k32"}, // 4 waves, 4 stages of K 32
+    {256, 256, "dma256x256il"},  // tile 5 with the DMA issue interleaved into the MFMA stream
+    {256, 256, "dma256x256ilp"}, // + s_setprio around MFMA groups
+    {128, 128, "dma128x256il"},
+    {128, 128, "dma128x256ilp"},
+    {64, 64, "dma64x256il"},
+    {32, 32, "dma32x256il"},
+    {64, 64, "dma64x256k32il"},  // cin 32 layers
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
