@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=4, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=8, help="frames per GPU per step")
     ap.add_argument("--arch", default="drn_d_22")
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--width", type=int, default=2048)
@@ -100,6 +100,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from drnmi import _lib
+    from drnmi.dist import max_over_ranks
     from drnmi.drnseg import INFO_MEAN, INFO_STD, build
     from drnmi.roofline import MFMA_PEAK, network_roofline, node_work
 
@@ -146,11 +147,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = t.item()
+    el = max_over_ranks(time.perf_counter() - t0, device=dev)   # the slowest rank defines the job
 
     # per-kernel durations from the events recorded inside the timed region; the dominant
     # kernel is the template instance (as rocprofv3 names it) with the largest total time

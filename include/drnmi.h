@@ -135,6 +135,13 @@ int drnmi_mask_apply_bits_f32(int32_t ntensors, float* const* weights,
                               const uint32_t* const* mask_bits, const int64_t* numels,
                               void* stream);
 
+/* Eval: accumulate the nclass x nclass confusion matrix hist[label*nclass + pred] += 1 over the
+ * pixels with 0 <= label < nclass and pred < nclass (int64 hist, NOT cleared: accumulates across
+ * calls like the reference's running hist).  Replaces fast_hist (semantic_seg.py:293-296) used by
+ * test()/val_miou() (:455, :655).  pred/label dtypes: DRNMI_U8 or DRNMI_I64; nclass <= 32. */
+int drnmi_confusion_matrix(const void* pred, int32_t pred_dtype, const void* label, int32_t label_dtype,
+                           int64_t npix, int32_t nclass, int64_t* hist, void* stream);
+
 /* Library version string, e.g. "drnmi 0.1.0 gfx950". */
 const char* drnmi_version(void);
 

@@ -261,3 +261,18 @@ def test_forced_tile_larger_than_weights_is_rejected():
     wt = torch.randn(128, 128, 3, 3, device=DEV) * 0.05
     with pytest.raises(RuntimeError, match="EINVAL"):
         ops.conv2d_bn_act(x, wt, padding=1, tile=5)
+
+
+@pytest.mark.parametrize("dt", [(torch.uint8, torch.uint8), (torch.int64, torch.int64), (torch.uint8, torch.int64)])
+def test_confusion_matrix_matches_fast_hist(dt):
+    from drnmi import metrics
+    g = torch.Generator().manual_seed(9)
+    pred = torch.randint(0, 19, (2, 61, 97), generator=g)
+    label = torch.randint(0, 21, (2, 61, 97), generator=g)
+    label[label >= 19] = 255                      # ignore label
+    ref = O.fast_hist(pred.numpy().reshape(-1), label.numpy().reshape(-1), 19)
+    h = metrics.fast_hist(pred.to(DEV, dt[0]), label.to(DEV, dt[1]), 19)
+    h = metrics.fast_hist(pred.to(DEV, dt[0]), label.to(DEV, dt[1]), 19, hist=h)   # accumulates
+    np.testing.assert_array_equal(h.cpu().numpy(), 2 * ref)
+    np.testing.assert_allclose(metrics.per_class_iu(h), O.per_class_iu(2 * ref))
+    assert metrics.miou(h) == round(float(np.nanmean(O.per_class_iu(ref))) * 100, 2)

@@ -308,6 +308,29 @@ __global__ void __launch_bounds__(256) mask_apply_bits_kernel(const MaskBatchBit
   }
 }
 
+// ---------------------------------------------------------------- confusion matrix (eval)
+// hist[label * n + pred] += 1 over pixels with 0 <= label < n and pred < n
+// (semantic_seg.py:293-296 fast_hist; per-block LDS histogram, one global atomic per bin).
+constexpr int kMaxHistClasses = 32;
+
+template <typename TP, typename TL>
+__global__ void __launch_bounds__(256)
+confusion_kernel(const TP* __restrict__ pred, const TL* __restrict__ label, int64_t npix, int n,
+                 unsigned long long* __restrict__ hist) {
+  __shared__ unsigned int h[kMaxHistClasses * kMaxHistClasses];
+  for (int i = threadIdx.x; i < n * n; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < npix; i += stride) {
+    const int64_t l = static_cast<int64_t>(label[i]);
+    const int64_t p = static_cast<int64_t>(pred[i]);
+    if (l >= 0 && l < n && p >= 0 && p < n) atomicAdd(&h[l * n + p], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n * n; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], static_cast<unsigned long long>(h[i]));
+}
+
 inline unsigned grid1d(int64_t n, int block = 256) {
   return static_cast<unsigned>((n + block - 1) / block);
 }
@@ -459,3 +482,30 @@ extern "C" int drnmi_mask_apply_bits_f32(int32_t ntensors, float* const* weights
 }
 
 extern "C" const char* drnmi_version(void) { return "drnmi 0.1.0 gfx950"; }
+
+extern "C" int drnmi_confusion_matrix(const void* pred, int32_t pred_dtype, const void* label,
+                                      int32_t label_dtype, int64_t npix, int32_t nclass, int64_t* hist,
+                                      void* stream) {
+  if (pred == nullptr || label == nullptr || hist == nullptr || npix < 0) return DRNMI_EINVAL;
+  if (nclass <= 0 || nclass > kMaxHistClasses) return DRNMI_ENOTSUP;
+  if ((pred_dtype != DRNMI_U8 && pred_dtype != DRNMI_I64) || (label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64))
+    return DRNMI_EINVAL;
+  if (npix == 0) return DRNMI_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  unsigned g = grid1d(npix);
+  g = g > 2048 ? 2048 : g;
+  auto* h = reinterpret_cast<unsigned long long*>(hist);
+  if (pred_dtype == DRNMI_U8 && label_dtype == DRNMI_U8)
+    hipLaunchKernelGGL((confusion_kernel<uint8_t, uint8_t>), dim3(g), dim3(256), 0, s,
+                       (const uint8_t*)pred, (const uint8_t*)label, npix, nclass, h);
+  else if (pred_dtype == DRNMI_U8)
+    hipLaunchKernelGGL((confusion_kernel<uint8_t, int64_t>), dim3(g), dim3(256), 0, s,
+                       (const uint8_t*)pred, (const int64_t*)label, npix, nclass, h);
+  else if (label_dtype == DRNMI_U8)
+    hipLaunchKernelGGL((confusion_kernel<int64_t, uint8_t>), dim3(g), dim3(256), 0, s,
+                       (const int64_t*)pred, (const uint8_t*)label, npix, nclass, h);
+  else
+    hipLaunchKernelGGL((confusion_kernel<int64_t, int64_t>), dim3(g), dim3(256), 0, s,
+                       (const int64_t*)pred, (const int64_t*)label, npix, nclass, h);
+  return static_cast<int>(hipGetLastError());
+}

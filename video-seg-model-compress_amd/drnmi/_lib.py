@@ -54,6 +54,7 @@ SIGNATURES = {
     "drnmi_up8_logsoftmax_argmax": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_mask_apply_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP]),
     "drnmi_mask_apply_bits_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP]),
+    "drnmi_confusion_matrix": (ctypes.c_int, [_VP, _I32, _VP, _I32, _I64, _I32, _VP, _VP]),
     "drnmi_version": (ctypes.c_char_p, []),
 }
 
