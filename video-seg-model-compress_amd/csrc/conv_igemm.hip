@@ -255,20 +255,11 @@ constexpr TileDesc kTiles[] = {
     {128, 64, "128x64"},
     {256, 32, "256x32"},
     {256, 16, "256x16"},
-    // conv_big.hip (bf16, LDS-DMA, cin >= 64, ks 1/3): cout tile x 256 pixels
-    {128, 128, "dma128x256"},   // 4 waves, 3 stages
-    {256, 256, "dma256x256"},   // 8 waves, 2 stages
-    {64, 64, "dma64x256"},      // 4 waves, 3 stages
-    {32, 32, "dma32x256"},      // 4 waves, 3 stages (seg 1x1)
-    {256, 256, "dma256x256k32"}, // 8 waves, 4 stages of K 32
-    {128, 128, "dma128x256k32"}, // 4 waves, 4 stages of K 32
-    {256, 256, "dma256x256il"},  // tile 5 with the DMA issue interleaved into the MFMA stream
-    {256, 256, "dma256x256ilp"}, // + s_setprio around MFMA groups
-    {128, 128, "dma128x256il"},
-    {128, 128, "dma128x256ilp"},
-    {64, 64, "dma64x256il"},
-    {32, 32, "dma32x256il"},
-    {64, 64, "dma64x256k32il"},  // cin 32 layers
+    // conv_big.hip (bf16, LDS-DMA implicit GEMM, cin >= 32, ks 1/3): cout tile x 256 pixels
+    {128, 128, "dma128"}, {256, 256, "dma256"}, {64, 64, "dma64k32"}, {32, 32, "dma32"},
+    {256, 256, "dma256k32"}, {128, 128, "dma128k32"},
+    {128, 128, "dma128p"}, {256, 256, "dma256p"}, {64, 64, "dma64k32p"}, {32, 32, "dma32p"},
+    {256, 256, "dma256k32p"}, {128, 128, "dma128k32p"},   // p = persistent
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 

@@ -66,7 +66,7 @@ def load(path: str | None = None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("DRNMI_LIB") or LIB_PATH   # DRNMI_LIB: diagnostic builds only
     if not os.path.exists(path):
         raise RuntimeError(
             f"drnmi: HIP library not built ({path}); run __graft_entry__.build() or "
