@@ -225,7 +225,8 @@ def test_stem_u8_fused_ingest():
 
 @pytest.mark.parametrize("shape", [(64, 128, 3, 2, 1, 37, 51), (128, 256, 3, 1, 2, 33, 40),
                                    (512, 512, 3, 1, 4, 24, 40), (256, 512, 1, 1, 1, 20, 30),
-                                   (64, 128, 1, 2, 1, 37, 51), (32, 64, 3, 2, 1, 41, 53), (32, 64, 1, 2, 1, 41, 53)])
+                                   (64, 128, 1, 2, 1, 37, 51), (32, 64, 3, 2, 1, 41, 53), (32, 64, 1, 2, 1, 41, 53),
+                                   (64, 256, 1, 1, 1, 19, 23), (128, 256, 3, 1, 1, 29, 35)])
 def test_dma_conv_matches_register_staged(shape):
     """bf16 LDS-DMA kernel (tile 4) vs the register-staged bf16 tile 0 on the same inputs."""
     cin, cout, ks, stride, dil, h, w = shape
@@ -242,7 +243,8 @@ def test_dma_conv_matches_register_staged(shape):
     ref = _ref_conv(x.float(), wt.bfloat16().float(), sc, sh, res.float().permute(0, 3, 1, 2).cpu(), stride,
                     pad, dil, True)
     ran = 0
-    for t in range(4, 16):        # every LDS-DMA variant that accepts this shape
+    from drnmi import _lib
+    for t in range(4, _lib.load().drnmi_conv_num_tiles()):   # every LDS-DMA variant that takes the shape
         try:
             b = ops.conv2d_bn_act(xd, wt.to(DEV), sc.to(DEV), sh.to(DEV), res, stride, pad, dil, True,
                                   tile=t).float()

@@ -66,6 +66,67 @@ __device__ __forceinline__ int xcd_remap2(int bid, int nwg) {
   return base + bid / 8;
 }
 
+// Epilogue shared by the conv kernels: lane owns channels co..co+3 of pixel m for FM x 4
+// accumulator fragments (folded BN scale/shift, optional residual, ReLU); bf16 NHWC rows get
+// one 8-byte store per fragment, other layouts (fp32 / strided seg logits) element stores.
+template <int FM, int WCO>
+__device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4 (&acc)[FM][4], int cur_px0,
+                                           int cur_co0, int wc, int wp, int fr, int fq) {
+  const int M = p.n * p.ho * p.wo;
+  const int hw_o = p.ho * p.wo;
+  const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
+  const bool nhwc16 = p.out_dtype == DRNMI_BF16 && p.y_sc == 1;
+#pragma unroll
+  for (int fn = 0; fn < 4; ++fn) {
+    const int m = cur_px0 + wp * 64 + fn * 16 + fr;
+    if (m >= M) continue;
+    const int n = m / hw_o;
+    const int q = m - n * hw_o;
+    const int64_t ybase = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int co = cur_co0 + wc * WCO + fm * 16 + fq * 4;
+      if (co >= p.cout) continue;
+      const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);   // padded to cout_pad
+      const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+      float v[4] = {acc[fm][fn][0] * sc.x + sh.x, acc[fm][fn][1] * sc.y + sh.y,
+                    acc[fm][fn][2] * sc.z + sh.z, acc[fm][fn][3] * sc.w + sh.w};
+      const bool full = co + 3 < p.cout;
+      if (res != nullptr) {
+        if (full) {
+          const uint2 rv = *reinterpret_cast<const uint2*>(res + static_cast<int64_t>(m) * p.cout + co);
+          v[0] += bf16_to_f32(static_cast<uint16_t>(rv.x & 0xffff));
+          v[1] += bf16_to_f32(static_cast<uint16_t>(rv.x >> 16));
+          v[2] += bf16_to_f32(static_cast<uint16_t>(rv.y & 0xffff));
+          v[3] += bf16_to_f32(static_cast<uint16_t>(rv.y >> 16));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (co + j < p.cout) v[j] += bf16_to_f32(res[static_cast<int64_t>(m) * p.cout + co + j]);
+        }
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
+      if (nhwc16 && full) {
+        uint2 o;
+        o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+        o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.y) + ybase + co) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (co + j >= p.cout) break;
+          const int64_t off = ybase + static_cast<int64_t>(co + j) * p.y_sc;
+          if (p.out_dtype == DRNMI_BF16) reinterpret_cast<uint16_t*>(p.y)[off] = f32_to_bf16(v[j]);
+          else reinterpret_cast<float*>(p.y)[off] = v[j];
+        }
+      }
+    }
+  }
+}
+
 template <int WCO, int WC, int NST, int BK>
 struct BigCfg {
   static constexpr int BCO = WCO * WC;              // output channels per tile
@@ -152,14 +213,17 @@ conv_big_kernel(const drnmi_conv_args p) {
     }
   };
 
+  // K step kt = (channel block cb, tap): taps innermost, so the KS*KS steps that re-read one
+  // channel slice of the same pixel neighbourhood run back to back (L2 hits, not MALL).
   struct StepP { int k0, dh, dw; int64_t toff; };
   auto step_params = [&](int kt) {
     StepP sp;
-    sp.k0 = kt * BK;
-    const int tap = sp.k0 >> lc;
+    const int cb = kt / (KS * KS);
+    const int tap = kt - cb * (KS * KS);
+    sp.k0 = (tap << lc) + cb * BK;                 // packed weight column: tap * cin + channel
     sp.dh = (tap / KS) * dil;
     sp.dw = (tap - (tap / KS) * KS) * dil;
-    sp.toff = (static_cast<int64_t>(sp.dh) * W + sp.dw) * cin + (sp.k0 & (cin - 1));   // uniform over rows
+    sp.toff = (static_cast<int64_t>(sp.dh) * W + sp.dw) * cin + cb * BK;   // uniform over rows
     return sp;
   };
   // one DMA instruction ("piece") of a step: pieces [0, A_INSTR) weights, then pixel rows
@@ -182,9 +246,6 @@ conv_big_kernel(const drnmi_conv_args p) {
   };
 
   f32x4 acc[C::FM][4];
-  const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
-  const bool nhwc16 = p.out_dtype == DRNMI_BF16 && p.y_sc == 1;
-
   int tl = blockIdx.x;
   int tile = xcd_remap2(tl, ntiles);
   int px0 = (tile / nco) * kBPX;
@@ -278,58 +339,222 @@ conv_big_kernel(const drnmi_conv_args p) {
       }
     }
 
-    // --- epilogue: lane owns channels co..co+3 of pixel m, for FM x 4 fragments
-#pragma unroll
-    for (int fn = 0; fn < 4; ++fn) {
-      const int m = cur_px0 + wp * 64 + fn * 16 + fr;
-      if (m >= M) continue;
-      const int n = m / hw_o;
-      const int q = m - n * hw_o;
-      const int64_t ybase = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp;
-#pragma unroll
-      for (int fm = 0; fm < C::FM; ++fm) {
-        const int co = cur_co0 + wc * WCO + fm * 16 + fq * 4;
-        if (co >= p.cout) continue;
-        const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);   // padded to cout_pad
-        const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
-        float v[4] = {acc[fm][fn][0] * sc.x + sh.x, acc[fm][fn][1] * sc.y + sh.y,
-                      acc[fm][fn][2] * sc.z + sh.z, acc[fm][fn][3] * sc.w + sh.w};
-        const bool full = co + 3 < p.cout;
-        if (res != nullptr) {
-          if (full) {
-            const uint2 rv = *reinterpret_cast<const uint2*>(res + static_cast<int64_t>(m) * p.cout + co);
-            v[0] += bf16_to_f32(static_cast<uint16_t>(rv.x & 0xffff));
-            v[1] += bf16_to_f32(static_cast<uint16_t>(rv.x >> 16));
-            v[2] += bf16_to_f32(static_cast<uint16_t>(rv.y & 0xffff));
-            v[3] += bf16_to_f32(static_cast<uint16_t>(rv.y >> 16));
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (co + j < p.cout) v[j] += bf16_to_f32(res[static_cast<int64_t>(m) * p.cout + co + j]);
-          }
-        }
-        if (p.relu) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-        }
-        if (nhwc16 && full) {
-          uint2 o;
-          o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
-          o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.y) + ybase + co) = o;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (co + j >= p.cout) break;
-            const int64_t off = ybase + static_cast<int64_t>(co + j) * p.y_sc;
-            if (p.out_dtype == DRNMI_BF16) reinterpret_cast<uint16_t*>(p.y)[off] = f32_to_bf16(v[j]);
-            else reinterpret_cast<float*>(p.y)[off] = v[j];
-          }
-        }
-      }
-    }
+    store_tile<C::FM, WCO>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
     if (!more) break;
   }
+}
+
+// --- Ping-pong 256 x 256 schedule (variant "pp256").
+//
+// Same tile, LDS image and fragment layout as conv_big_kernel<KS, 128, 2, 2, 64>, but each
+// 64-deep K step runs as 4 phases, one per quadrant of the wave's 128 x 64 output block
+// (16 MFMAs each), and every phase is {load segment} s_barrier {MFMA segment} s_barrier.
+// The two waves of a SIMD (w and w + 4: the two channel halves wc) run one barrier apart,
+// so on every SIMD one wave issues its LDS fragment reads and DMA pieces while the other
+// one runs its MFMA cluster (cdna_hip_programming.md "256^2 8-phase template", T3-T5).
+// The stage is split in halves that free up at different phases: the first half (channel
+// rows 0-63 of each wc block, pixel rows 0-31 of each 64-pixel block) is read in phase 0,
+// the second half in phases 1-2.  Pieces in flight: phases 0-1 of step s stage the second
+// half of step s+1, phases 2-3 the first half of step s+2, so every piece has >= 6
+// segments to land, with counted vmcnt waits (never 0 in steady state).
+template <int KS>
+__global__ void __launch_bounds__(512, 1)
+conv_pp_kernel(const drnmi_conv_args p) {
+  constexpr int BK = 64, ROWB = 128, A_BYTES = 256 * ROWB, STAGE = 2 * A_BYTES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar branches)
+  const int wc = wave >> 2;
+  const int wp = wave & 3;
+  const int M = p.n * p.ho * p.wo;
+  const int hw_o = p.ho * p.wo;
+  const int nco = p.cout / 256;
+  const int npx = (M + kBPX - 1) / kBPX;
+  const int ntiles = npx * nco;
+  const int tile = xcd_remap2(blockIdx.x, ntiles);
+  const int px0 = (tile / nco) * kBPX;
+  const int co0 = (tile % nco) * 256;
+
+  const int cin = p.cin;
+  const int lc = 31 - __builtin_clz(cin);
+  const int H = p.h, W = p.w, dil = p.dil;
+  const uint16_t* __restrict__ x = reinterpret_cast<const uint16_t*>(p.x);
+  const uint16_t* __restrict__ wt = reinterpret_cast<const uint16_t*>(p.wgt);
+  const int nk = p.k_pad / BK;
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+
+  // DMA pieces: half h, slot j: weight rows ((2w+j)/8)*128 + h*64 + ((2w+j)%8)*8 .. +8 and
+  // pixel rows ((2w+j)/4)*64 + h*32 + ((2w+j)%4)*8 .. +8 (lane -> row + lane/8, chunk lane%8)
+  const int lrow = lane >> 3;
+  const int lslot = lane & 7;
+  int a_off[2][2], a_row0[2][2], b_row0[2][2], b_ih0[2][2], b_iw0[2][2];
+  const uint16_t* b_base[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = 2 * wave + j;
+      a_row0[h][j] = (q >> 3) * 128 + h * 64 + (q & 7) * 8;
+      const int ra = a_row0[h][j] + lrow;
+      a_off[h][j] = (co0 + ra) * p.k_pad + swz<BK>(ra, lslot) * 8;
+      b_row0[h][j] = (q >> 2) * 64 + h * 32 + (q & 3) * 8;
+      const int rb = b_row0[h][j] + lrow;
+      const int m = px0 + rb;
+      b_ih0[h][j] = -(1 << 28);
+      b_iw0[h][j] = -(1 << 28);
+      b_base[h][j] = x;
+      if (m < M) {
+        const int n = m / hw_o;
+        const int qq = m - n * hw_o;
+        const int oh = qq / p.wo;
+        const int ow = qq - oh * p.wo;
+        b_ih0[h][j] = oh * p.stride - p.pad;
+        b_iw0[h][j] = ow * p.stride - p.pad;
+        b_base[h][j] = x + ((static_cast<int64_t>(n) * H + b_ih0[h][j]) * W + b_iw0[h][j]) * cin +
+                       swz<BK>(rb, lslot) * 8;
+      }
+    }
+  const char* zero_src = reinterpret_cast<const char*>(g_zero_page) + lane * 16;
+
+  // stage pieces (h, j) of K step kt (one weight piece + one pixel piece)
+  auto issue = [&](int kt, int h, int j) {
+    const int cb = kt / (KS * KS);                 // channel block outer, tap inner (as conv_big)
+    const int tap = kt - cb * (KS * KS);
+    const int k0 = (tap << lc) + cb * BK;
+    const int dh = (tap / KS) * dil;
+    const int dw = (tap - (tap / KS) * KS) * dil;
+    const int64_t toff = (static_cast<int64_t>(dh) * W + dw) * cin + cb * BK;
+    char* sa = smem + (kt & 1) * STAGE;
+    glds16(wt + a_off[h][j] + k0, sa + a_row0[h][j] * ROWB);
+    const bool ok = static_cast<unsigned>(b_ih0[h][j] + dh) < static_cast<unsigned>(H) &&
+                    static_cast<unsigned>(b_iw0[h][j] + dw) < static_cast<unsigned>(W);
+    const void* src = ok ? static_cast<const void*>(b_base[h][j] + toff) : static_cast<const void*>(zero_src);
+    glds16(src, sa + A_BYTES + b_row0[h][j] * ROWB);
+  };
+  auto barrier = [&]() {
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // fragments: channel half hh (4 fragments x 2 substeps), pixel half g (2 x 2)
+  auto load_a = [&](bf16x8 (&dst)[4][2], const char* sa, int hh) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const int r = wc * 128 + hh * 64 + f * 16 + fr;
+        dst[f][sub] = *reinterpret_cast<const bf16x8*>(sa + r * ROWB + swz<BK>(r, sub * 4 + fq) * 16);
+      }
+  };
+  auto load_b = [&](bf16x8 (&dst)[2][2], const char* sa, int g) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const int r = wp * 64 + g * 32 + f * 16 + fr;
+        dst[f][sub] = *reinterpret_cast<const bf16x8*>(sa + A_BYTES + r * ROWB + swz<BK>(r, sub * 4 + fq) * 16);
+      }
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfma = [&](const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int hh, int g) {
+    if constexpr ((DRNMI_ABLATE & 2) != 0) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) asm volatile("" :: "v"(a[f][0]), "v"(a[f][1]));
+#pragma unroll
+      for (int e = 0; e < 2; ++e) asm volatile("" :: "v"(b[e][0]), "v"(b[e][1]));
+      return;
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          acc[hh * 4 + f][g * 2 + e] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f][sub], b[e][sub], acc[hh * 4 + f][g * 2 + e], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: step 0 (both halves) and the first half of step 1
+  issue(0, 0, 0);
+  issue(0, 0, 1);
+  issue(0, 1, 0);
+  issue(0, 1, 1);
+  if (nk > 1) {
+    issue(1, 0, 0);
+    issue(1, 0, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  barrier();
+  if (wc == 1) barrier();   // the second channel half runs one barrier behind
+
+  bf16x8 a_f[4][2], b0[2][2], b1[2][2];
+  for (int s = 0; s < nk; ++s) {
+    const char* sa = smem + (s & 1) * STAGE;
+    const bool n1 = (DRNMI_ABLATE & 1) ? false : s + 1 < nk, n2 = (DRNMI_ABLATE & 1) ? false : s + 2 < nk;
+    // phase 0: quadrant (channels 0-63, pixels 0-31); retire the second half of step s
+    load_a(a_f, sa, 0);
+    load_b(b0, sa, 0);
+    if (n1) {
+      issue(s + 1, 1, 0);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    mfma(a_f, b0, 0, 0);
+    barrier();
+    // phase 1: (channels 0-63, pixels 32-63)
+    load_b(b1, sa, 1);
+    if (n1) issue(s + 1, 1, 1);
+    barrier();
+    mfma(a_f, b1, 0, 1);
+    barrier();
+    // phase 2: (channels 64-127, pixels 32-63)
+    load_a(a_f, sa, 1);
+    if (n2) issue(s + 2, 0, 0);
+    barrier();
+    mfma(a_f, b1, 1, 1);
+    barrier();
+    // phase 3: (channels 64-127, pixels 0-31); retire the first half of step s+1
+    if (n2) {
+      issue(s + 2, 0, 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (n1) {
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    barrier();
+    mfma(a_f, b0, 1, 0);
+    barrier();
+  }
+  if (wc == 0) barrier();   // balance the barrier count of the two halves
+
+  store_tile<8, 128>(p, acc, px0, co0, wc, wp, fr, fq);
+}
+
+template <int KS>
+hipError_t launch_pp(const drnmi_conv_args& p, hipStream_t s) {
+  constexpr int LDS = 2 * 2 * 256 * 128;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_pp_kernel<KS>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const int64_t blocks = ((M + kBPX - 1) / kBPX) * (p.cout / 256);
+  hipLaunchKernelGGL((conv_pp_kernel<KS>), dim3(static_cast<unsigned>(blocks)), dim3(512), LDS, s, p);
+  return hipGetLastError();
 }
 
 int g_num_cus = 0;
@@ -384,7 +609,9 @@ constexpr Variant kVariants[] = {
     {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, true>", "conv_big_kernel<1, 32, 1, 3, 64, true>"},
     {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, true>", "conv_big_kernel<1, 128, 2, 4, 32, true>"},
     {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, true>", "conv_big_kernel<1, 128, 1, 4, 32, true>"},
+    {256, 64, "conv_pp_kernel<3>", "conv_pp_kernel<1>"},
 };
+constexpr int kPingPong = 12;
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 template <int KS, bool PERSIST>
@@ -421,9 +648,14 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   if (p.cin < v.bk) return DRNMI_ENOTSUP;                            // a K step must fit in one tap
   // every weight row a tile's DMA reads must exist: ceil(cout / BCO) * BCO <= cout_pad
   if ((p.cout + v.bco - 1) / v.bco * v.bco > p.cout_pad) return DRNMI_EINVAL;
+  hipError_t e;
+  if (variant == kPingPong) {
+    if (p.cout % 256 != 0) return DRNMI_ENOTSUP;
+    e = p.ks == 3 ? launch_pp<3>(p, s) : launch_pp<1>(p, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
   const int base = variant % 6;
   const bool persist = variant >= 6;
-  hipError_t e;
   if (p.ks == 3) e = persist ? launch_base<3, true>(p, base, s) : launch_base<3, false>(p, base, s);
   else e = persist ? launch_base<1, true>(p, base, s) : launch_base<1, false>(p, base, s);
   return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);

@@ -260,6 +260,7 @@ constexpr TileDesc kTiles[] = {
     {256, 256, "dma256k32"}, {128, 128, "dma128k32"},
     {128, 128, "dma128p"}, {256, 256, "dma256p"}, {64, 64, "dma64k32p"}, {32, 32, "dma32p"},
     {256, 256, "dma256k32p"}, {128, 128, "dma128k32p"},   // p = persistent
+    {256, 256, "pp256"},                                   // ping-pong 4-phase schedule
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
