@@ -46,7 +46,8 @@ enum drnmi_status {
 typedef struct drnmi_conv_args {
   const void* x;       /* NHWC input [n][h][w][cin]                                   */
   const void* wgt;     /* packed weights [cout_pad][k_pad]                            */
-  const float* scale;  /* [cout_pad] folded BN scale                                  */
+  const float* scale;  /* [cout_pad] folded BN scale, or NULL = 1 (scale pre-folded    */
+                       /* into wgt; lets the bf16 kernels start from shift + res)    */
   const float* shift;  /* [cout_pad] folded BN shift (or conv bias)                   */
   const void* res;     /* optional NHWC residual [n*ho*wo][cout] in x's dtype, or NULL */
   void* y;             /* output                                                      */

@@ -226,7 +226,9 @@ def test_stem_u8_fused_ingest():
 @pytest.mark.parametrize("shape", [(64, 128, 3, 2, 1, 37, 51), (128, 256, 3, 1, 2, 33, 40),
                                    (512, 512, 3, 1, 4, 24, 40), (256, 512, 1, 1, 1, 20, 30),
                                    (64, 128, 1, 2, 1, 37, 51), (32, 64, 3, 2, 1, 41, 53), (32, 64, 1, 2, 1, 41, 53),
-                                   (64, 256, 1, 1, 1, 19, 23), (128, 256, 3, 1, 1, 29, 35)])
+                                   (64, 256, 1, 1, 1, 19, 23), (128, 256, 3, 1, 1, 29, 35),
+                                   (64, 64, 3, 1, 1, 37, 70), (128, 128, 3, 1, 1, 21, 131),
+                                   (64, 128, 3, 1, 2, 19, 67), (128, 64, 3, 1, 1, 9, 200)])
 def test_dma_conv_matches_register_staged(shape):
     """bf16 LDS-DMA kernel (tile 4) vs the register-staged bf16 tile 0 on the same inputs."""
     cin, cout, ks, stride, dil, h, w = shape
@@ -255,6 +257,37 @@ def test_dma_conv_matches_register_staged(shape):
         assert (a - b).abs().max().item() <= 1e-2 * a.abs().max().item(), f"tile {t}"
         assert (b.permute(0, 3, 1, 2).cpu() - ref).abs().max().item() <= 1.5e-2 * ref.abs().max().item()
     assert ran >= (1 if cin < 64 else 3)
+
+
+@pytest.mark.parametrize("shape", [(512, 512, 3, 1, 4, 20, 37), (256, 256, 3, 1, 2, 33, 40), (256, 512, 1, 1, 1, 20, 30),
+                                   (64, 64, 3, 1, 1, 37, 70), (128, 128, 3, 1, 1, 21, 131), (64, 128, 3, 2, 1, 37, 51),
+                                   (32, 64, 1, 2, 1, 41, 53), (512, 19, 1, 1, 1, 17, 23)])
+def test_null_scale_seeds_accumulator(shape):
+    """scale = NULL (BN scale folded into the weights): the LDS-DMA kernels start from
+    shift + residual; result matches the scaled launch within bf16 rounding, every variant."""
+    from drnmi import _lib
+    cin, cout, ks, stride, dil, h, w = shape
+    pad = dil * (ks // 2)
+    x = _rand((2, h, w, cin), 71).bfloat16().to(DEV)
+    wt = _rand((cout, cin, ks, ks), 72, (2.0 / (ks * ks * cout)) ** 0.5).to(DEV)
+    sc = (torch.rand(cout, generator=torch.Generator().manual_seed(73)) + 0.5).to(DEV)
+    sh = (torch.rand(cout, generator=torch.Generator().manual_seed(74)) - 0.5).to(DEV)
+    ho = (h + 2 * pad - dil * (ks - 1) - 1) // stride + 1
+    wo = (w + 2 * pad - dil * (ks - 1) - 1) // stride + 1
+    seg = cout == 19
+    res = None if seg else _rand((2, ho, wo, cout), 75).bfloat16().to(DEV)
+    ran = 0
+    for t in [-1] + list(range(4, _lib.load().drnmi_conv_num_tiles())):
+        kw = dict(stride=stride, padding=pad, dilation=dil, relu=not seg, out_nchw_fp32=seg, tile=t)
+        try:
+            a = ops.conv2d_bn_act(x, wt, sc, sh, res, **kw).float()
+            b = ops.conv2d_bn_act(x, wt, sc, sh, res, fold_scale=True, **kw).float()
+        except RuntimeError as e:
+            assert "EINVAL" in str(e) or "ENOTSUP" in str(e)
+            continue
+        ran += 1
+        assert (a - b).abs().max().item() <= 1.5e-2 * a.abs().max().item(), f"tile {t}"
+    assert ran >= 2
 
 
 def test_forced_tile_larger_than_weights_is_rejected():

@@ -69,6 +69,57 @@ __device__ __forceinline__ int xcd_remap2(int bid, int nwg) {
 // Epilogue shared by the conv kernels: lane owns channels co..co+3 of pixel m for FM x 4
 // accumulator fragments (folded BN scale/shift, optional residual, ReLU); bf16 NHWC rows get
 // one 8-byte store per fragment, other layouts (fp32 / strided seg logits) element stores.
+// Accumulator start value.  With a NULL scale (BN scale pre-folded into the weights) the
+// tile starts from shift + residual: the residual loads go out with the prologue DMA and
+// hide under it, and the epilogue is a plain ReLU + convert + store.
+template <int FM, int WCO>
+__device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)[FM][4], int px0, int co0,
+                                          int wc, int wp, int fr, int fq) {
+  if (p.scale != nullptr) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  const int M = p.n * p.ho * p.wo;
+  const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm) {
+    const int co = co0 + wc * WCO + fm * 16 + fq * 4;
+    const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);   // padded to cout_pad
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = f32x4{sh.x, sh.y, sh.z, sh.w};
+  }
+  if (res == nullptr) return;
+  uint2 rv[FM][4];
+#pragma unroll
+  for (int fn = 0; fn < 4; ++fn) {
+    const int m = px0 + wp * 64 + fn * 16 + fr;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int co = co0 + wc * WCO + fm * 16 + fq * 4;
+      rv[fm][fn] = make_uint2(0, 0);
+      if (m < M && co + 3 < p.cout) rv[fm][fn] = *reinterpret_cast<const uint2*>(res + static_cast<int64_t>(m) * p.cout + co);
+      else if (m < M) {
+        uint16_t t[4] = {0, 0, 0, 0};
+        for (int j = 0; j < 4; ++j)
+          if (co + j < p.cout) t[j] = res[static_cast<int64_t>(m) * p.cout + co + j];
+        rv[fm][fn] = make_uint2(t[0] | (static_cast<uint32_t>(t[1]) << 16), t[2] | (static_cast<uint32_t>(t[3]) << 16));
+      }
+    }
+  }
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) {
+      acc[fm][fn][0] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x & 0xffff));
+      acc[fm][fn][1] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x >> 16));
+      acc[fm][fn][2] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y & 0xffff));
+      acc[fm][fn][3] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y >> 16));
+    }
+}
+
 template <int FM, int WCO>
 __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4 (&acc)[FM][4], int cur_px0,
                                            int cur_co0, int wc, int wp, int fr, int fq) {
@@ -87,12 +138,17 @@ __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4
     for (int fm = 0; fm < FM; ++fm) {
       const int co = cur_co0 + wc * WCO + fm * 16 + fq * 4;
       if (co >= p.cout) continue;
-      const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);   // padded to cout_pad
-      const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
-      float v[4] = {acc[fm][fn][0] * sc.x + sh.x, acc[fm][fn][1] * sc.y + sh.y,
-                    acc[fm][fn][2] * sc.z + sh.z, acc[fm][fn][3] * sc.w + sh.w};
       const bool full = co + 3 < p.cout;
-      if (res != nullptr) {
+      float v[4] = {acc[fm][fn][0], acc[fm][fn][1], acc[fm][fn][2], acc[fm][fn][3]};
+      if (p.scale != nullptr) {   // else shift and residual are already in the accumulator
+        const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);   // padded to cout_pad
+        const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+        v[0] = v[0] * sc.x + sh.x;
+        v[1] = v[1] * sc.y + sh.y;
+        v[2] = v[2] * sc.z + sh.z;
+        v[3] = v[3] * sc.w + sh.w;
+      }
+      if (p.scale != nullptr && res != nullptr) {
         if (full) {
           const uint2 rv = *reinterpret_cast<const uint2*>(res + static_cast<int64_t>(m) * p.cout + co);
           v[0] += bf16_to_f32(static_cast<uint16_t>(rv.x & 0xffff));
@@ -251,13 +307,10 @@ conv_big_kernel(const drnmi_conv_args p) {
   int px0 = (tile / nco) * kBPX;
   int co0 = (tile % nco) * C::BCO;
   setup(px0, co0);
+  init_tile<C::FM, WCO>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
   for (int t = 0; t < NST - 1 && t < nk; ++t) issue(t, t);
 
   while (true) {
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     for (int t = 0; t < nk; ++t) {
       const int cur = t % NST;
@@ -341,6 +394,7 @@ conv_big_kernel(const drnmi_conv_args p) {
 
     store_tile<C::FM, WCO>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
     if (!more) break;
+    init_tile<C::FM, WCO>(p, acc, px0, co0, wc, wp, fr, fq);
   }
 }
 
@@ -458,10 +512,6 @@ conv_pp_kernel(const drnmi_conv_args p) {
       }
   };
   f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mfma = [&](const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int hh, int g) {
     if constexpr ((DRNMI_ABLATE & 2) != 0) {
 #pragma unroll
@@ -482,6 +532,7 @@ conv_pp_kernel(const drnmi_conv_args p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
+  init_tile<8, 128>(p, acc, px0, co0, wc, wp, fr, fq);
   // prologue: step 0 (both halves) and the first half of step 1
   issue(0, 0, 0);
   issue(0, 0, 1);
@@ -612,6 +663,7 @@ constexpr Variant kVariants[] = {
     {256, 64, "conv_pp_kernel<3>", "conv_pp_kernel<1>"},
 };
 constexpr int kPingPong = 12;
+constexpr int kHalo = 13;   // conv_halo.hip (tile id 17)
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 template <int KS, bool PERSIST>
@@ -641,6 +693,7 @@ bool big_conv_supported(const drnmi_conv_args& p) {
 }
 
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
+  if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_dispatch(p, s);
   if (!big_conv_supported(p)) return DRNMI_ENOTSUP;
   if (variant < 0) variant = auto_variant(p);
   if (variant >= kNumVariants) return DRNMI_ENOTSUP;
@@ -662,6 +715,7 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 }
 
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
+  if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_name(p);
   if (variant < 0) variant = auto_variant(p);
   if (variant >= kNumVariants) return nullptr;
   return p.ks == 3 ? kVariants[variant].name3 : kVariants[variant].name1;

@@ -1,0 +1,279 @@
+// Halo-patch 3x3 convolution for the mid-size stride-1 layers (cin 64/128, cout 64/128):
+// DRN-D layer3/layer4 BasicBlock convs (lmodels/drn.py:27-29, :49-65; the D-38/54 layer3/4
+// Bottleneck 3x3 convs, :86-106, take the same path).
+//
+// conv_big streams the im2col B operand per K step, so every input pixel is fetched 9 times
+// (once per tap) and, at cout <= 128, those DMA pieces outnumber the MFMAs they feed.  Here a
+// workgroup owns a 4 x 64 output block and all cout channels; its input neighbourhood
+// ((4 + 2 dil) x (64 + 2 dil) pixels x cin) is DMA'd into LDS once, and the 9 taps are read
+// from that patch at shifted pixel rows.  Only the weights stream per K step (a small
+// LDS-DMA ring shared by every wave).
+//
+//   * LDS patch rows = pixels (cin * 2 bytes), 16-B chunk c of row r at slot c ^ f(r)
+//     (applied on the DMA source and on the fragment read, as in conv_big);
+//     out-of-image pixels come from a zero page (the conv's zero padding).
+//   * K step = (64-channel block, tap), taps innermost; A = weights [cout][64] per step.
+//   * MFMA v_mfma_f32_16x16x32_bf16, A = weights (rows = channels), B = pixels: wave
+//     (wc, wp) owns channels wc*64..+64 of output row wp (64 pixels), 4 x 4 fragments.
+#include "common.h"
+#include "kernels.h"
+
+namespace drnmi {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void g_void_t;
+
+__device__ uint4 g_halo_zero[64];   // zero-initialised source of padded pixels
+
+constexpr int kTR = 4, kTC = 64;     // output block: rows x columns
+constexpr int kNST = 3;              // weight ring stages
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+template <int ROWB>
+__device__ __forceinline__ int hswz(int row, int chunk) {
+  if constexpr (ROWB == 128) return chunk ^ ((row >> 1) & 7);
+  else return chunk ^ (row & 15);   // 256-B rows span all 64 banks
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// LDS bytes of the patch, rounded up to whole 1-KB DMA pieces
+__host__ __device__ constexpr int patch_bytes(int cin, int dil) {
+  return ((kTR + 2 * dil) * (kTC + 2 * dil) * cin * 2 + 1023) / 1024 * 1024;
+}
+
+template <int CIN, int WC>
+__global__ void __launch_bounds__(256 * WC, 1)
+conv_halo_kernel(const drnmi_conv_args p) {
+  constexpr int NW = 4 * WC;
+  constexpr int ROWB = CIN * 2;          // patch row bytes
+  constexpr int CPR = ROWB / 16;         // chunks per patch row
+  constexpr int RPP = 1024 / ROWB;       // patch rows per DMA piece
+  constexpr int COUT_T = 64 * WC;        // channels per tile
+  constexpr int A_STAGE = COUT_T * 128;  // weights [COUT_T][64] bf16
+  constexpr int A_PIECES = A_STAGE / 1024 / NW;   // per wave per step (2)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* ring = smem;
+  char* patch = smem + kNST * A_STAGE;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wc = wave >> 2;
+  const int wp = wave & 3;
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  const int H = p.h, W = p.w, dil = p.dil;
+  const int PW = kTC + 2 * dil;
+  const int PROWS = (kTR + 2 * dil) * PW;
+  const int tiles_x = (p.wo + kTC - 1) / kTC;
+  const int tiles_y = (p.ho + kTR - 1) / kTR;
+  const int ntiles = p.n * tiles_y * tiles_x;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int n = tile / (tiles_y * tiles_x);
+  const int trem = tile - n * tiles_y * tiles_x;
+  const int oh0 = (trem / tiles_x) * kTR;
+  const int ow0 = (trem - (trem / tiles_x) * tiles_x) * kTC;
+  const uint16_t* __restrict__ x = reinterpret_cast<const uint16_t*>(p.x);
+  const uint16_t* __restrict__ wt = reinterpret_cast<const uint16_t*>(p.wgt);
+  constexpr int NCB = CIN / 64;
+  const int nk = 9 * NCB;
+
+  // --- accumulator start: 0, or shift + residual when the BN scale is folded into the
+  // weights (scale == NULL); those loads go out ahead of the DMA and hide under it
+  const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
+  const int oh = oh0 + wp;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int fm = 0; fm < 4; ++fm) {
+    const int co = wc * 64 + fm * 16 + fq * 4;
+    f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (p.scale == nullptr) {
+      const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+      a0 = f32x4{sh.x, sh.y, sh.z, sh.w};
+    }
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = a0;
+  }
+  if (p.scale == nullptr && res != nullptr && oh < p.ho) {
+    uint2 rv[4][4];
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) {
+      const int ow = ow0 + fn * 16 + fr;
+      const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + (ow < p.wo ? ow : p.wo - 1);
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+        rv[fm][fn] = *reinterpret_cast<const uint2*>(res + m * p.cout + wc * 64 + fm * 16 + fq * 4);
+    }
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        acc[fm][fn][0] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x & 0xffff));
+        acc[fm][fn][1] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x >> 16));
+        acc[fm][fn][2] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y & 0xffff));
+        acc[fm][fn][3] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y >> 16));
+      }
+  }
+
+  // --- patch: DMA once (pieces dealt round-robin over the waves)
+  {
+    const int npieces = (PROWS + RPP - 1) / RPP;
+    const char* zero_src = reinterpret_cast<const char*>(g_halo_zero) + lane * 16;
+    const int lr = lane / CPR, ls = lane % CPR;
+    const int64_t img = static_cast<int64_t>(n) * H;
+    for (int pc = wave; pc < npieces; pc += NW) {
+      const int row = pc * RPP + lr;
+      const int pr = row / PW;
+      const int ih = oh0 - p.pad + pr;
+      const int iw = ow0 - p.pad + (row - pr * PW);
+      const bool ok = row < PROWS && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      const void* src = ok ? static_cast<const void*>(x + ((img + ih) * W + iw) * CIN + hswz<ROWB>(row, ls) * 8)
+                           : static_cast<const void*>(zero_src);
+      glds16(src, patch + pc * 1024);
+    }
+  }
+  // --- weights ring: step kt = (cb, tap) -> packed column tap * CIN + cb * 64
+  const int lrow = lane >> 3, lslot = lane & 7;   // 128-B rows, 8 per piece
+  int a_off[A_PIECES];
+#pragma unroll
+  for (int i = 0; i < A_PIECES; ++i) {
+    const int r = (wave * A_PIECES + i) * 8 + lrow;
+    a_off[i] = r * p.k_pad + (hswz<128>(r, lslot)) * 8;
+  }
+  auto a_col = [&](int kt) {
+    const int cb = kt / 9;
+    return (kt - cb * 9) * CIN + cb * 64;
+  };
+  auto issue_a = [&](int kt, int i) {
+    glds16(wt + a_off[i] + a_col(kt), ring + (kt % kNST) * A_STAGE + (wave * A_PIECES + i) * 1024);
+  };
+  for (int t = 0; t < kNST - 1 && t < nk; ++t)
+#pragma unroll
+    for (int i = 0; i < A_PIECES; ++i) issue_a(t, i);
+
+
+  for (int t = 0; t < nk; ++t) {
+    // retire step t (the patch went out before every weight piece, so it is retired too)
+    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(A_PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const bool nxt = t + kNST - 1 < nk;
+    const char* sa = ring + (t % kNST) * A_STAGE;
+    const int cb = t / 9;
+    const int tap = t - cb * 9;
+    const int dh = (tap / 3) * dil, dw = (tap - (tap / 3) * 3) * dil;
+    const int prow0 = (wp + dh) * PW + dw;            // patch row of this wave's pixel 0
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int r = wc * 64 + f * 16 + fr;
+        af[f] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + hswz<128>(r, sub * 4 + fq) * 16);
+        const int pr = prow0 + f * 16 + fr;
+        bfr[f] = *reinterpret_cast<const bf16x8*>(patch + pr * ROWB + hswz<ROWB>(pr, cb * 8 + sub * 4 + fq) * 16);
+      }
+      if (sub == 0 && nxt) {
+#pragma unroll
+        for (int i = 0; i < A_PIECES; ++i) issue_a(t + kNST - 1, i);
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+    }
+  }
+
+  // --- epilogue: lane owns channels co..co+3 of pixel (oh0 + wp, ow0 + fn*16 + fr)
+  if (oh >= p.ho) return;
+#pragma unroll
+  for (int fn = 0; fn < 4; ++fn) {
+    const int ow = ow0 + fn * 16 + fr;
+    if (ow >= p.wo) continue;
+    const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow;
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) {
+      const int co = wc * 64 + fm * 16 + fq * 4;
+      if (co >= p.cout) continue;
+      float v[4] = {acc[fm][fn][0], acc[fm][fn][1], acc[fm][fn][2], acc[fm][fn][3]};
+      if (p.scale != nullptr) {
+        const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);
+        const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+        v[0] = v[0] * sc.x + sh.x;
+        v[1] = v[1] * sc.y + sh.y;
+        v[2] = v[2] * sc.z + sh.z;
+        v[3] = v[3] * sc.w + sh.w;
+      }
+      if (p.scale != nullptr && res != nullptr) {
+        const uint2 rv = *reinterpret_cast<const uint2*>(res + m * p.cout + co);
+        v[0] += bf16_to_f32(static_cast<uint16_t>(rv.x & 0xffff));
+        v[1] += bf16_to_f32(static_cast<uint16_t>(rv.x >> 16));
+        v[2] += bf16_to_f32(static_cast<uint16_t>(rv.y & 0xffff));
+        v[3] += bf16_to_f32(static_cast<uint16_t>(rv.y >> 16));
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
+      uint2 o;
+      o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+      o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.y) + m * p.cout + co) = o;
+    }
+  }
+}
+
+template <int CIN, int WC>
+hipError_t launch_halo(const drnmi_conv_args& p, hipStream_t s) {
+  const int lds = kNST * 64 * WC * 128 + patch_bytes(CIN, p.dil);
+  static int attr_lds = 0;
+  if (attr_lds < lds) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<CIN, WC>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr_lds = lds;
+  }
+  const int64_t tiles = static_cast<int64_t>(p.n) * ((p.ho + kTR - 1) / kTR) * ((p.wo + kTC - 1) / kTC);
+  hipLaunchKernelGGL((conv_halo_kernel<CIN, WC>), dim3(static_cast<unsigned>(tiles)), dim3(256 * WC), lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool halo_conv_supported(const drnmi_conv_args& p) {
+  if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.ks != 3 || p.stride != 1 || p.pad != p.dil)
+    return false;
+  if ((p.cin != 64 && p.cin != 128) || (p.cout != 64 && p.cout != 128) || p.cout_pad < p.cout)
+    return false;
+  if (p.k != 9 * p.cin || p.k_pad != p.k || p.y_sc != 1 || p.y_sp != p.cout || p.dil < 1 || p.dil > 8)
+    return false;
+  const int wc = p.cout / 64;
+  return kNST * 64 * wc * 128 + patch_bytes(p.cin, p.dil) <= 160 * 1024;
+}
+
+int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
+  if (!halo_conv_supported(p)) return DRNMI_ENOTSUP;
+  hipError_t e;
+  if (p.cin == 64) e = p.cout == 64 ? launch_halo<64, 1>(p, s) : launch_halo<64, 2>(p, s);
+  else e = p.cout == 64 ? launch_halo<128, 1>(p, s) : launch_halo<128, 2>(p, s);
+  return static_cast<int>(e);
+}
+
+const char* halo_conv_name(const drnmi_conv_args& p) {
+  if (p.cin == 64) return p.cout == 64 ? "conv_halo_kernel<64, 1>" : "conv_halo_kernel<64, 2>";
+  return p.cout == 64 ? "conv_halo_kernel<128, 1>" : "conv_halo_kernel<128, 2>";
+}
+
+}  // namespace drnmi

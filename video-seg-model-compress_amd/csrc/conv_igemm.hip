@@ -236,7 +236,7 @@ conv_igemm_kernel(const drnmi_conv_args p) {
       for (int fn = 0; fn < FN; ++fn) {
         const int co = bn0 + wn * WTN + fn * 16 + col_l;
         if (co >= p.cout) continue;
-        float v = acc[fm][fn][j] * p.scale[co] + p.shift[co];
+        float v = acc[fm][fn][j] * (p.scale != nullptr ? p.scale[co] : 1.f) + p.shift[co];
         if (res != nullptr) v += Elem<T>::to_f32(res[static_cast<int64_t>(m) * p.cout + co]);
         if (p.relu) v = fmaxf(v, 0.f);
         store_out(p.y, ybase + static_cast<int64_t>(co) * p.y_sc, v, p.out_dtype);
@@ -261,6 +261,7 @@ constexpr TileDesc kTiles[] = {
     {128, 128, "dma128p"}, {256, 256, "dma256p"}, {64, 64, "dma64k32p"}, {32, 32, "dma32p"},
     {256, 256, "dma256k32p"}, {128, 128, "dma128k32p"},   // p = persistent
     {256, 256, "pp256"},                                   // ping-pong 4-phase schedule
+    {128, 128, "halo"},                                    // conv_halo.hip, 4x64 pixel block
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
@@ -317,7 +318,7 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (a == nullptr) return DRNMI_EINVAL;
   const drnmi_conv_args& p = *a;
   if (p.algo == DRNMI_ALGO_PATCH) {
-    if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.scale == nullptr || p.shift == nullptr ||
+    if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.shift == nullptr ||
         p.n <= 0 || p.h <= 0 || p.w <= 0 || p.cout > p.cout_pad)
       return DRNMI_EINVAL;
     if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
@@ -330,7 +331,7 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (!pow2 || p.n <= 0 || p.h <= 0 || p.w <= 0 || p.ho <= 0 || p.wo <= 0) return DRNMI_EINVAL;
   if (p.cout <= 0 || p.cout > p.cout_pad || p.k != p.ks * p.ks * p.cin) return DRNMI_EINVAL;
   if (p.k_pad < p.k || p.k_pad % kBK != 0 || p.stride <= 0 || p.dil <= 0 || p.pad < 0) return DRNMI_EINVAL;
-  if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.scale == nullptr || p.shift == nullptr)
+  if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.shift == nullptr)
     return DRNMI_EINVAL;
   if ((p.dtype != DRNMI_BF16 && p.dtype != DRNMI_F32) ||
       (p.out_dtype != DRNMI_BF16 && p.out_dtype != DRNMI_F32))
@@ -339,7 +340,7 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
       p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
     return DRNMI_EINVAL;
-  if (p.tile >= 4 || (p.tile < 0 && big_conv_supported(p)))
+  if (p.tile >= 4 || (p.tile < 0 && (big_conv_supported(p) || halo_conv_supported(p))))
     return big_conv_dispatch(p, p.tile < 0 ? -1 : p.tile - 4, reinterpret_cast<hipStream_t>(stream));
   const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;
   if (tile >= 4 || p.cout_pad % kTiles[tile].bn != 0) return DRNMI_EINVAL;
@@ -355,7 +356,8 @@ extern "C" const char* drnmi_conv_kernel_name(const drnmi_conv_args* a) {
   if (a == nullptr) return nullptr;
   const drnmi_conv_args& p = *a;
   if (p.algo == DRNMI_ALGO_PATCH) return patch_conv_name(p);
-  if (p.tile >= 4 || (p.tile < 0 && big_conv_supported(p))) return big_conv_name(p, p.tile < 0 ? -1 : p.tile - 4);
+  if (p.tile >= 4 || (p.tile < 0 && (big_conv_supported(p) || halo_conv_supported(p))))
+    return big_conv_name(p, p.tile < 0 ? -1 : p.tile - 4);
   const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;
   if (tile > 3 || (p.ks != 1 && p.ks != 3 && p.ks != 7)) return nullptr;
   static const char* tn[4] = {"128, 128, 2, 2", "128, 64, 2, 2", "256, 32, 4, 1", "256, 16, 4, 1"};

@@ -166,7 +166,7 @@ patch_conv_kernel(const drnmi_conv_args p) {
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        v[j] = acc[mf][q][j] * p.scale[co + j] + p.shift[co + j];
+        v[j] = acc[mf][q][j] * (p.scale != nullptr ? p.scale[co + j] : 1.f) + p.shift[co + j];
         if (p.relu) v[j] = fmaxf(v[j], 0.f);
       }
       uint2 o;

@@ -67,6 +67,7 @@ class ConvNode:
     k: int = 0
     k_pad: int = 0
     cout_pad: int = 0
+    scale_folded: bool = False   # BN scale multiplied into wpk; launched with scale = NULL
 
 
 @dataclass
@@ -191,6 +192,11 @@ class PackedNet:
                 elif conv.bias is not None:
                     shift[:cout] = conv.bias.detach().to(self.device, torch.float32)
                 nd.scale, nd.shift = scale.contiguous(), shift.contiguous()
+                # bf16 LDS-DMA kernels: fold the BN scale into the weights so the kernel starts its
+                # accumulators from shift + residual (include/drnmi.h: scale may be NULL)
+                nd.scale_folded = self.precision == "bf16" and _fused_init_route(nd, cs)
+                if nd.scale_folded:
+                    nd.wpk = (full * scale[:, None]).to(self.tdtype).contiguous()
             # fused-ingest stem weights (bf16 patch kernel reads uint8 frames directly)
             self.stem_u8_w = None
             stem = self.graph.nodes[0]
@@ -201,6 +207,35 @@ class PackedNet:
                 full = torch.zeros(stem.cout_pad, STEM_U8_K, device=self.device, dtype=torch.float32)
                 full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
                 self.stem_u8_w = full.to(self.tdtype).contiguous()
+
+
+def _uses_patch(nd: ConvNode, cin_stride: int, precision: str) -> bool:
+    c = nd.conv
+    shape = (cin_stride, c.out_channels, c.kernel_size[0], c.stride[0], c.dilation[0])
+    return precision == "bf16" and shape in PATCH_SHAPES and nd.res is None and not nd.out_fp32_nchw
+
+
+def _fused_init_route(nd: ConvNode, cin_stride: int) -> bool:
+    """True when the bf16 launch of `nd` goes to conv_big / conv_pp / conv_halo (the kernels
+    that take scale = NULL and seed the accumulators with shift + residual).  Routing does not
+    depend on the spatial size, so a 16x16 probe decides it."""
+    if _uses_patch(nd, cin_stride, "bf16"):
+        return False
+    c = nd.conv
+    a = _lib.ConvArgs()
+    a.n, a.h, a.w, a.cin = 1, 16, 16, cin_stride
+    a.ks, a.stride, a.pad, a.dil = c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0]
+    a.ho = _conv_out(16, a.ks, a.stride, a.pad, a.dil)
+    a.wo = a.ho
+    a.cout, a.cout_pad, a.k, a.k_pad = c.out_channels, nd.cout_pad, nd.k, nd.k_pad
+    a.dtype = _lib.DRNMI_BF16
+    if nd.out_fp32_nchw:
+        a.out_dtype, a.y_sp, a.y_sc = _lib.DRNMI_F32, 1, a.ho * a.wo
+    else:
+        a.out_dtype, a.y_sp, a.y_sc = _lib.DRNMI_BF16, c.out_channels, 1
+    a.tile, a.algo = -1, _lib.ALGO_IGEMM
+    name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
+    return name is not None and name.decode().startswith(("conv_big", "conv_pp", "conv_halo"))
 
 
 def _conv_out(h, k, s, p, d):
@@ -262,7 +297,7 @@ class Plan:
         a = _lib.ConvArgs()
         a.x = self.bufs[nd.src].data_ptr()
         a.wgt = nd.wpk.data_ptr()
-        a.scale = nd.scale.data_ptr()
+        a.scale = None if nd.scale_folded else nd.scale.data_ptr()
         a.shift = nd.shift.data_ptr()
         a.res = self.bufs[nd.res].data_ptr() if nd.res else None
         a.y = self.bufs[nd.dst].data_ptr()
@@ -285,10 +320,7 @@ class Plan:
         a.relu = 1 if nd.relu else 0
         a.dtype = pk.code
         a.tile = -1
-        shape = (nd.cin_stride, cout, c.kernel_size[0], c.stride[0], c.dilation[0])
-        use_patch = (pk.precision == "bf16" and shape in PATCH_SHAPES and nd.res is None
-                     and not nd.out_fp32_nchw)
-        a.algo = _lib.ALGO_PATCH if use_patch else _lib.ALGO_IGEMM
+        a.algo = _lib.ALGO_PATCH if _uses_patch(nd, nd.cin_stride, pk.precision) else _lib.ALGO_IGEMM
         return a
 
     def _stem_u8_args(self) -> _lib.ConvArgs | None:
@@ -307,7 +339,7 @@ class Plan:
     def refresh_weight_ptrs(self):
         for a, nd in zip(self.args, self.packed.graph.nodes):
             a.wgt = nd.wpk.data_ptr()
-            a.scale = nd.scale.data_ptr()
+            a.scale = None if nd.scale_folded else nd.scale.data_ptr()
             a.shift = nd.shift.data_ptr()
         if self.stem_u8 is not None:
             nd = self.packed.graph.nodes[0]

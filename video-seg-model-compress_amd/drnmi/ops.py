@@ -30,11 +30,17 @@ def pack_conv_weight(weight: torch.Tensor, cin_stride: int, dtype: torch.dtype):
 
 def conv2d_bn_act(x_nhwc: torch.Tensor, weight: torch.Tensor, scale=None, shift=None, residual=None,
                   stride=1, padding=0, dilation=1, relu=False, out_nchw_fp32=False, tile=-1,
-                  packed=None, algo=_lib.ALGO_IGEMM):
-    """y = act(conv(x) * scale + shift [+ residual]) on NHWC x (channel stride = x.shape[3])."""
+                  packed=None, algo=_lib.ALGO_IGEMM, fold_scale=False):
+    """y = act(conv(x) * scale + shift [+ residual]) on NHWC x (channel stride = x.shape[3]).
+    fold_scale: multiply the scale into the packed weights and launch with scale = NULL."""
     n, h, w, cs = x_nhwc.shape
     cout, cin, ks, _ = weight.shape
     dt = x_nhwc.dtype
+    if fold_scale:
+        if packed is not None:
+            raise ValueError("fold_scale packs its own weights")
+        if scale is not None:
+            weight = weight * scale.to(weight.device).float().view(-1, 1, 1, 1)
     if packed is None:
         wpk, k = pack_conv_weight(weight, cs, dt)
     else:
@@ -58,7 +64,8 @@ def conv2d_bn_act(x_nhwc: torch.Tensor, weight: torch.Tensor, scale=None, shift=
         strides = (ho * wo * cout, cout, 1)
         out_code = _CODE[dt]
     a = _lib.ConvArgs()
-    a.x, a.wgt, a.scale, a.shift = x_nhwc.data_ptr(), wpk.data_ptr(), sc.data_ptr(), sh.data_ptr()
+    a.x, a.wgt, a.shift = x_nhwc.data_ptr(), wpk.data_ptr(), sh.data_ptr()
+    a.scale = None if fold_scale else sc.data_ptr()
     a.res = residual.data_ptr() if residual is not None else None
     a.y = y.data_ptr()
     a.y_sn, a.y_sp, a.y_sc = strides
