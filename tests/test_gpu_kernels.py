@@ -207,8 +207,26 @@ def test_patch_conv_bf16(case):
     assert (got - y2.float().permute(0, 3, 1, 2).cpu()).abs().max().item() <= 1e-2 * scale
 
 
-def test_stem_u8_fused_ingest():
-    frames = torch.randint(0, 256, (2, 45, 83, 3), dtype=torch.uint8,
+@pytest.mark.parametrize("hw", [(45, 83), (64, 128), (9, 301), (130, 67)])
+def test_stem_u8_ingest_bit_exact(hw):
+    """Centre-tap identity weights: the stem outputs the normalised frame itself, which must
+    equal the reference ToTensor+Normalize (oracle preprocess_u8) rounded to bf16, bit for bit,
+    including the zero padding at every image edge (frame widths with W*3 % 4 != 0 too)."""
+    h, w = hw
+    frames = torch.randint(0, 256, (3, h, w, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(h * w))
+    wt = torch.zeros(16, 3, 7, 7)
+    for c in range(3):
+        wt[c, c, 3, 3] = 1.0
+    y = ops.stem_u8(frames.to(DEV), wt, torch.ones(16), torch.zeros(16), O.INFO_MEAN, O.INFO_STD, relu=False)
+    ref = O.preprocess_u8(frames.numpy()).bfloat16()            # [N,3,H,W]
+    got = y.cpu()[..., :3].permute(0, 3, 1, 2)
+    assert torch.equal(got, ref)
+    assert torch.count_nonzero(y[..., 3:]).item() == 0
+
+
+@pytest.mark.parametrize("hw", [(45, 83), (33, 130)])
+def test_stem_u8_fused_ingest(hw):
+    frames = torch.randint(0, 256, (2, hw[0], hw[1], 3), dtype=torch.uint8,
                            generator=torch.Generator().manual_seed(3))
     wt = _rand((16, 3, 7, 7), 50, 0.1).bfloat16().float()
     sc = torch.rand(16, generator=torch.Generator().manual_seed(4)) + 0.5

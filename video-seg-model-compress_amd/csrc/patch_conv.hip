@@ -15,6 +15,8 @@
 // :256-281; same fp32 op order), so the frame-ingest pass and its 8-channel
 // intermediate disappear.  Its K is laid out kh*32 + kw*4 + c (kw < 8, c < 4) so a
 // k-step is one kernel row and a fragment is two adjacent pixels x 4 channels.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -44,19 +46,20 @@ __global__ void __launch_bounds__(kThreads)
 patch_conv_kernel(const drnmi_conv_args p) {
   using C = PatchCfg<CIN, COUT, KS, S, TR, TC, SRC_U8>;
   __shared__ __attribute__((aligned(16))) bf16_t patch[C::LDS_ELEMS];
+  // Persistent: each workgroup walks tiles blockIdx.x, +gridDim.x, ...  The next tile's
+  // input is loaded into registers while the current one computes (the 4x64-pixel tiles are
+  // too short-lived to pay a workgroup dispatch each).
+  constexpr int VPP = SRC_U8 ? 1 : CIN / 8;                 // staged units per pixel
+  constexpr int NUNITS = C::PR * C::PC * VPP;
+  constexpr int NPT = (NUNITS + kThreads - 1) / kThreads;    // per thread
+  using Unit = typename std::conditional<SRC_U8, uint32_t, uint4>::type;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int tiles_w = (p.wo + TC - 1) / TC;
   const int tiles_h = (p.ho + TR - 1) / TR;
-  const int b = blockIdx.x;
-  const int n = b / (tiles_w * tiles_h);
-  const int rem = b - n * tiles_w * tiles_h;
-  const int oh0 = (rem / tiles_w) * TR;
-  const int ow0 = (rem % tiles_w) * TC;
-  const int ih0 = oh0 * S - p.pad;
-  const int iw0 = ow0 * S - p.pad;
+  const int ntiles = p.n * tiles_w * tiles_h;
 
   // ---- weights -> registers: A fragment (mf, ks) = W[mf*16 + lane&15][ks*32 + 8*(lane>>4) ..+7]
   const bf16_t* __restrict__ wt = reinterpret_cast<const bf16_t*>(p.wgt);
@@ -68,50 +71,63 @@ patch_conv_kernel(const drnmi_conv_args p) {
       wa[mf][ks] = *reinterpret_cast<const bf16x8*>(
           wt + static_cast<int64_t>(mf * 16 + (lane & 15)) * p.k_pad + ks * 32 + 8 * (lane >> 4));
 
-  // ---- stage the input patch (zero outside the image = the conv's zero padding)
-  if constexpr (SRC_U8) {
-    const uint8_t* __restrict__ fr = reinterpret_cast<const uint8_t*>(p.x) +
-                                     static_cast<int64_t>(n) * p.h * p.w * 3;
-    for (int i = tid; i < C::PR * C::PC; i += kThreads) {
-      const int pr = i / C::PC, pc = i - pr * C::PC;
-      const int ih = ih0 + pr, iw = iw0 + pc;
-      uint2 v = make_uint2(0, 0);
-      if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) &&
-          static_cast<unsigned>(iw) < static_cast<unsigned>(p.w)) {
-        const uint8_t* px = fr + (static_cast<int64_t>(ih) * p.w + iw) * 3;
-        float c0 = static_cast<float>(px[0]), c1 = static_cast<float>(px[1]), c2 = static_cast<float>(px[2]);
-        if (p.bgr) { const float t = c0; c0 = c2; c2 = t; }
-        const float v0 = (c0 / 255.0f - p.mean[0]) / p.std[0];
-        const float v1 = (c1 / 255.0f - p.mean[1]) / p.std[1];
-        const float v2 = (c2 / 255.0f - p.mean[2]) / p.std[2];
-        v.x = static_cast<uint32_t>(f32_to_bf16(v0)) | (static_cast<uint32_t>(f32_to_bf16(v1)) << 16);
-        v.y = static_cast<uint32_t>(f32_to_bf16(v2));
-      }
-      *reinterpret_cast<uint2*>(patch + i * 4) = v;
-    }
-  } else {
-    const bf16_t* __restrict__ x = reinterpret_cast<const bf16_t*>(p.x) +
-                                   static_cast<int64_t>(n) * p.h * p.w * CIN;
-    constexpr int VPP = CIN / 8;  // 16-B vectors per pixel
-    for (int i = tid; i < C::PR * C::PC * VPP; i += kThreads) {
+  // ---- input patch of a tile -> registers (zero outside the image = the conv's padding)
+  Unit stage[NPT];
+  auto load_tile = [&](int b) {
+    const int n = b / (tiles_w * tiles_h);
+    const int rem = b - n * tiles_w * tiles_h;
+    const int ih0 = (rem / tiles_w) * TR * S - p.pad;
+    const int iw0 = (rem % tiles_w) * TC * S - p.pad;
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+      const int i = tid + u * kThreads;
       const int pix = i / VPP, v8 = i - pix * VPP;
       const int pr = pix / C::PC, pc = pix - pr * C::PC;
       const int ih = ih0 + pr, iw = iw0 + pc;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) &&
-          static_cast<unsigned>(iw) < static_cast<unsigned>(p.w))
-        v = *reinterpret_cast<const uint4*>(x + (static_cast<int64_t>(ih) * p.w + iw) * CIN + v8 * 8);
-      *reinterpret_cast<uint4*>(patch + pix * CIN + v8 * 8) = v;
+      const bool ok = i < NUNITS && static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) &&
+                      static_cast<unsigned>(iw) < static_cast<unsigned>(p.w);
+      if constexpr (SRC_U8) {
+        uint32_t v = 0xffffffffu;                      // marks a padded pixel
+        if (ok) {
+          const uint8_t* px = reinterpret_cast<const uint8_t*>(p.x) +
+                              ((static_cast<int64_t>(n) * p.h + ih) * p.w + iw) * 3;
+          v = static_cast<uint32_t>(px[0]) | (static_cast<uint32_t>(px[1]) << 8) |
+              (static_cast<uint32_t>(px[2]) << 16);
+        }
+        stage[u] = v;
+      } else {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (ok)
+          v = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.x) +
+                                              ((static_cast<int64_t>(n) * p.h + ih) * p.w + iw) * CIN + v8 * 8);
+        stage[u] = v;
+      }
     }
-  }
-  __syncthreads();
-
-  // ---- MFMA: this wave's pixel fragments pf = wave + 4*q
-  f32x4 acc[C::MF][C::PFW];
+  };
+  auto store_patch = [&]() {
 #pragma unroll
-  for (int mf = 0; mf < C::MF; ++mf)
-#pragma unroll
-    for (int q = 0; q < C::PFW; ++q) acc[mf][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < NPT; ++u) {
+      const int i = tid + u * kThreads;
+      if (i >= NUNITS) break;
+      if constexpr (SRC_U8) {
+        // reference normalisation, same fp32 op order (data_transforms.py:109-125, :256-281)
+        uint2 v = make_uint2(0, 0);
+        if (stage[u] != 0xffffffffu) {
+          float c0 = static_cast<float>(stage[u] & 0xff), c1 = static_cast<float>((stage[u] >> 8) & 0xff),
+                c2 = static_cast<float>((stage[u] >> 16) & 0xff);
+          if (p.bgr) { const float t = c0; c0 = c2; c2 = t; }
+          const float v0 = (c0 / 255.0f - p.mean[0]) / p.std[0];
+          const float v1 = (c1 / 255.0f - p.mean[1]) / p.std[1];
+          const float v2 = (c2 / 255.0f - p.mean[2]) / p.std[2];
+          v.x = static_cast<uint32_t>(f32_to_bf16(v0)) | (static_cast<uint32_t>(f32_to_bf16(v1)) << 16);
+          v.y = static_cast<uint32_t>(f32_to_bf16(v2));
+        }
+        *reinterpret_cast<uint2*>(patch + i * 4) = v;
+      } else {
+        *reinterpret_cast<uint4*>(patch + i * 8) = stage[u];
+      }
+    }
+  };
 
   int prow[C::PFW], pcol[C::PFW];
 #pragma unroll
@@ -121,71 +137,500 @@ patch_conv_kernel(const drnmi_conv_args p) {
     pcol[q] = (idx % TC) * S;
   }
   const int kq = lane >> 4;
+  bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(p.y);
+
+  int b = blockIdx.x;
+  if (b < ntiles) load_tile(b);
+  for (; b < ntiles; b += gridDim.x) {
+    __syncthreads();               // every wave done reading the previous patch
+    store_patch();
+    __syncthreads();
+    if (b + static_cast<int>(gridDim.x) < ntiles) load_tile(b + gridDim.x);   // in flight during the MFMAs
+
+    // ---- MFMA: this wave's pixel fragments pf = wave + 4*q
+    f32x4 acc[C::MF][C::PFW];
 #pragma unroll
-  for (int ks = 0; ks < C::NK; ++ks) {
+    for (int mf = 0; mf < C::MF; ++mf)
 #pragma unroll
-    for (int q = 0; q < C::PFW; ++q) {
-      bf16x8 bv;
-      if constexpr (SRC_U8) {
-        // k = kh*32 + kw*4 + c: step ks = kernel row kh, fragment = taps kw = 2kq, 2kq+1
-        const bf16_t* src = patch + ((prow[q] + ks) * C::PC + pcol[q] + 2 * kq) * 4;
-        const uint2 lo = *reinterpret_cast<const uint2*>(src);
-        const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
-        const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        bv = __builtin_bit_cast(bf16x8, u);
-      } else {
-        const int k0 = ks * 32 + 8 * kq;
-        const int tap = k0 / CIN;
-        const int ci = k0 % CIN;
-        if (tap < KS * KS) {
-          const int kh = tap / KS, kw = tap % KS;
-          const uint4 u = *reinterpret_cast<const uint4*>(
-              patch + ((prow[q] + kh) * C::PC + pcol[q] + kw) * CIN + ci);
+      for (int q = 0; q < C::PFW; ++q) acc[mf][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < C::NK; ++ks) {
+#pragma unroll
+      for (int q = 0; q < C::PFW; ++q) {
+        bf16x8 bv;
+        if constexpr (SRC_U8) {
+          // k = kh*32 + kw*4 + c: step ks = kernel row kh, fragment = taps kw = 2kq, 2kq+1
+          const bf16_t* src = patch + ((prow[q] + ks) * C::PC + pcol[q] + 2 * kq) * 4;
+          const uint2 lo = *reinterpret_cast<const uint2*>(src);
+          const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
+          const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
           bv = __builtin_bit_cast(bf16x8, u);
         } else {
-          bv = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+          const int k0 = ks * 32 + 8 * kq;
+          const int tap = k0 / CIN;
+          const int ci = k0 % CIN;
+          if (tap < KS * KS) {
+            const int kh = tap / KS, kw = tap % KS;
+            const uint4 u = *reinterpret_cast<const uint4*>(
+                patch + ((prow[q] + kh) * C::PC + pcol[q] + kw) * CIN + ci);
+            bv = __builtin_bit_cast(bf16x8, u);
+          } else {
+            bv = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+          }
         }
-      }
 #pragma unroll
-      for (int mf = 0; mf < C::MF; ++mf)
-        acc[mf][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[mf][ks], bv, acc[mf][q], 0, 0, 0);
+        for (int mf = 0; mf < C::MF; ++mf)
+          acc[mf][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[mf][ks], bv, acc[mf][q], 0, 0, 0);
+      }
     }
-  }
 
-  // ---- epilogue: lane owns channels co..co+3 of one pixel
-  bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(p.y);
+    // ---- epilogue: lane owns channels co..co+3 of one pixel
+    const int n = b / (tiles_w * tiles_h);
+    const int rem = b - n * tiles_w * tiles_h;
+    const int oh0 = (rem / tiles_w) * TR;
+    const int ow0 = (rem % tiles_w) * TC;
 #pragma unroll
-  for (int q = 0; q < C::PFW; ++q) {
-    const int idx = (wave + 4 * q) * 16 + (lane & 15);
-    const int oh = oh0 + idx / TC, ow = ow0 + idx % TC;
-    if (oh >= p.ho || ow >= p.wo) continue;
-    const int64_t base = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(oh * p.wo + ow) * p.y_sp;
+    for (int q = 0; q < C::PFW; ++q) {
+      const int idx = (wave + 4 * q) * 16 + (lane & 15);
+      const int oh = oh0 + idx / TC, ow = ow0 + idx % TC;
+      if (oh >= p.ho || ow >= p.wo) continue;
+      const int64_t base = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(oh * p.wo + ow) * p.y_sp;
 #pragma unroll
-    for (int mf = 0; mf < C::MF; ++mf) {
-      const int co = mf * 16 + kq * 4;
-      float v[4];
+      for (int mf = 0; mf < C::MF; ++mf) {
+        const int co = mf * 16 + kq * 4;
+        float v[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = acc[mf][q][j] * (p.scale != nullptr ? p.scale[co + j] : 1.f) + p.shift[co + j];
-        if (p.relu) v[j] = fmaxf(v[j], 0.f);
+        for (int j = 0; j < 4; ++j) {
+          v[j] = acc[mf][q][j] * (p.scale != nullptr ? p.scale[co + j] : 1.f) + p.shift[co + j];
+          if (p.relu) v[j] = fmaxf(v[j], 0.f);
+        }
+        uint2 o;
+        o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+        o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+        *reinterpret_cast<uint2*>(y + base + co) = o;
       }
-      uint2 o;
-      o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
-      o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
-      *reinterpret_cast<uint2*>(y + base + co) = o;
     }
   }
 }
 
+// ---- LDS-DMA multi-buffered variant for bf16 inputs (layer1 16->16, layer2 16->32 s2).
+//
+// Persistent workgroups walk their tiles with NB patch buffers in LDS: the patch of tile
+// t+NB-1 is DMA'd (buffer_load ... lds, no VGPR round trip, out-of-image pixels = an
+// out-of-range buffer offset, which the hardware returns as zeros) while tile t computes.
+// A patch is PR rows of PC*CIN*2 contiguous bytes in both global memory and LDS, so a 1-KB
+// DMA piece is 64 x 16 B of consecutive patch bytes; each wave issues the same number of
+// pieces and of (buffer, out-of-range-dropping) stores per tile, so one counted vmcnt per
+// tile retires exactly the patch about to be read.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+template <int CIN, int COUT, int S, int TR, int TC>
+struct DmaCfg {
+  static constexpr int PR = (TR - 1) * S + 3;
+  static constexpr int PC = (TC - 1) * S + 3;
+  static constexpr int ROWB = PC * CIN * 2;                   // bytes per patch row
+  static constexpr int PB = (PR * ROWB + 4095) / 4096 * 4096;  // buffer bytes (whole 4-KB rounds)
+  static constexpr int P = PB / 4096;                          // DMA pieces per wave per tile
+  static constexpr int NB = 3;                                 // patch buffers
+  static constexpr int K = 9 * CIN;
+  static constexpr int NK = (K + 31) / 32;
+  static constexpr int MF = COUT / 16;
+  static constexpr int PFW = TR * TC / 16 / 4;                 // pixel fragments per wave
+  static constexpr int ST = PFW * MF;                          // stores per lane per tile
+  static constexpr int LDS = NB * PB;
+  static_assert(TR * TC % 64 == 0, "tile must split over 4 waves");
+};
+
+template <int CIN, int COUT, int S, int TR, int TC>
+__global__ void __launch_bounds__(kThreads)
+patch_dma_kernel(const drnmi_conv_args p) {
+  using C = DmaCfg<CIN, COUT, S, TR, TC>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int kq = lane >> 4;
+  const int tiles_w = (p.wo + TC - 1) / TC;
+  const int tiles_h = (p.ho + TR - 1) / TR;
+  const int ntiles = p.n * tiles_w * tiles_h;
+  const int H = p.h, W = p.w;
+
+  const bf16_t* __restrict__ wt = reinterpret_cast<const bf16_t*>(p.wgt);
+  bf16x8 wa[C::MF][C::NK];
+#pragma unroll
+  for (int mf = 0; mf < C::MF; ++mf)
+#pragma unroll
+    for (int ks = 0; ks < C::NK; ++ks)
+      wa[mf][ks] = *reinterpret_cast<const bf16x8*>(
+          wt + static_cast<int64_t>(mf * 16 + (lane & 15)) * p.k_pad + ks * 32 + 8 * (lane >> 4));
+  float sc[C::MF][4], sh[C::MF][4];
+#pragma unroll
+  for (int mf = 0; mf < C::MF; ++mf)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = mf * 16 + kq * 4 + j;
+      sc[mf][j] = p.scale != nullptr ? p.scale[co] : 1.f;
+      sh[mf][j] = p.shift[co];
+    }
+
+  // DMA pieces: tile-independent (row, column, byte) of this lane's 16 bytes in each piece
+  int pc_r[C::P], pc_c[C::P], pc_off[C::P];
+#pragma unroll
+  for (int j = 0; j < C::P; ++j) {
+    const int off = (j * 4 + wave) * 1024 + lane * 16;
+    const int r = off / C::ROWB;
+    const int rb = off - r * C::ROWB;
+    const int c = rb / (CIN * 2);
+    pc_r[j] = r < C::PR ? r : (1 << 20);                     // slack bytes: out of range
+    pc_c[j] = c;
+    pc_off[j] = (r * W + c) * CIN * 2 + (rb - c * CIN * 2);
+  }
+  const int64_t frame_bytes = static_cast<int64_t>(H) * W * CIN * 2;
+  auto issue = [&](int b, int buf) {
+    const int n = b / (tiles_w * tiles_h);
+    const int rem = b - n * tiles_w * tiles_h;
+    const int ih0 = (rem / tiles_w) * TR * S - p.pad;
+    const int iw0 = (rem % tiles_w) * TC * S - p.pad;
+    const char* fb = reinterpret_cast<const char*>(p.x) + static_cast<int64_t>(n) * frame_bytes;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(fb), 0, static_cast<int>(frame_bytes), 0x00020000);
+    const int base = (ih0 * W + iw0) * CIN * 2;
+#pragma unroll
+    for (int j = 0; j < C::P; ++j) {
+      const bool ok = static_cast<unsigned>(ih0 + pc_r[j]) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(iw0 + pc_c[j]) < static_cast<unsigned>(W);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(smem + buf * C::PB + (j * 4 + wave) * 1024), 16,
+          ok ? static_cast<unsigned>(base + pc_off[j]) : 0xffffffffu, 0, 0, 0);
+    }
+  };
+
+  int prow[C::PFW], pcol[C::PFW];
+#pragma unroll
+  for (int q = 0; q < C::PFW; ++q) {
+    const int idx = (wave + 4 * q) * 16 + (lane & 15);
+    prow[q] = (idx / TC) * S;
+    pcol[q] = (idx % TC) * S;
+  }
+  int boff[C::NK];                                  // B fragment byte offset of (ks, this lane)
+#pragma unroll
+  for (int ks = 0; ks < C::NK; ++ks) {
+    const int k0 = ks * 32 + 8 * kq;
+    const int tap = k0 / CIN, ci = k0 % CIN;
+    boff[ks] = tap < 9 ? (((tap / 3) * C::PC + tap % 3) * CIN + ci) * 2 : -1;
+  }
+  const int64_t ybytes = static_cast<int64_t>(p.n) * p.ho * p.wo * COUT * 2;
+  const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
+      p.y, 0, static_cast<int>(ybytes < 0x7fffffff ? ybytes : 0x7fffffff), 0x00020000);
+
+  const int b0 = blockIdx.x;
+  const int G = gridDim.x;
+  if (b0 < ntiles) issue(b0, 0);
+  if (b0 + G < ntiles) issue(b0 + G, 1);
+  int t = 0;
+  for (int b = b0; b < ntiles; b += G, ++t) {
+    // retire tile t's patch: younger ops are stores(t-2), DMA(t+1), stores(t-1)
+    if (t >= 2 && b + G < ntiles) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::P + 2 * C::ST) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (b + 2 * G < ntiles) issue(b + 2 * G, (t + 2) % C::NB);
+    const char* pt = smem + (t % C::NB) * C::PB;
+
+    f32x4 acc[C::MF][C::PFW];
+#pragma unroll
+    for (int mf = 0; mf < C::MF; ++mf)
+#pragma unroll
+      for (int q = 0; q < C::PFW; ++q) acc[mf][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < C::NK; ++ks) {
+#pragma unroll
+      for (int q = 0; q < C::PFW; ++q) {
+        bf16x8 bv = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+        if (boff[ks] >= 0)
+          bv = *reinterpret_cast<const bf16x8*>(pt + boff[ks] + (prow[q] * C::PC + pcol[q]) * CIN * 2);
+#pragma unroll
+        for (int mf = 0; mf < C::MF; ++mf)
+          acc[mf][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[mf][ks], bv, acc[mf][q], 0, 0, 0);
+      }
+    }
+
+    const int n = b / (tiles_w * tiles_h);
+    const int rem = b - n * tiles_w * tiles_h;
+    const int oh0 = (rem / tiles_w) * TR;
+    const int ow0 = (rem % tiles_w) * TC;
+#pragma unroll
+    for (int q = 0; q < C::PFW; ++q) {
+      const int idx = (wave + 4 * q) * 16 + (lane & 15);
+      const int oh = oh0 + idx / TC, ow = ow0 + idx % TC;
+      const bool ok = oh < p.ho && ow < p.wo;
+      const int64_t pix = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow;
+#pragma unroll
+      for (int mf = 0; mf < C::MF; ++mf) {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = acc[mf][q][j] * sc[mf][j] + sh[mf][j];
+          if (p.relu) v[j] = fmaxf(v[j], 0.f);
+        }
+        u32x2_t o;
+        o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+        o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+        // every lane issues the store (out-of-range offset = dropped): constant vmcnt per tile
+        const unsigned yoff = ok ? static_cast<unsigned>((pix * COUT + mf * 16 + kq * 4) * 2) : 0xffffffffu;
+        __builtin_amdgcn_raw_buffer_store_b64(o, ys, yoff, 0, 0);
+      }
+    }
+  }
+}
+
+// ---- Fused-ingest stem, LDS-DMA pipelined (uint8 HWC3 frames -> 7x7 conv 3->16).
+//
+// Raw frame bytes are DMA'd (buffer_load_dword ... lds, 4 bytes per lane, one patch row per
+// wave instruction, dword-aligned below the row start) two tiles ahead into a 3-slot ring;
+// each tile then converts its raw rows into the normalised bf16 patch through a per-channel
+// 256-entry table that the workgroup builds once with the reference op order
+// ((c / 255 - mean) / std, data_transforms.py:109-125, :256-281), so the conversion is
+// bit-identical to the per-pixel division and costs three LDS lookups per pixel.
+constexpr int kStemTR = 4, kStemTC = 64;
+constexpr int kStemPR = kStemTR + 6, kStemPC = kStemTC + 7;     // +1: the zero kw=7 tap
+constexpr int kStemRows = 12;                                    // 3 row loads per wave
+constexpr int kStemRawB = kStemRows * 256;                       // one ring slot
+constexpr int kStemPatchB = kStemPR * kStemPC * 8;
+constexpr int kStemLDS = 3 * kStemRawB + kStemPatchB + 3 * 256 * 2;
+
+__global__ void __launch_bounds__(kThreads)
+stem_dma_kernel(const drnmi_conv_args p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* raw = smem;
+  bf16_t* patch = reinterpret_cast<bf16_t*>(smem + 3 * kStemRawB);
+  bf16_t* lut = reinterpret_cast<bf16_t*>(smem + 3 * kStemRawB + kStemPatchB);
+  constexpr int NK = 7, PFW = 4, ST = PFW;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int kq = lane >> 4;
+  const int H = p.h, W = p.w;
+  const int tiles_w = (p.wo + kStemTC - 1) / kStemTC;
+  const int tiles_h = (p.ho + kStemTR - 1) / kStemTR;
+  const int ntiles = p.n * tiles_w * tiles_h;
+
+  // table: lut[c][v] = bf16((v / 255 - mean[c]) / std[c]) for output channel c
+  for (int i = tid; i < 3 * 256; i += kThreads) {
+    const int c = i >> 8;
+    const float v = static_cast<float>(i & 255);
+    lut[i] = f32_to_bf16((v / 255.0f - p.mean[c]) / p.std[c]);
+  }
+  const bf16_t* __restrict__ wt = reinterpret_cast<const bf16_t*>(p.wgt);
+  bf16x8 wa[NK];
+#pragma unroll
+  for (int ks = 0; ks < NK; ++ks)
+    wa[ks] = *reinterpret_cast<const bf16x8*>(wt + static_cast<int64_t>(lane & 15) * p.k_pad + ks * 32 + 8 * kq);
+  float sc[4], sh[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sc[j] = p.scale != nullptr ? p.scale[kq * 4 + j] : 1.f;
+    sh[j] = p.shift[kq * 4 + j];
+  }
+  const int frame_bytes = H * W * 3;
+  const int total = p.n * frame_bytes;          // < 2^31 (stem_dma_ok)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.x), 0, total, 0x00020000);
+  auto tile_org = [&](int b, int& n, int& ih0, int& iw0) {
+    n = b / (tiles_w * tiles_h);
+    const int rem = b - n * tiles_w * tiles_h;
+    ih0 = (rem / tiles_w) * kStemTR - p.pad;
+    iw0 = (rem % tiles_w) * kStemTC - p.pad;
+  };
+  auto issue = [&](int b, int slot) {
+    int n, ih0, iw0;
+    tile_org(b, n, ih0, iw0);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int r = wave + 4 * j;                       // patch row (10, 11: slack)
+      const int ih = ih0 + r;
+      const int start = n * frame_bytes + (ih * W + iw0) * 3;   // byte of the row's first patch pixel
+      const int a0 = start >= 0 ? (start & ~3) : -((-start + 3) & ~3);
+      const int o = a0 + lane * 4;
+      // a dword straddling the end of the batch would read as zero (out of range): convert()
+      // takes those last pixels from global memory directly
+      const bool ok = r < kStemPR && static_cast<unsigned>(ih) < static_cast<unsigned>(H) && o >= 0;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(raw + slot * kStemRawB + r * 256), 4,
+          ok ? static_cast<unsigned>(o) : 0xffffffffu, 0, 0, 0);
+    }
+  };
+  auto convert = [&](int b, int slot) {
+    int n, ih0, iw0;
+    tile_org(b, n, ih0, iw0);
+    const unsigned char* rb = reinterpret_cast<const unsigned char*>(raw + slot * kStemRawB);
+    for (int i = tid; i < kStemPR * kStemPC; i += kThreads) {
+      const int pr = i / kStemPC, pc = i - pr * kStemPC;
+      const int ih = ih0 + pr, iw = iw0 + pc;
+      uint2 v = make_uint2(0, 0);
+      if (static_cast<unsigned>(ih) < static_cast<unsigned>(H) && static_cast<unsigned>(iw) < static_cast<unsigned>(W)) {
+        const int start = n * frame_bytes + (ih * W + iw0) * 3;
+        const int a0 = start >= 0 ? (start & ~3) : -((-start + 3) & ~3);
+        const unsigned char* px = rb + pr * 256 + (start - a0) + pc * 3;
+        const int pb = start + pc * 3;
+        if (pb + 3 > (total & ~3)) px = reinterpret_cast<const unsigned char*>(p.x) + pb;   // batch tail
+        int c0 = px[0], c1 = px[1], c2 = px[2];
+        if (p.bgr) { const int t = c0; c0 = c2; c2 = t; }
+        v.x = static_cast<uint32_t>(lut[c0]) | (static_cast<uint32_t>(lut[256 + c1]) << 16);
+        v.y = static_cast<uint32_t>(lut[512 + c2]);
+      }
+      *reinterpret_cast<uint2*>(patch + i * 4) = v;
+    }
+  };
+
+  int prow[PFW], pcol[PFW];
+#pragma unroll
+  for (int q = 0; q < PFW; ++q) {
+    const int idx = (wave + 4 * q) * 16 + (lane & 15);
+    prow[q] = idx / kStemTC;
+    pcol[q] = idx % kStemTC;
+  }
+  const int64_t ybytes = static_cast<int64_t>(p.n) * p.ho * p.wo * 16 * 2;
+  const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
+      p.y, 0, static_cast<int>(ybytes < 0x7fffffff ? ybytes : 0x7fffffff), 0x00020000);
+
+  const int b0 = blockIdx.x;
+  const int G = gridDim.x;
+  if (b0 < ntiles) issue(b0, 0);
+  if (b0 + G < ntiles) issue(b0 + G, 1);
+  int t = 0;
+  for (int b = b0; b < ntiles; b += G, ++t) {
+    // retire tile t's raw rows: younger ops are stores(t-2), rows(t+1), stores(t-1)
+    if (t >= 2 && b + G < ntiles) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 + 2 * ST) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (b + 2 * G < ntiles) issue(b + 2 * G, (t + 2) % 3);
+    convert(b, t % 3);
+    __syncthreads();
+
+    f32x4 acc[PFW];
+#pragma unroll
+    for (int q = 0; q < PFW; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NK; ++ks) {
+#pragma unroll
+      for (int q = 0; q < PFW; ++q) {
+        // k = kh*32 + kw*4 + c: step ks = kernel row kh, fragment = taps kw = 2kq, 2kq+1
+        const bf16_t* src = patch + ((prow[q] + ks) * kStemPC + pcol[q] + 2 * kq) * 4;
+        const uint2 lo = *reinterpret_cast<const uint2*>(src);
+        const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks], __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y)),
+                                                         acc[q], 0, 0, 0);
+      }
+    }
+    int n, oh0, ow0;
+    tile_org(b, n, oh0, ow0);
+    oh0 += p.pad;
+    ow0 += p.pad;
+#pragma unroll
+    for (int q = 0; q < PFW; ++q) {
+      const int idx = (wave + 4 * q) * 16 + (lane & 15);
+      const int oh = oh0 + idx / kStemTC, ow = ow0 + idx % kStemTC;
+      const bool ok = oh < p.ho && ow < p.wo;
+      const int64_t pix = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = acc[q][j] * sc[j] + sh[j];
+        if (p.relu) v[j] = fmaxf(v[j], 0.f);
+      }
+      u32x2_t o;
+      o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+      o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+      __builtin_amdgcn_raw_buffer_store_b64(o, ys, ok ? static_cast<unsigned>((pix * 16 + kq * 4) * 2) : 0xffffffffu,
+                                            0, 0);
+    }
+  }
+}
+
+int g_num_cus = 0;
+
 template <int CIN, int COUT, int KS, int S, int TR, int TC, bool SRC_U8>
 hipError_t launch_patch(const drnmi_conv_args& p, hipStream_t s) {
+  static int per_cu = 0;
+  auto kern = patch_conv_kernel<CIN, COUT, KS, S, TR, TC, SRC_U8>;
+  if (per_cu == 0) {
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(kern), kThreads, 0) !=
+            hipSuccess || blocks <= 0)
+      blocks = 2;
+    g_num_cus = cus;
+    per_cu = blocks;
+  }
   const int64_t tiles = static_cast<int64_t>(p.n) * ((p.ho + TR - 1) / TR) * ((p.wo + TC - 1) / TC);
-  hipLaunchKernelGGL((patch_conv_kernel<CIN, COUT, KS, S, TR, TC, SRC_U8>), dim3(static_cast<unsigned>(tiles)),
-                     dim3(kThreads), 0, s, p);
+  const int64_t cap = static_cast<int64_t>(g_num_cus) * per_cu;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(tiles < cap ? tiles : cap)), dim3(kThreads), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_stem_dma(const drnmi_conv_args& p, hipStream_t s) {
+  static int per_cu = 0;
+  if (per_cu == 0) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(stem_dma_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kStemLDS);
+    if (e != hipSuccess) return e;
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(stem_dma_kernel),
+                                                     kThreads, kStemLDS) != hipSuccess || blocks <= 0)
+      blocks = 1;
+    g_num_cus = cus;
+    per_cu = blocks;
+  }
+  const int64_t tiles = static_cast<int64_t>(p.n) * ((p.ho + kStemTR - 1) / kStemTR) * ((p.wo + kStemTC - 1) / kStemTC);
+  const int64_t cap = static_cast<int64_t>(g_num_cus) * per_cu;
+  hipLaunchKernelGGL(stem_dma_kernel, dim3(static_cast<unsigned>(tiles < cap ? tiles : cap)), dim3(kThreads),
+                     kStemLDS, s, p);
+  return hipGetLastError();
+}
+
+template <int CIN, int COUT, int S, int TR, int TC>
+hipError_t launch_patch_dma(const drnmi_conv_args& p, hipStream_t s) {
+  using C = DmaCfg<CIN, COUT, S, TR, TC>;
+  static int per_cu = 0;
+  auto kern = patch_dma_kernel<CIN, COUT, S, TR, TC>;
+  if (per_cu == 0) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    if (e != hipSuccess) return e;
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(kern), kThreads,
+                                                     C::LDS) != hipSuccess || blocks <= 0)
+      blocks = 1;
+    g_num_cus = cus;
+    per_cu = blocks;
+  }
+  const int64_t tiles = static_cast<int64_t>(p.n) * ((p.ho + TR - 1) / TR) * ((p.wo + TC - 1) / TC);
+  const int64_t cap = static_cast<int64_t>(g_num_cus) * per_cu;
+  hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(tiles < cap ? tiles : cap)), dim3(kThreads), C::LDS, s, p);
   return hipGetLastError();
 }
 
 }  // namespace
+
+// buffer offsets are 32-bit: one frame of input and the whole output must stay below 2 GB
+static bool dma_ok(const drnmi_conv_args& p) {
+  return static_cast<int64_t>(p.h) * p.w * p.cin * 2 < (int64_t(1) << 31) &&
+         static_cast<int64_t>(p.n) * p.ho * p.wo * p.cout * 2 < (int64_t(1) << 31) && p.pad == 1;
+}
+
+static bool stem_dma_ok(const drnmi_conv_args& p) {
+  return static_cast<int64_t>(p.n) * p.h * p.w * 3 < (int64_t(1) << 31) &&
+         static_cast<int64_t>(p.n) * p.ho * p.wo * 16 * 2 < (int64_t(1) << 31) && p.pad == 3 && p.w >= 8;
+}
 
 int patch_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.dil != 1 || p.res != nullptr) return DRNMI_ENOTSUP;
@@ -194,9 +639,13 @@ int patch_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (p.src_u8) {
     if (p.cin != 4 || p.cout != 16 || p.ks != 7 || p.stride != 1 || p.k != 224 || p.k_pad != 224)
       return DRNMI_ENOTSUP;
-    e = launch_patch<4, 16, 7, 1, 4, 64, true>(p, s);
+    e = stem_dma_ok(p) ? launch_stem_dma(p, s) : launch_patch<4, 16, 7, 1, 4, 64, true>(p, s);
   } else if (p.cin == 8 && p.cout == 16 && p.ks == 7 && p.stride == 1) {
     e = launch_patch<8, 16, 7, 1, 4, 64, false>(p, s);
+  } else if (p.cin == 16 && p.cout == 16 && p.ks == 3 && p.stride == 1 && dma_ok(p)) {
+    e = launch_patch_dma<16, 16, 1, 4, 64>(p, s);
+  } else if (p.cin == 16 && p.cout == 32 && p.ks == 3 && p.stride == 2 && dma_ok(p)) {
+    e = launch_patch_dma<16, 32, 2, 4, 32>(p, s);
   } else if (p.cin == 16 && p.cout == 16 && p.ks == 3 && p.stride == 1) {
     e = launch_patch<16, 16, 3, 1, 4, 64, false>(p, s);
   } else if (p.cin == 16 && p.cout == 32 && p.ks == 3 && p.stride == 2) {
@@ -210,10 +659,12 @@ int patch_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
 }
 
 const char* patch_conv_name(const drnmi_conv_args& p) {
-  if (p.src_u8) return "patch_conv_kernel<4, 16, 7, 1, 4, 64, true>";
+  if (p.src_u8) return stem_dma_ok(p) ? "stem_dma_kernel" : "patch_conv_kernel<4, 16, 7, 1, 4, 64, true>";
   if (p.cin == 8 && p.cout == 16 && p.ks == 7) return "patch_conv_kernel<8, 16, 7, 1, 4, 64, false>";
-  if (p.cin == 16 && p.cout == 16 && p.ks == 3 && p.stride == 1) return "patch_conv_kernel<16, 16, 3, 1, 4, 64, false>";
-  if (p.cin == 16 && p.cout == 32 && p.ks == 3 && p.stride == 2) return "patch_conv_kernel<16, 32, 3, 2, 4, 64, false>";
+  if (p.cin == 16 && p.cout == 16 && p.ks == 3 && p.stride == 1)
+    return dma_ok(p) ? "patch_dma_kernel<16, 16, 1, 4, 64>" : "patch_conv_kernel<16, 16, 3, 1, 4, 64, false>";
+  if (p.cin == 16 && p.cout == 32 && p.ks == 3 && p.stride == 2)
+    return dma_ok(p) ? "patch_dma_kernel<16, 32, 2, 4, 32>" : "patch_conv_kernel<16, 32, 3, 2, 4, 64, false>";
   if (p.cin == 32 && p.cout == 64 && p.ks == 3 && p.stride == 2) return "patch_conv_kernel<32, 64, 3, 2, 2, 64, false>";
   return nullptr;
 }
