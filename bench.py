@@ -184,13 +184,15 @@ def main():
                    "arch": args.arch, "height": H, "width": W, "frames_per_gpu_step": B,
                    "global_batch": B * world, "parallelism": f"dp{world} (frames sharded, no data-path collective)"},
     }
+    traffic, traffic_src = pmc_traffic(args, dominant) if durs else (None, None)
     if durs:
         avg_d = sum(durs) / len(durs)
         avg_f = sum(flops) / len(flops)
         ach = avg_f / avg_d / 1e12
         peak = MFMA_PEAK[args.precision] / 1e12
         out["roofline"] = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 2), "peak": peak,
-                           "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+                           "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
+                           "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                            "launches": len(durs), "avg_launch_us": round(avg_d * 1e6, 2),
                            "avg_launch_gflop": round(avg_f / 1e9, 3),
                            "share_of_step": round(sum(durs) / el, 3)}
@@ -209,6 +211,24 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(args, kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC capture of this exact
+    workload (profiles/*_pmc_traffic.json, made by scripts/pmc_traffic.sh: FETCH_SIZE x 2 +
+    WRITE_SIZE, MI355X_MICROARCH.md §HBM); PMC counters cannot be read inside the timed run."""
+    import glob
+    want = {"arch": args.arch, "height": args.height, "width": args.width, "frames_per_gpu_step": args.batch,
+            "precision": args.precision}
+    here = os.path.dirname(os.path.abspath(__file__))
+    for f in sorted(glob.glob(os.path.join(here, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") == want and kernel in d.get("kernels", {}):
+            return round(d["kernels"][kernel]["traffic_bytes"]), os.path.relpath(f, here)
+    return None, None
 
 
 if __name__ == "__main__":

@@ -1,0 +1,14 @@
+#!/bin/bash
+# HBM traffic per kernel launch of the bench workload (MI355X_MICROARCH.md §HBM): two PMC
+# passes (FETCH_SIZE, WRITE_SIZE cannot share one), then scripts/pmc_traffic.py.
+# usage (GPU box): bash scripts/pmc_traffic.sh OUTNAME [bench args...]
+set -u
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$1; shift
+mkdir -p $OUT
+for c in FETCH_SIZE WRITE_SIZE; do
+  (cd /tmp && timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o run -- \
+    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $OUT/$c.log 2>&1) || { echo "pass $c failed"; exit 1; }
+done
+python3 $R/scripts/pmc_traffic.py $OUT > $OUT/traffic.json && cat $OUT/traffic.json
