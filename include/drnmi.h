@@ -143,6 +143,107 @@ int drnmi_mask_apply_bits_f32(int32_t ntensors, float* const* weights,
 int drnmi_confusion_matrix(const void* pred, int32_t pred_dtype, const void* label, int32_t label_dtype,
                            int64_t npix, int32_t nclass, int64_t* hist, void* stream);
 
+/* ======================================================================================
+ * Fine-tune (train-mode) path, fp32 — csrc/train.hip.
+ * Replaces the reference training step (semantic_seg.py:166-230): model.train() forward
+ * with batch-statistics BatchNorm (lmodels/drn.py:7), CrossEntropyLoss(ignore_index=255) on
+ * the log-probs (semantic_seg.py:817, :197-198), loss.backward(), torch.optim.SGD(momentum,
+ * weight_decay) (:963-966, :212) and Pruner.apply_masks (:213-214, pruners/Pruner.py:17-20).
+ * Conv forward and data-gradient passes go through drnmi_conv2d_bn_act (fp32): dgrad is a
+ * stride-1 conv of dy with weights packed by drnmi_pack_conv_weight(mode = 1), after
+ * drnmi_zero_insert_f32 for stride-s convs.  All reductions are fp64, fixed order
+ * (bit-reproducible).  Workspaces are caller-provided device buffers of the queried size.
+ * ====================================================================================== */
+
+/* OIHW fp32 weights -> packed [rows_pad][k_pad] (out_dtype F32 or BF16), zero elsewhere.
+ * mode 0 (forward):  row = co, k = (kh*ks + kw)*kin_stride + ci, value w[co][ci][kh][kw] *
+ *                    row_scale[co] (row_scale may be NULL = 1; folds an eval BN scale).
+ * mode 1 (dgrad):    row = ci, k = (kh*ks + kw)*kin_stride + co, value
+ *                    w[co][ci][ks-1-kh][ks-1-kw] (transposed, spatially flipped).
+ * Replaces the host-side permute/pad of the conv weights (lmodels/drn.py:27-29 layout). */
+int drnmi_pack_conv_weight(const float* w, int32_t cout, int32_t cin, int32_t ks, int32_t kin_stride,
+                           int32_t rows_pad, int32_t k_pad, int32_t mode, const float* row_scale,
+                           int32_t out_dtype, void* out, void* stream);
+
+/* Workspace bytes for the per-channel reductions over `rows` x `channels` (power of two >= 4). */
+int64_t drnmi_reduce_workspace_bytes(int64_t rows, int32_t channels);
+
+/* Train-mode BatchNorm2d statistics over rows of NHWC y [rows][C]: mean, invstd =
+ * 1/sqrt(biased_var + eps); if running_mean/var are given: r = (1-momentum)*r + momentum*batch
+ * (running_var with the unbiased variance), and *num_batches_tracked += 1 (if non-NULL). */
+int drnmi_bn_stats_f32(const float* y, int64_t rows, int32_t C, float eps, float momentum,
+                       float* mean, float* invstd, float* running_mean, float* running_var,
+                       int64_t* num_batches_tracked, void* ws, void* stream);
+
+/* z = relu?(((y - mean) * invstd) * gamma + beta [+ res]) over [rows][C]; gamma/beta/res NULL-able.
+ * (BasicBlock / Bottleneck tail: lmodels/drn.py:49-65, :86-106.) */
+int drnmi_bn_act_f32(const float* y, const float* mean, const float* invstd, const float* gamma,
+                     const float* beta, const float* res, int32_t relu, int64_t rows, int32_t C,
+                     float* z, void* stream);
+
+/* Backward of drnmi_bn_act_f32 (train-mode BN): dr = dz * (relu ? z > 0 : 1);
+ * dbeta = sum dr, dgamma = sum dr * xhat; dy = gamma*invstd*(dr - mean(dr) - xhat*mean(dr*xhat));
+ * dres (NULL-able) = dr (or += dr with dres_accumulate).  dy may alias dz.
+ * grad_accumulate: dgamma/dbeta += instead of =. */
+int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float* y, const float* mean,
+                         const float* invstd, const float* gamma, int32_t relu, int64_t rows,
+                         int32_t C, float* dy, float* dres, int32_t dres_accumulate, float* dgamma,
+                         float* dbeta, int32_t grad_accumulate, void* ws, void* stream);
+
+/* out[c] (+)= sum over rows of x[row][c], c < cvalid (row stride C).  Conv-bias gradient
+ * (seg 1x1 + bias, lmodels/drnseg.py:278-284). */
+int drnmi_channel_sum_f32(const float* x, int64_t rows, int32_t C, int32_t cvalid, float* out,
+                          int32_t accumulate, void* ws, void* stream);
+
+/* Weight gradient of a conv: dw[co][ci][kh][kw] (+)= sum_pixels dy[pix][co] * x[tap(pix)][ci].
+ * dy: NHWC [n*ho*wo][dy_stride] (first cout valid), x: NHWC [n][h][w][cin_stride]. */
+typedef struct drnmi_wgrad_args {
+  const float* dy;
+  const float* x;
+  float* dw;             /* OIHW [cout][cin][ks][ks] fp32 (the parameter's .grad)          */
+  void* ws;              /* workspace, ws_bytes >= drnmi_conv_wgrad_workspace_bytes()      */
+  int64_t ws_bytes;
+  int32_t n, h, w, cin, cin_stride, ho, wo, cout, dy_stride;
+  int32_t ks, stride, pad, dil;
+  int32_t accumulate;    /* 1: dw += ; 0: dw =                                            */
+} drnmi_wgrad_args;
+int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* args);
+int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* args, void* stream);
+
+/* out[n][y][x][c] = dy[n][y/s][x/s][c] where y, x are multiples of s (and inside dy), else 0;
+ * out is [n][hu][wu][c] (c % 4 == 0).  Input of the stride-1 dgrad conv of a stride-s conv. */
+int drnmi_zero_insert_f32(const float* dy, int32_t n, int32_t ho, int32_t wo, int32_t c, int32_t stride,
+                          int32_t hu, int32_t wu, float* out, void* stream);
+
+/* Head backward: du = grad_scale * (g_lp - exp(lp) * sum_c g_lp) (LogSoftmax, dim 1), then
+ * dlogits = up^T(du) [+ g_logits] — the transpose of the fixed bilinear ConvTranspose2d(k16,
+ * s8, p4) (lmodels/drnseg.py:285-299).  g_logprobs/logprobs/du_ws: NCHW [n][c][8h][8w];
+ * dlogits/g_logits: [n][c][h][w]; g_logprobs NULL = logits-only gradient. */
+int drnmi_up8_lsm_bwd_f32(const float* g_logprobs, const float* logprobs, const float* g_logits,
+                          const float* up_w, float grad_scale, int32_t n, int32_t c, int32_t h,
+                          int32_t w, float* du_ws, float* dlogits, void* stream);
+
+/* CrossEntropyLoss(ignore_index) applied to log-probs [n][c][hw] with int64 targets [n][hw]:
+ * loss[0] = mean over target != ignore of (logsumexp(lp) - lp[target]) (NaN if a target is out
+ * of range), count[0] = number of counted pixels.  Device scalars; ws of drnmi_ce_workspace_bytes. */
+int64_t drnmi_ce_workspace_bytes(void);
+int drnmi_ce_loss_f32(const float* logprobs, const int64_t* target, int32_t n, int32_t c, int64_t hw,
+                      int64_t ignore_index, float* loss, float* count, void* ws, void* stream);
+/* g_logprobs = dloss[0] / count[0] * (softmax(lp) - onehot(target)), 0 on ignored pixels. */
+int drnmi_ce_loss_bwd_f32(const float* logprobs, const int64_t* target, int32_t n, int32_t c, int64_t hw,
+                          int64_t ignore_index, const float* dloss, const float* count,
+                          float* g_logprobs, void* stream);
+
+/* Multi-tensor torch.optim.SGD step (semantic_seg.py:963-966, torch semantics: d = g + wd*w;
+ * buf = first ? d : momentum*buf + (1-dampening)*d; d = nesterov ? d + momentum*buf : buf;
+ * w -= lr*d) with the pruner mask fused: w *= bit (mask_bits[t] NULL-able; NULL array = none).
+ * params/grads/momentum_bufs/numels/mask_bits/first_step are HOST arrays of device pointers. */
+int drnmi_sgd_step_f32(int32_t ntensors, float* const* params, const float* const* grads,
+                       float* const* momentum_bufs, const int64_t* numels,
+                       const uint32_t* const* mask_bits, const int32_t* first_step, float lr,
+                       float momentum, float dampening, float weight_decay, int32_t nesterov,
+                       void* stream);
+
 /* Library version string, e.g. "drnmi 0.1.0 gfx950". */
 const char* drnmi_version(void);
 

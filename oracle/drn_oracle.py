@@ -43,7 +43,18 @@ INFO_MEAN = (0.29010095242892997, 0.32808144844279574, 0.28696394422942517)
 INFO_STD = (0.1829540508368939, 0.18656561047509476, 0.18447508988480435)
 
 
+_TRAIN = {"on": False}
+
+
 def _bn(sd, p, x):
+    """BatchNorm2d (lmodels/drn.py:7): eval uses running stats; train mode (the fine-tune
+    path) normalises by batch stats and updates the running stats in place (momentum 0.1,
+    unbiased running var) and num_batches_tracked."""
+    if _TRAIN["on"]:
+        if (p + ".num_batches_tracked") in sd:
+            sd[p + ".num_batches_tracked"] += 1
+        return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"],
+                            sd[p + ".bias"], training=True, momentum=0.1, eps=1e-5)
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"], sd[p + ".weight"],
                         sd[p + ".bias"], training=False, momentum=0.0, eps=1e-5)
 
@@ -154,6 +165,53 @@ def preprocess_u8(frames_hwc: np.ndarray, mean=INFO_MEAN, std=INFO_STD) -> torch
     for c in range(3):
         t[:, c].sub_(mean[c]).div_(std[c])
     return t
+
+
+TRAINABLE_SUFFIXES = (".weight", ".bias")
+
+
+def trainable_keys(sd):
+    """optim_parameters() of DRNSeg (semantic_seg.py:160-164): every layer.* / seg.* weight and
+    bias (convs and BN affine), excluding up.weight."""
+    return [k for k in sd if k.endswith(TRAINABLE_SUFFIXES) and not k.startswith("up.")]
+
+
+def drnseg_train_steps(sd, arch, inputs, targets, lr=0.01, momentum=0.9, weight_decay=1e-4,
+                       masks=None, ignore_index=255, dtype=torch.float32):
+    """The reference fine-tune loop body (semantic_seg.py:166-230) for len(inputs) steps:
+    train-mode forward, CrossEntropyLoss(ignore_index) on the log-probs (:817, :197-198),
+    zero_grad, backward, torch.optim.SGD(momentum, weight_decay) step (:963-966), then
+    Pruner.apply_masks (:213-214).  Returns (losses, grads of the LAST step, final state_dict);
+    sd is not modified.  dtype=torch.float64 gives the exact-arithmetic yardstick the fp32
+    implementations (the reference's and ours) are both measured against."""
+    sd = {k: v.detach().clone() for k, v in sd.items()}
+    for k, v in sd.items():
+        if v.is_floating_point():
+            sd[k] = v.to(dtype)
+    keys = trainable_keys(sd)
+    params = [sd[k].requires_grad_(True) for k in keys]
+    opt = torch.optim.SGD(params, lr, momentum=momentum, weight_decay=weight_decay)
+    losses, grads = [], {}
+    _TRAIN["on"] = True
+    try:
+        for x, t in zip(inputs, targets):
+            feat, _ = backbone(sd, arch, x.to(dtype))
+            logits = _conv(sd, "seg", feat, bias=True)
+            lp = up_logsoftmax(sd, logits)
+            loss = F.cross_entropy(lp, t.long(), ignore_index=ignore_index)
+            opt.zero_grad()
+            loss.backward()
+            grads = {k: sd[k].grad.detach().clone() for k in keys}
+            opt.step()
+            if masks:
+                with torch.no_grad():
+                    for k, m in masks.items():
+                        sd[k].mul_(m.to(dtype))
+            losses.append(float(loss.detach()))
+    finally:
+        _TRAIN["on"] = False
+    out = {k: v.detach().clone() for k, v in sd.items()}
+    return losses, grads, out
 
 
 def apply_masks(weights: dict, masks: dict) -> dict:

@@ -1,0 +1,50 @@
+"""Diagnostic: per-parameter gradient error of one HIP train step vs the oracle in fp32 and fp64."""
+import sys, os
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "video-seg-model-compress_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+import torch
+import torch.nn.functional as F
+import train_case as TC
+from oracle import drn_oracle as O
+from drnmi.drnseg import DRNSeg
+from drnmi.weights import synth_state_dict
+from drnmi.train import CrossEntropyLoss
+
+
+def grads_in(dtype, sd, arch, x, t):
+    sd = {k: (v.detach().clone().to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+    keys = O.trainable_keys(sd)
+    for k in keys:
+        sd[k].requires_grad_(True)
+    O._TRAIN["on"] = True
+    feat, _ = O.backbone(sd, arch, x.to(dtype))
+    O._TRAIN["on"] = False
+    lp = O.up_logsoftmax(sd, O._conv(sd, "seg", feat, bias=True))
+    loss = F.cross_entropy(lp, t, ignore_index=255)
+    loss.backward()
+    return float(loss), {k: sd[k].grad.double() for k in keys}
+
+
+arch = sys.argv[1] if len(sys.argv) > 1 else "drn_d_22"
+H = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+torch.manual_seed(0)
+m = DRNSeg(arch, 19, pretrained=False)
+m.load_state_dict(synth_state_dict(m, 11))
+x = torch.randn(2, 3, H, H)
+t = torch.randint(0, 19, (2, H, H))
+sd0 = m.state_dict()
+l32, g32 = grads_in(torch.float32, sd0, arch, x, t)
+l64, g64 = grads_in(torch.float64, sd0, arch, x, t)
+m = m.cuda().train()
+out = m(x.cuda())[0]
+loss = CrossEntropyLoss(ignore_index=255)(out, t.cuda())
+loss.backward()
+print("loss hip", float(loss), "fp32", l32, "fp64", l64)
+print(f"{'param':40s} {'hip-vs-64':>10s} {'f32-vs-64':>10s}")
+for k, p in m.named_parameters():
+    if k.startswith("up."):
+        continue
+    eh = TC.rel_err(p.grad.detach().double().cpu().numpy(), g64[k].numpy())
+    e3 = TC.rel_err(g32[k].numpy(), g64[k].numpy())
+    print(f"{k:40s} {eh:10.2e} {e3:10.2e}")

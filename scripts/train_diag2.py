@@ -1,0 +1,50 @@
+"""Diagnostic: gradient wrt each stage output (layer0..layer8), HIP vs fp64 oracle, golden case step 1."""
+import sys, os
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "video-seg-model-compress_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
+import torch
+import torch.nn.functional as F
+import train_case as TC
+from oracle import drn_oracle as O
+from drnmi.train import CrossEntropyLoss, TrainRunner
+
+g = TC.load()
+m, pr = TC.model_and_masks(g)
+xs, ts = TC.inputs(g)
+x, t = xs[0], ts[0]
+
+
+def stage_grads(dtype):
+    sd = {k: (v.detach().clone().to(dtype) if v.is_floating_point() else v.clone()) for k, v in m.state_dict().items()}
+    keys = O.trainable_keys(sd)
+    for k in keys:
+        sd[k].requires_grad_(True)
+    O._TRAIN["on"] = True
+    feat, stages = O.backbone(sd, "drn_d_22", x.to(dtype))
+    O._TRAIN["on"] = False
+    for v in stages.values():
+        v.retain_grad()
+    lp = O.up_logsoftmax(sd, O._conv(sd, "seg", feat, bias=True))
+    F.cross_entropy(lp, t, ignore_index=255).backward()
+    return {k: v.grad.double() for k, v in stages.items()}, {k: sd[k].grad.double() for k in keys}
+
+
+s32, p32 = stage_grads(torch.float32)
+s64, p64 = stage_grads(torch.float64)
+mc = m.cuda().train()
+mc._train_runner = TrainRunner(mc)
+mc._train_runner.debug_value_grads = {}
+out = mc(x.cuda())[0]
+CrossEntropyLoss(ignore_index=255)(out, t.cuda()).backward()
+dbg = mc._train_runner.debug_value_grads
+for st, v in mc._graph.stage_outputs.items():
+    if v not in dbg:
+        print(st, "no grad captured"); continue
+    ref = s64[st]
+    n, c, h, w = ref.shape
+    hip = dbg[v].double().cpu().reshape(n, h, w, -1)[..., :c].permute(0, 3, 1, 2)
+    print(f"{st:8s} hip {TC.rel_err(hip.numpy(), ref.numpy()):.2e}  cpu32 {TC.rel_err(s32[st].numpy(), ref.numpy()):.2e}")
+for k, p in mc.named_parameters():
+    if k in p64:
+        print(f"{k:32s} hip {TC.rel_err(p.grad.double().cpu().numpy(), p64[k].numpy()):.2e}  cpu32 {TC.rel_err(p32[k].numpy(), p64[k].numpy()):.2e}  l2 hip {TC.rel_l2(p.grad.double().cpu().numpy(), p64[k].numpy()):.2e} cpu32 {TC.rel_l2(p32[k].numpy(), p64[k].numpy()):.2e}")

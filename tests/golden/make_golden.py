@@ -16,6 +16,10 @@ drnmi.weights.synth_state_dict, which keys only on state_dict names):
                 the external-kernel make_kwargs/exec_args fields are dropped)
   bsr_8x8.txt / rmb_8x8.txt    BlockPruner / RmbPruner text dumps of a seeded 8x8 matrix
   block_test.txt               the reference's committed fixture (pruners/block_test.txt)
+  train.npz     two reference fine-tune steps of D-22 (train-mode BN, CrossEntropyLoss(255),
+                SGD lr 1e-3 momentum 0.9 wd 1e-4, BlockPruner masks applied before and after each
+                step): losses, last-step grads and final params (full for small tensors,
+                every 97th element otherwise, plus sum / abs-sum), running stats
 """
 from __future__ import annotations
 
@@ -298,6 +302,63 @@ def dump_cases(tmp):
     return out
 
 
+def train_cases(tmp):
+    """Two reference fine-tune steps (semantic_seg.py:166-230 loop body) of D-22 at 2x3x64x64:
+    model.train(); output = model(input)[0]; CrossEntropyLoss(ignore_index=255); zero_grad;
+    backward; SGD(optim_parameters(), lr, momentum=0.9, weight_decay=1e-4) (:963-966); then
+    BlockPruner.apply_masks (:213-214; masks generated once before training, :1063)."""
+    from pruners.BlockPruner import BlockPruner
+    out = {}
+    m = ref_seg_model(REF, "drn_d_22")
+    m.load_state_dict(synth_state_dict(m, 11))
+    pr = BlockPruner(os.path.join(HERE, "block_d22_4x4_sub32.json"), on_gpu=False)
+    pr.generate_masks(m, is_static=False)
+    pr.apply_masks(m)
+    g = torch.Generator().manual_seed(123)
+    xs = [torch.randn(2, 3, 64, 64, generator=g) for _ in range(2)]
+    ts = []
+    for _ in range(2):
+        t = torch.randint(0, 19, (2, 64, 64), generator=g)
+        t[torch.rand(2, 64, 64, generator=g) < 0.1] = 255
+        ts.append(t)
+    crit = torch.nn.CrossEntropyLoss(ignore_index=255)
+    # lr 1e-3: with the reference default 0.01 the second step of this tiny hash-initialised case
+    # is ill-conditioned (fp32 vs fp64 gradients differ by 1.25e-2 rel-L2); at 1e-3 they agree to 3e-6
+    opt = torch.optim.SGD(m.optim_parameters(), 0.001, momentum=0.9, weight_decay=1e-4)
+    m.train()
+    losses = []
+    for x, t in zip(xs, ts):
+        output = m(x)[0]
+        loss = crit(output, t.long())
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        pr.apply_masks(m)
+        losses.append(float(loss))
+    out["d22_train/meta"] = np.array([11, 2, 64, 64])
+    out["d22_train/losses"] = np.array(losses, dtype=np.float64)
+    for i in range(2):
+        out[f"d22_train/x{i}"] = xs[i].numpy()
+        out[f"d22_train/t{i}"] = ts[i].numpy().astype(np.uint8)
+    for layer, mk in pr.mask_dict.items():
+        out[f"d22_train/mask_sha/{layer}"] = np.array(sha(mk.numpy() != 0))
+    sd = m.state_dict()
+    named = dict(m.named_parameters())
+    for k, v in sd.items():
+        if k.startswith("up."):
+            continue
+        v = v.detach().float().numpy()
+        out[f"d22_train/final/{k}"] = v.reshape(-1)[::97][:256] if v.size > 4096 else v.reshape(-1)
+        out[f"d22_train/final_sum/{k}"] = np.array([v.sum(dtype=np.float64), np.abs(v).sum(dtype=np.float64)])
+        p = named.get(k)
+        if p is not None and p.grad is not None:
+            gr = p.grad.detach().numpy()
+            out[f"d22_train/grad/{k}"] = gr.reshape(-1)[::97][:256] if gr.size > 4096 else gr.reshape(-1)
+            out[f"d22_train/grad_sum/{k}"] = np.array([gr.sum(dtype=np.float64), np.abs(gr).sum(dtype=np.float64)])
+    print("train losses", losses)
+    return out
+
+
 def main():
     global REF
     ap = argparse.ArgumentParser()
@@ -315,6 +376,8 @@ def main():
                 np.savez_compressed(os.path.join(HERE, "forward.npz"), **forward_cases())
             if args.only in ("", "masks"):
                 np.savez_compressed(os.path.join(HERE, "masks.npz"), **mask_cases(tmp))
+            if args.only in ("", "train"):
+                np.savez_compressed(os.path.join(HERE, "train.npz"), **train_cases(tmp))
             if args.only in ("", "dumps"):
                 np.savez_compressed(os.path.join(HERE, "dumps.npz"), **dump_cases(tmp))
         finally:

@@ -1,0 +1,922 @@
+// Fine-tune (train-mode) kernels: the backward half of the DRN-D hot path, fp32.
+//
+// The reference fine-tunes DRNSeg with train-mode BatchNorm, CrossEntropyLoss on the
+// log-probs, SGD(momentum, weight_decay) and Pruner.apply_masks after every step
+// (semantic_seg.py:166-230, :817, :963-966; pruners/Pruner.py:17-20).  The convs' forward
+// and data-gradient (dgrad) passes reuse the implicit-GEMM conv of conv_igemm.hip (dgrad =
+// a stride-1 conv of dy with transposed/flipped weights, after a zero-insert for stride-s
+// layers); this file holds everything else:
+//
+//   pack_conv_weight   OIHW fp32 -> packed [rows_pad][k_pad] (forward or dgrad layout)
+//   bn stats / apply   train-mode BatchNorm2d: batch mean / biased var, running-stat update
+//                      (momentum, unbiased var), y -> relu(bn(y) [+ res])
+//   bn backward        relu mask, dgamma / dbeta, dy, residual-branch gradient
+//   channel_sum        per-channel column sums (conv bias gradient)
+//   conv_wgrad         weight gradient: GEMM over pixels, v_mfma_f32_16x16x4f32, split over
+//                      pixel ranges with a fixed-order (deterministic) reduction
+//   zero_insert        dy of a stride-s conv spread onto the input grid (dgrad input)
+//   up8_lsm_bwd        LogSoftmax backward + transpose of the fixed bilinear up-conv
+//   ce_loss            CrossEntropyLoss(ignore_index) forward / backward on log-probs
+//   sgd_step           torch.optim.SGD step (momentum, dampening, wd, nesterov) with the
+//                      pruner mask (bit-packed) applied in the same pass
+//
+// Every reduction accumulates in fp64 in a fixed order (no atomics), so results are
+// bit-reproducible run to run.
+#include "common.h"
+
+namespace drnmi {
+namespace {
+
+constexpr int kThreads = 256;
+
+inline unsigned grid_of(int64_t n, int per = kThreads) {
+  const int64_t g = (n + per - 1) / per;
+  return static_cast<unsigned>(g < 1 ? 1 : (g > 65535 * 16 ? 65535 * 16 : g));
+}
+
+// ------------------------------------------------------------------ weight packing
+// mode 0 (forward): out[co][ (kh*ks + kw) * kin_stride + ci ] = w[co][ci][kh][kw] * scale[co]
+// mode 1 (dgrad):   out[ci][ (kh'*ks + kw') * kin_stride + co ] = w[co][ci][ks-1-kh'][ks-1-kw']
+// Everything else in [rows_pad][k_pad] is zero.
+template <typename TO>
+__global__ void __launch_bounds__(kThreads)
+pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int ks, int kin_stride, int rows_pad,
+                   int k_pad, int mode, const float* __restrict__ scale, TO* __restrict__ out) {
+  const int64_t total = static_cast<int64_t>(rows_pad) * k_pad;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int row = static_cast<int>(i / k_pad);
+    const int k = static_cast<int>(i - static_cast<int64_t>(row) * k_pad);
+    const int tap = k / kin_stride;
+    const int c = k - tap * kin_stride;
+    float v = 0.f;
+    if (tap < ks * ks) {
+      const int kh = tap / ks, kw = tap - (tap / ks) * ks;
+      if (mode == 0) {
+        if (row < cout && c < cin) {
+          v = w[((static_cast<int64_t>(row) * cin + c) * ks + kh) * ks + kw];
+          if (scale != nullptr) v *= scale[row];
+        }
+      } else {
+        // row = ci (dgrad output channel), c = co (dgrad input channel)
+        if (row < cin && c < cout)
+          v = w[((static_cast<int64_t>(c) * cin + row) * ks + (ks - 1 - kh)) * ks + (ks - 1 - kw)];
+      }
+    }
+    if constexpr (sizeof(TO) == 2) out[i] = f32_to_bf16(v);
+    else out[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------ column reductions
+// Rows x C (C = row stride, a power of two >= 4), fp32 in, fp64 partial sums.
+// Block: TPR threads per row (4 channels each, float4), RG = 256 / TPR row groups.
+// grid = (G splits, C / (4 * TPR) channel chunks).  Partials ws[2][G][C] (S1, S2).
+enum { RED_STATS = 0, RED_BNBWD = 1, RED_SUM = 2 };
+
+struct RedArgs {
+  const float* a;       // STATS: y ; BNBWD: dz ; SUM: x
+  const float* z;       // BNBWD: z (relu mask), or NULL
+  const float* y;       // BNBWD: y (pre-BN conv output)
+  int64_t rows;
+  int C;
+  int G;
+  int64_t rows_per_split;
+  int relu;
+  double* ws;
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) colred_kernel(const RedArgs r) {
+  const int tpr = (r.C / 4) < 64 ? (r.C / 4) : 64;
+  const int rg = kThreads / tpr;
+  const int t = threadIdx.x;
+  const int tc = t % tpr;
+  const int tr = t / tpr;
+  const int c0 = blockIdx.y * 4 * tpr + 4 * tc;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * r.rows_per_split;
+  const int64_t r1 = (r0 + r.rows_per_split) < r.rows ? (r0 + r.rows_per_split) : r.rows;
+  double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  for (int64_t row = r0 + tr; row < r1; row += rg) {
+    const int64_t off = row * r.C + c0;
+    const float4 av = *reinterpret_cast<const float4*>(r.a + off);
+    float a[4] = {av.x, av.y, av.z, av.w};
+    if constexpr (MODE == RED_STATS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s1[j] += a[j];
+        s2[j] += static_cast<double>(a[j]) * a[j];
+      }
+    } else if constexpr (MODE == RED_BNBWD) {
+      if (r.relu) {
+        const float4 zv = *reinterpret_cast<const float4*>(r.z + off);
+        a[0] = zv.x > 0.f ? a[0] : 0.f;
+        a[1] = zv.y > 0.f ? a[1] : 0.f;
+        a[2] = zv.z > 0.f ? a[2] : 0.f;
+        a[3] = zv.w > 0.f ? a[3] : 0.f;
+      }
+      const float4 yv = *reinterpret_cast<const float4*>(r.y + off);
+      const float y[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s1[j] += a[j];
+        s2[j] += static_cast<double>(a[j]) * y[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s1[j] += a[j];
+    }
+  }
+  __shared__ double sh1[kThreads * 4], sh2[kThreads * 4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sh1[t * 4 + j] = s1[j];
+    sh2[t * 4 + j] = s2[j];
+  }
+  __syncthreads();
+  // thread q < 4*tpr sums channel q of the block over the rg row groups, in order
+  if (t < 4 * tpr) {
+    const int q_tc = t / 4, q_j = t % 4;
+    double a1 = 0, a2 = 0;
+    for (int g = 0; g < rg; ++g) {
+      a1 += sh1[(g * tpr + q_tc) * 4 + q_j];
+      a2 += sh2[(g * tpr + q_tc) * 4 + q_j];
+    }
+    const int c = blockIdx.y * 4 * tpr + t;
+    r.ws[static_cast<int64_t>(blockIdx.x) * r.C + c] = a1;
+    r.ws[static_cast<int64_t>(r.G + blockIdx.x) * r.C + c] = a2;
+  }
+}
+
+int red_splits(int64_t rows, int C) {
+  const int tpr = (C / 4) < 64 ? (C / 4) : 64;
+  const int chunks = C / (4 * tpr);
+  const int rg = kThreads / tpr;
+  int64_t g = 1024 / chunks;
+  const int64_t by_rows = (rows + 16 * rg - 1) / (16 * rg);   // >= 16 rows per thread
+  if (g > by_rows) g = by_rows;
+  return static_cast<int>(g < 1 ? 1 : g);
+}
+
+template <int MODE>
+hipError_t launch_colred(RedArgs& r, hipStream_t s) {
+  const int tpr = (r.C / 4) < 64 ? (r.C / 4) : 64;
+  r.G = red_splits(r.rows, r.C);
+  r.rows_per_split = (r.rows + r.G - 1) / r.G;
+  hipLaunchKernelGGL(colred_kernel<MODE>, dim3(r.G, r.C / (4 * tpr)), dim3(kThreads), 0, s, r);
+  return hipGetLastError();
+}
+
+// finalize: one thread per channel, partials summed in split order.
+__global__ void __launch_bounds__(kThreads)
+bn_stats_final_kernel(const double* __restrict__ ws, int G, int C, int64_t rows, float eps, float momentum,
+                      float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rmean,
+                      float* __restrict__ rvar, int64_t* __restrict__ nbt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt != nullptr) nbt[0] += 1;
+  if (c >= C) return;
+  double s1 = 0, s2 = 0;
+  for (int g = 0; g < G; ++g) {
+    s1 += ws[static_cast<int64_t>(g) * C + c];
+    s2 += ws[static_cast<int64_t>(G + g) * C + c];
+  }
+  const double m = s1 / static_cast<double>(rows);
+  double var = s2 / static_cast<double>(rows) - m * m;
+  if (var < 0) var = 0;
+  const float mf = static_cast<float>(m);
+  const float vf = static_cast<float>(var);
+  mean[c] = mf;
+  invstd[c] = 1.f / sqrtf(vf + eps);
+  if (rmean != nullptr) {
+    const float unb = rows > 1 ? static_cast<float>(var * static_cast<double>(rows) / static_cast<double>(rows - 1)) : vf;
+    rmean[c] = momentum * mf + (1.f - momentum) * rmean[c];
+    rvar[c] = momentum * unb + (1.f - momentum) * rvar[c];
+  }
+}
+
+// z = relu?(((y - mean) * invstd) * gamma + beta [+ res]) over [rows][C], float4 lanes
+__global__ void __launch_bounds__(kThreads)
+bn_act_kernel(const float* __restrict__ y, const float* __restrict__ mean, const float* __restrict__ invstd,
+              const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ res,
+              int relu, int64_t n4, int C, float* __restrict__ z) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>((i * 4) & (C - 1));
+    const float4 v = reinterpret_cast<const float4*>(y)[i];
+    float o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float g = gamma != nullptr ? gamma[c + j] : 1.f;
+      const float b = beta != nullptr ? beta[c + j] : 0.f;
+      o[j] = ((o[j] - mean[c + j]) * invstd[c + j]) * g + b;
+    }
+    if (res != nullptr) {
+      const float4 rv = reinterpret_cast<const float4*>(res)[i];
+      o[0] += rv.x; o[1] += rv.y; o[2] += rv.z; o[3] += rv.w;
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    reinterpret_cast<float4*>(z)[i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// BN backward finalize: dbeta = S1, dgamma = invstd * (S2 - mean * S1) with S2 = sum(dr * y);
+// coefficients for dy = a * (dr - b - (y - mean) * d):
+//   a = gamma * invstd, b = S1 / rows, d = invstd^2 * (S2 - mean * S1) / rows
+__global__ void __launch_bounds__(kThreads)
+bn_bwd_final_kernel(const double* __restrict__ ws, int G, int C, int64_t rows, const float* __restrict__ mean,
+                    const float* __restrict__ invstd, const float* __restrict__ gamma, float* __restrict__ dgamma,
+                    float* __restrict__ dbeta, int accumulate, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0, s2 = 0;
+  for (int g = 0; g < G; ++g) {
+    s1 += ws[static_cast<int64_t>(g) * C + c];
+    s2 += ws[static_cast<int64_t>(G + g) * C + c];
+  }
+  const double is = invstd[c];
+  const double sx = s2 - static_cast<double>(mean[c]) * s1;   // sum(dr * (y - mean))
+  const float dg = static_cast<float>(is * sx);
+  const float db = static_cast<float>(s1);
+  if (dgamma != nullptr) dgamma[c] = accumulate ? dgamma[c] + dg : dg;
+  if (dbeta != nullptr) dbeta[c] = accumulate ? dbeta[c] + db : db;
+  const double g = gamma != nullptr ? gamma[c] : 1.0;
+  coef[c] = static_cast<float>(g * is);
+  coef[C + c] = static_cast<float>(s1 / static_cast<double>(rows));
+  coef[2 * C + c] = static_cast<float>(is * is * sx / static_cast<double>(rows));
+}
+
+__global__ void __launch_bounds__(kThreads)
+bn_bwd_apply_kernel(const float* dz, const float* __restrict__ z, const float* __restrict__ y,
+                    const float* __restrict__ mean, const float* __restrict__ coef, int relu, int64_t n4, int C,
+                    float* dy, float* dres, int dres_acc) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>((i * 4) & (C - 1));
+    const float4 gv = reinterpret_cast<const float4*>(dz)[i];
+    float dr[4] = {gv.x, gv.y, gv.z, gv.w};
+    if (relu) {
+      const float4 zv = reinterpret_cast<const float4*>(z)[i];
+      dr[0] = zv.x > 0.f ? dr[0] : 0.f;
+      dr[1] = zv.y > 0.f ? dr[1] : 0.f;
+      dr[2] = zv.z > 0.f ? dr[2] : 0.f;
+      dr[3] = zv.w > 0.f ? dr[3] : 0.f;
+    }
+    const float4 yv = reinterpret_cast<const float4*>(y)[i];
+    const float yy[4] = {yv.x, yv.y, yv.z, yv.w};
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = coef[c + j] * (dr[j] - coef[C + c + j] - (yy[j] - mean[c + j]) * coef[2 * C + c + j]);
+    if (dres != nullptr) {
+      float4 rv = make_float4(dr[0], dr[1], dr[2], dr[3]);
+      if (dres_acc) {
+        const float4 old = reinterpret_cast<const float4*>(dres)[i];
+        rv.x += old.x; rv.y += old.y; rv.z += old.z; rv.w += old.w;
+      }
+      reinterpret_cast<float4*>(dres)[i] = rv;
+    }
+    reinterpret_cast<float4*>(dy)[i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+colsum_final_kernel(const double* __restrict__ ws, int G, int C, int cvalid, float* __restrict__ out, int acc) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cvalid) return;
+  double s = 0;
+  for (int g = 0; g < G; ++g) s += ws[static_cast<int64_t>(g) * C + c];
+  out[c] = acc ? out[c] + static_cast<float>(s) : static_cast<float>(s);
+}
+
+// ------------------------------------------------------------------ weight gradient
+// dW[co][tap][ci] = sum_m dy[m][co] * x[pix(m, tap)][ci]: C = A * B with A = dy^T (co x m),
+// B = im2col(x) (m x k).  Tile 64 co x 64 k per workgroup (4 waves, 32 x 32 each, 2 x 2
+// fragments of v_mfma_f32_16x16x4f32), K loop over 32-pixel chunks of the block's pixel
+// split.  Operand tiles go to LDS transposed ([row][m]) so one ds_read_b128 feeds 4 MFMAs:
+// lane l reads m = mm + 4*(l/16) + {0..3}; MFMA j consumes element j of both operands,
+// so the pairing of A and B over m is identical and the 4 MFMAs together cover 16 pixels.
+struct WgradP {
+  const float* dy;
+  const float* x;
+  float* ws;
+  int dys, cout;
+  int n, h, w, cs, ho, wo, ks, stride, pad, dil;
+  int K;                 // ks * ks * cs
+  int64_t M;
+  int64_t pix_per_split;
+};
+
+constexpr int kWT = 64;      // tile rows / cols
+constexpr int kWM = 32;      // pixels per chunk
+constexpr int kWLD = kWM + 4;
+
+__global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
+  __shared__ __attribute__((aligned(16))) float As[2][kWT][kWLD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kWT][kWLD];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wr = wave >> 1, wcn = wave & 1;
+  const int co0 = blockIdx.y * kWT;
+  const int kc0 = blockIdx.x * kWT;
+  const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * p.pix_per_split;
+  int64_t m_end = m_begin + p.pix_per_split;
+  if (m_end > p.M) m_end = p.M;
+  const int lm = t >> 3;      // pixel row of the chunk this thread loads
+  const int lv = t & 7;       // 8-column group
+  const int hw = p.ho * p.wo;
+  // B column group: (tap, ci) fixed for the whole loop
+  const int kcol = kc0 + 8 * lv;
+  const int tap = kcol / p.cs;
+  const int ci = kcol - tap * p.cs;
+  const bool kval = kcol < p.K && tap < p.ks * p.ks;
+  const int kh = kval ? tap / p.ks : 0;
+  const int kw = kval ? tap - kh * p.ks : 0;
+  const int co = co0 + 8 * lv;
+
+  float ra[8], rb[8];
+  auto load = [&](int64_t mc) {
+    const int64_t m = mc + lm;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ra[j] = 0.f; rb[j] = 0.f; }
+    if (m >= m_end) return;
+    const float* dr = p.dy + m * p.dys;
+    if (co + 8 <= p.dys && co + 8 <= p.cout) {
+      const float4 a0 = *reinterpret_cast<const float4*>(dr + co);
+      const float4 a1 = *reinterpret_cast<const float4*>(dr + co + 4);
+      ra[0] = a0.x; ra[1] = a0.y; ra[2] = a0.z; ra[3] = a0.w;
+      ra[4] = a1.x; ra[5] = a1.y; ra[6] = a1.z; ra[7] = a1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (co + j < p.cout) ra[j] = dr[co + j];
+    }
+    if (kval) {
+      const int nn = static_cast<int>(m / hw);
+      const int q = static_cast<int>(m - static_cast<int64_t>(nn) * hw);
+      const int oh = q / p.wo;
+      const int ow = q - oh * p.wo;
+      const int ih = oh * p.stride - p.pad + kh * p.dil;
+      const int iw = ow * p.stride - p.pad + kw * p.dil;
+      if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.w)) {
+        const float* xr = p.x + ((static_cast<int64_t>(nn) * p.h + ih) * p.w + iw) * p.cs + ci;
+        const float4 b0 = *reinterpret_cast<const float4*>(xr);
+        const float4 b1 = *reinterpret_cast<const float4*>(xr + 4);
+        rb[0] = b0.x; rb[1] = b0.y; rb[2] = b0.z; rb[3] = b0.w;
+        rb[4] = b1.x; rb[5] = b1.y; rb[6] = b1.z; rb[7] = b1.w;
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      As[buf][8 * lv + j][lm] = ra[j];
+      Bs[buf][8 * lv + j][lm] = rb[j];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  int buf = 0;
+  load(m_begin);
+  store(0);
+  __syncthreads();
+  for (int64_t mc = m_begin; mc < m_end; mc += kWM) {
+    const bool more = mc + kWM < m_end;
+    if (more) load(mc + kWM);
+#pragma unroll
+    for (int mm = 0; mm < kWM; mm += 16) {
+      float4 a4[2], b4[2];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        a4[f] = *reinterpret_cast<const float4*>(&As[buf][wr * 32 + f * 16 + fr][mm + 4 * fq]);
+        b4[f] = *reinterpret_cast<const float4*>(&Bs[buf][wcn * 32 + f * 16 + fr][mm + 4 * fq]);
+      }
+#pragma unroll
+      for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+        for (int fj = 0; fj < 2; ++fj) {
+          acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].x, b4[fj].x, acc[fi][fj], 0, 0, 0);
+          acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].y, b4[fj].y, acc[fi][fj], 0, 0, 0);
+          acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].z, b4[fj].z, acc[fi][fj], 0, 0, 0);
+          acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].w, b4[fj].w, acc[fi][fj], 0, 0, 0);
+        }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // D[row = 4*(l/16) + r][col = l%16] of each 16x16 fragment; rows = co, cols = k
+  float* out = p.ws + static_cast<int64_t>(blockIdx.z) * p.cout * p.K;
+#pragma unroll
+  for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+    for (int fj = 0; fj < 2; ++fj) {
+      const int k = kc0 + wcn * 32 + fj * 16 + fr;
+      if (k >= p.K) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = co0 + wr * 32 + fi * 16 + 4 * fq + r;
+        if (c < p.cout) out[static_cast<int64_t>(c) * p.K + k] = acc[fi][fj][r];
+      }
+    }
+}
+
+// dw[co][ci][kh][kw] (+)= sum_z ws[z][co][(kh*ks + kw)*cs + ci]
+__global__ void __launch_bounds__(kThreads)
+wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin, int cs, int ks, int K,
+                    float* __restrict__ dw, int acc) {
+  const int64_t total = static_cast<int64_t>(cout) * cin * ks * ks;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int kw = static_cast<int>(i % ks);
+    const int kh = static_cast<int>((i / ks) % ks);
+    const int ci = static_cast<int>((i / (ks * ks)) % cin);
+    const int co = static_cast<int>(i / (static_cast<int64_t>(ks) * ks * cin));
+    const int64_t off = static_cast<int64_t>(co) * K + (kh * ks + kw) * cs + ci;
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += ws[static_cast<int64_t>(z) * cout * K + off];
+    dw[i] = acc ? dw[i] + s : s;
+  }
+}
+
+void wgrad_plan(const drnmi_wgrad_args& a, int* splits, int64_t* per) {
+  const int K = a.ks * a.ks * a.cin_stride;
+  const int64_t M = static_cast<int64_t>(a.n) * a.ho * a.wo;
+  const int64_t tiles = static_cast<int64_t>((a.cout + kWT - 1) / kWT) * ((K + kWT - 1) / kWT);
+  int64_t s = 2048 / tiles;
+  const int64_t by_pix = (M + 511) / 512;
+  if (s > by_pix) s = by_pix;
+  if (s > 512) s = 512;
+  if (s < 1) s = 1;
+  int64_t pp = (M + s - 1) / s;
+  pp = (pp + kWM - 1) / kWM * kWM;
+  s = (M + pp - 1) / pp;
+  if (s < 1) s = 1;
+  *splits = static_cast<int>(s);
+  *per = pp;
+}
+
+// ------------------------------------------------------------------ zero insert (stride-s dgrad)
+__global__ void __launch_bounds__(kThreads)
+zero_insert_kernel(const float* __restrict__ dy, int n, int ho, int wo, int c4, int s, int hu, int wu,
+                   float* __restrict__ out) {
+  const int64_t total = static_cast<int64_t>(n) * hu * wu * c4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int cv = static_cast<int>(i % c4);
+    const int64_t pix = i / c4;
+    const int x = static_cast<int>(pix % wu);
+    const int y = static_cast<int>((pix / wu) % hu);
+    const int b = static_cast<int>(pix / (static_cast<int64_t>(wu) * hu));
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (y % s == 0 && x % s == 0 && y / s < ho && x / s < wo)
+      v = reinterpret_cast<const float4*>(dy)[((static_cast<int64_t>(b) * ho + y / s) * wo + x / s) * c4 + cv];
+    reinterpret_cast<float4*>(out)[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------ head backward
+// du[n][c][p] = scale * (g[n][c][p] - exp(lp[n][c][p]) * sum_c' g[n][c'][p])  (LogSoftmax bwd)
+__global__ void __launch_bounds__(kThreads)
+lsm_bwd_kernel(const float* __restrict__ g, const float* __restrict__ lp, int nimg, int c, int64_t hw, float scale,
+               float* __restrict__ du) {
+  const int64_t total = static_cast<int64_t>(nimg) * hw;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t b = i / hw, p = i - b * hw;
+    const int64_t base = b * c * hw + p;
+    float s = 0.f;
+    for (int k = 0; k < c; ++k) s += g[base + k * hw];
+    for (int k = 0; k < c; ++k) {
+      const int64_t o = base + k * hw;
+      du[o] = scale * (g[o] - expf(lp[o]) * s);
+    }
+  }
+}
+
+// dlogits[n][c][i][j] = sum_{ky,kx} W[ky][kx] * du[n][c][8i-4+ky][8j-4+kx] (+ g_logits); the
+// transpose of ConvTranspose2d(k16, s8, p4) (lmodels/drnseg.py:285-293).
+__global__ void __launch_bounds__(kThreads)
+up8_bwd_kernel(const float* __restrict__ du, const float* __restrict__ upw, const float* __restrict__ glog,
+               int nc, int h, int w, float* __restrict__ dlog) {
+  __shared__ float wk[256];
+  wk[threadIdx.x] = upw[threadIdx.x];
+  __syncthreads();
+  const int H = 8 * h, W = 8 * w;
+  const int64_t total = static_cast<int64_t>(nc) * h * w;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int j = static_cast<int>(i % w);
+    const int ii = static_cast<int>((i / w) % h);
+    const int64_t plane = i / (static_cast<int64_t>(w) * h);
+    const float* src = du + plane * H * W;
+    float s = 0.f;
+    for (int ky = 0; ky < 16; ++ky) {
+      const int y = 8 * ii - 4 + ky;
+      if (static_cast<unsigned>(y) >= static_cast<unsigned>(H)) continue;
+      const float* row = src + static_cast<int64_t>(y) * W;
+      for (int kx = 0; kx < 16; ++kx) {
+        const int x = 8 * j - 4 + kx;
+        if (static_cast<unsigned>(x) < static_cast<unsigned>(W)) s += wk[ky * 16 + kx] * row[x];
+      }
+    }
+    if (glog != nullptr) s += glog[i];
+    dlog[i] = s;
+  }
+}
+
+// ------------------------------------------------------------------ cross entropy
+// per pixel: lse(lp) - lp[t] over t != ignore (CrossEntropyLoss applied to log-probs,
+// semantic_seg.py:817 + :197-198); block partials (sum, count) in fp64, fixed order.
+constexpr int kCeBlocks = 512;
+
+__global__ void __launch_bounds__(kThreads)
+ce_fwd_kernel(const float* __restrict__ lp, const int64_t* __restrict__ tgt, int nimg, int c, int64_t hw,
+              int64_t ignore, double* __restrict__ ws) {
+  const int64_t total = static_cast<int64_t>(nimg) * hw;
+  double s = 0, cnt = 0, bad = 0;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t t = tgt[i];
+    if (t == ignore) continue;
+    if (t < 0 || t >= c) { bad += 1; continue; }
+    const int64_t b = i / hw, p = i - b * hw;
+    const float* v = lp + b * c * hw + p;
+    float mx = -INFINITY;
+    for (int k = 0; k < c; ++k) mx = fmaxf(mx, v[k * hw]);
+    float se = 0.f;
+    for (int k = 0; k < c; ++k) se += expf(v[k * hw] - mx);
+    const float lse = mx + logf(se);
+    s += static_cast<double>(lse - v[t * hw]);
+    cnt += 1;
+  }
+  __shared__ double sh[3][kThreads];
+  sh[0][threadIdx.x] = s;
+  sh[1][threadIdx.x] = cnt;
+  sh[2][threadIdx.x] = bad;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sh[0][threadIdx.x] += sh[0][threadIdx.x + o];
+      sh[1][threadIdx.x] += sh[1][threadIdx.x + o];
+      sh[2][threadIdx.x] += sh[2][threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    ws[blockIdx.x] = sh[0][0];
+    ws[kCeBlocks + blockIdx.x] = sh[1][0];
+    ws[2 * kCeBlocks + blockIdx.x] = sh[2][0];
+  }
+}
+
+__global__ void ce_final_kernel(const double* __restrict__ ws, int blocks, float* __restrict__ loss,
+                                float* __restrict__ count) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0, cnt = 0, bad = 0;
+  for (int b = 0; b < blocks; ++b) {
+    s += ws[b];
+    cnt += ws[kCeBlocks + b];
+    bad += ws[2 * kCeBlocks + b];
+  }
+  // an out-of-range target is an error in the reference (device assert); surface it as NaN
+  loss[0] = bad > 0 ? __builtin_nanf("") : static_cast<float>(s / cnt);
+  count[0] = static_cast<float>(cnt);
+}
+
+__global__ void __launch_bounds__(kThreads)
+ce_bwd_kernel(const float* __restrict__ lp, const int64_t* __restrict__ tgt, int nimg, int c, int64_t hw,
+              int64_t ignore, const float* __restrict__ dloss, const float* __restrict__ count,
+              float* __restrict__ glp) {
+  const float sc = dloss[0] / count[0];
+  const int64_t total = static_cast<int64_t>(nimg) * hw;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t t = tgt[i];
+    const int64_t b = i / hw, p = i - b * hw;
+    const float* v = lp + b * c * hw + p;
+    float* o = glp + b * c * hw + p;
+    if (t == ignore || t < 0 || t >= c) {
+      for (int k = 0; k < c; ++k) o[k * hw] = 0.f;
+      continue;
+    }
+    float mx = -INFINITY;
+    for (int k = 0; k < c; ++k) mx = fmaxf(mx, v[k * hw]);
+    float se = 0.f;
+    for (int k = 0; k < c; ++k) se += expf(v[k * hw] - mx);
+    const float lse = mx + logf(se);
+    for (int k = 0; k < c; ++k) o[k * hw] = sc * (expf(v[k * hw] - lse) - (k == t ? 1.f : 0.f));
+  }
+}
+
+// ------------------------------------------------------------------ SGD (+ mask)
+constexpr int kSgdBatch = 48;
+struct SgdBatch {
+  float* w[kSgdBatch];
+  const float* g[kSgdBatch];
+  float* buf[kSgdBatch];
+  const uint32_t* mask[kSgdBatch];
+  int64_t numel[kSgdBatch];
+  int first[kSgdBatch];
+};
+
+// torch.optim.SGD (dampening d, nesterov off/on): d_p = g + wd * w;
+// buf = first ? d_p : m * buf + (1 - d) * d_p;  d_p = nesterov ? d_p + m * buf : buf;
+// w = w - lr * d_p; then w *= mask (Pruner.apply_masks fused, pruners/Pruner.py:17-20).
+__global__ void __launch_bounds__(kThreads)
+sgd_kernel(const SgdBatch b, float lr, float mom, float damp, float wd, int nesterov) {
+  const int t = blockIdx.y;
+  float* __restrict__ w = b.w[t];
+  const float* __restrict__ g = b.g[t];
+  float* __restrict__ buf = b.buf[t];
+  const uint32_t* __restrict__ mk = b.mask[t];
+  const int64_t n = b.numel[t];
+  const int first = b.first[t];
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    float d = g[i];
+    const float wv = w[i];
+    if (wd != 0.f) d = d + wd * wv;
+    if (mom != 0.f) {
+      float bv;
+      if (first) bv = d;
+      else bv = mom * buf[i] + (1.f - damp) * d;
+      buf[i] = bv;
+      d = nesterov ? d + mom * bv : bv;
+    }
+    float nw = wv - lr * d;
+    if (mk != nullptr) nw *= static_cast<float>((mk[i >> 5] >> (i & 31)) & 1u);
+    w[i] = nw;
+  }
+}
+
+}  // namespace
+}  // namespace drnmi
+
+using namespace drnmi;
+
+// ================================================================== C-ABI
+extern "C" int drnmi_pack_conv_weight(const float* w, int32_t cout, int32_t cin, int32_t ks, int32_t kin_stride,
+                                      int32_t rows_pad, int32_t k_pad, int32_t mode, const float* row_scale,
+                                      int32_t out_dtype, void* out, void* stream) {
+  if (w == nullptr || out == nullptr || cout <= 0 || cin <= 0 || ks <= 0 || kin_stride <= 0 || k_pad <= 0)
+    return DRNMI_EINVAL;
+  if (mode != 0 && mode != 1) return DRNMI_EINVAL;
+  if (k_pad < ks * ks * kin_stride) return DRNMI_EINVAL;
+  if (mode == 0 && (rows_pad < cout || kin_stride < cin)) return DRNMI_EINVAL;
+  if (mode == 1 && (rows_pad < cin || kin_stride < cout || row_scale != nullptr)) return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t total = static_cast<int64_t>(rows_pad) * k_pad;
+  if (out_dtype == DRNMI_F32)
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(grid_of(total)), dim3(kThreads), 0, s, w, cout, cin, ks,
+                       kin_stride, rows_pad, k_pad, mode, row_scale, reinterpret_cast<float*>(out));
+  else if (out_dtype == DRNMI_BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16_t>, dim3(grid_of(total)), dim3(kThreads), 0, s, w, cout, cin, ks,
+                       kin_stride, rows_pad, k_pad, mode, row_scale, reinterpret_cast<bf16_t*>(out));
+  else
+    return DRNMI_EINVAL;
+  return static_cast<int>(hipGetLastError());
+}
+
+static bool pow2_ge4(int c) { return c >= 4 && (c & (c - 1)) == 0; }
+
+extern "C" int64_t drnmi_reduce_workspace_bytes(int64_t rows, int32_t channels) {
+  if (rows <= 0 || !pow2_ge4(channels)) return -1;
+  // partials (2 x G x C doubles) + 3 x C float coefficients
+  return static_cast<int64_t>(2) * red_splits(rows, channels) * channels * 8 + 3LL * channels * 4 + 256;
+}
+
+extern "C" int drnmi_bn_stats_f32(const float* y, int64_t rows, int32_t C, float eps, float momentum,
+                                  float* mean, float* invstd, float* running_mean, float* running_var,
+                                  int64_t* num_batches_tracked, void* ws, void* stream) {
+  if (y == nullptr || mean == nullptr || invstd == nullptr || ws == nullptr || rows <= 0 || !pow2_ge4(C))
+    return DRNMI_EINVAL;
+  if ((running_mean == nullptr) != (running_var == nullptr)) return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  RedArgs r{};
+  r.a = y;
+  r.rows = rows;
+  r.C = C;
+  r.ws = reinterpret_cast<double*>(ws);
+  hipError_t e = launch_colred<RED_STATS>(r, s);
+  if (e != hipSuccess) return static_cast<int>(e);
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(grid_of(C)), dim3(kThreads), 0, s, r.ws, r.G, C, rows, eps,
+                     momentum, mean, invstd, running_mean, running_var, num_batches_tracked);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_bn_act_f32(const float* y, const float* mean, const float* invstd, const float* gamma,
+                                const float* beta, const float* res, int32_t relu, int64_t rows, int32_t C,
+                                float* z, void* stream) {
+  if (y == nullptr || mean == nullptr || invstd == nullptr || z == nullptr || rows <= 0 || !pow2_ge4(C))
+    return DRNMI_EINVAL;
+  const int64_t n4 = rows * C / 4;
+  hipLaunchKernelGGL(bn_act_kernel, dim3(grid_of(n4)), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                     y, mean, invstd, gamma, beta, res, relu, n4, C, z);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float* y, const float* mean,
+                                    const float* invstd, const float* gamma, int32_t relu, int64_t rows, int32_t C,
+                                    float* dy, float* dres, int32_t dres_accumulate, float* dgamma, float* dbeta,
+                                    int32_t grad_accumulate, void* ws, void* stream) {
+  if (dz == nullptr || y == nullptr || mean == nullptr || invstd == nullptr || dy == nullptr || ws == nullptr ||
+      rows <= 0 || !pow2_ge4(C) || (relu && z == nullptr))
+    return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  RedArgs r{};
+  r.a = dz;
+  r.z = z;
+  r.y = y;
+  r.rows = rows;
+  r.C = C;
+  r.relu = relu;
+  r.ws = reinterpret_cast<double*>(ws);
+  hipError_t e = launch_colred<RED_BNBWD>(r, s);
+  if (e != hipSuccess) return static_cast<int>(e);
+  float* coef = reinterpret_cast<float*>(r.ws + static_cast<int64_t>(2) * r.G * C);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(grid_of(C)), dim3(kThreads), 0, s, r.ws, r.G, C, rows, mean, invstd,
+                     gamma, dgamma, dbeta, grad_accumulate, coef);
+  e = hipGetLastError();
+  if (e != hipSuccess) return static_cast<int>(e);
+  const int64_t n4 = rows * C / 4;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_of(n4)), dim3(kThreads), 0, s, dz, z, y, mean, coef, relu, n4,
+                     C, dy, dres, dres_accumulate);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_channel_sum_f32(const float* x, int64_t rows, int32_t C, int32_t cvalid, float* out,
+                                     int32_t accumulate, void* ws, void* stream) {
+  if (x == nullptr || out == nullptr || ws == nullptr || rows <= 0 || !pow2_ge4(C) || cvalid <= 0 || cvalid > C)
+    return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  RedArgs r{};
+  r.a = x;
+  r.rows = rows;
+  r.C = C;
+  r.ws = reinterpret_cast<double*>(ws);
+  hipError_t e = launch_colred<RED_SUM>(r, s);
+  if (e != hipSuccess) return static_cast<int>(e);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(grid_of(cvalid)), dim3(kThreads), 0, s, r.ws, r.G, C, cvalid, out,
+                     accumulate);
+  return static_cast<int>(hipGetLastError());
+}
+
+static int wgrad_check(const drnmi_wgrad_args* a) {
+  if (a == nullptr) return DRNMI_EINVAL;
+  if (a->n <= 0 || a->h <= 0 || a->w <= 0 || a->ho <= 0 || a->wo <= 0 || a->cout <= 0 || a->cin <= 0) return DRNMI_EINVAL;
+  if (a->cin_stride < 8 || (a->cin_stride & (a->cin_stride - 1)) != 0 || a->cin > a->cin_stride) return DRNMI_EINVAL;
+  if (a->dy_stride < a->cout || a->ks <= 0 || a->stride <= 0 || a->dil <= 0 || a->pad < 0) return DRNMI_EINVAL;
+  if (a->ho != (a->h + 2 * a->pad - a->dil * (a->ks - 1) - 1) / a->stride + 1 ||
+      a->wo != (a->w + 2 * a->pad - a->dil * (a->ks - 1) - 1) / a->stride + 1)
+    return DRNMI_EINVAL;
+  return DRNMI_OK;
+}
+
+extern "C" int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* a) {
+  if (wgrad_check(a) != DRNMI_OK) return -1;
+  int splits;
+  int64_t per;
+  wgrad_plan(*a, &splits, &per);
+  return static_cast<int64_t>(splits) * a->cout * a->ks * a->ks * a->cin_stride * 4;
+}
+
+extern "C" int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* a, void* stream) {
+  const int rc = wgrad_check(a);
+  if (rc != DRNMI_OK) return rc;
+  if (a->dy == nullptr || a->x == nullptr || a->dw == nullptr || a->ws == nullptr) return DRNMI_EINVAL;
+  if (a->ws_bytes < drnmi_conv_wgrad_workspace_bytes(a)) return DRNMI_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(a->dy) | reinterpret_cast<uintptr_t>(a->x)) & 15) return DRNMI_EINVAL;
+  if (a->dy_stride % 4 != 0) return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  WgradP p{};
+  p.dy = a->dy;
+  p.x = a->x;
+  p.ws = reinterpret_cast<float*>(a->ws);
+  p.dys = a->dy_stride;
+  p.cout = a->cout;
+  p.n = a->n; p.h = a->h; p.w = a->w; p.cs = a->cin_stride;
+  p.ho = a->ho; p.wo = a->wo; p.ks = a->ks; p.stride = a->stride; p.pad = a->pad; p.dil = a->dil;
+  p.K = a->ks * a->ks * a->cin_stride;
+  p.M = static_cast<int64_t>(a->n) * a->ho * a->wo;
+  int splits;
+  wgrad_plan(*a, &splits, &p.pix_per_split);
+  const dim3 grid((p.K + kWT - 1) / kWT, (a->cout + kWT - 1) / kWT, splits);
+  hipLaunchKernelGGL(wgrad_kernel, grid, dim3(kThreads), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return static_cast<int>(e);
+  const int64_t total = static_cast<int64_t>(a->cout) * a->cin * a->ks * a->ks;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_of(total)), dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin,
+                     a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_zero_insert_f32(const float* dy, int32_t n, int32_t ho, int32_t wo, int32_t c, int32_t stride,
+                                     int32_t hu, int32_t wu, float* out, void* stream) {
+  if (dy == nullptr || out == nullptr || n <= 0 || ho <= 0 || wo <= 0 || c <= 0 || c % 4 != 0 || stride <= 0 ||
+      hu <= 0 || wu <= 0)
+    return DRNMI_EINVAL;
+  const int64_t total = static_cast<int64_t>(n) * hu * wu * (c / 4);
+  hipLaunchKernelGGL(zero_insert_kernel, dim3(grid_of(total)), dim3(kThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), dy, n, ho, wo, c / 4, stride, hu, wu, out);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_up8_lsm_bwd_f32(const float* g_logprobs, const float* logprobs, const float* g_logits,
+                                     const float* up_w, float grad_scale, int32_t n, int32_t c, int32_t h, int32_t w,
+                                     float* du_ws, float* dlogits, void* stream) {
+  if (up_w == nullptr || dlogits == nullptr || n <= 0 || c <= 0 || h <= 0 || w <= 0) return DRNMI_EINVAL;
+  if (g_logprobs != nullptr && (logprobs == nullptr || du_ws == nullptr)) return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t hw = static_cast<int64_t>(64) * h * w;
+  if (g_logprobs != nullptr) {
+    hipLaunchKernelGGL(lsm_bwd_kernel, dim3(grid_of(n * hw)), dim3(kThreads), 0, s, g_logprobs, logprobs, n, c, hw,
+                       grad_scale, du_ws);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+    hipLaunchKernelGGL(up8_bwd_kernel, dim3(grid_of(static_cast<int64_t>(n) * c * h * w)), dim3(kThreads), 0, s,
+                       du_ws, up_w, g_logits, n * c, h, w, dlogits);
+  } else {
+    // logits-only gradient: dlogits = g_logits (through the same kernel with du = 0 rows skipped)
+    if (g_logits == nullptr) return DRNMI_EINVAL;
+    return static_cast<int>(hipMemcpyAsync(dlogits, g_logits, static_cast<size_t>(n) * c * h * w * 4,
+                                           hipMemcpyDeviceToDevice, s));
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int64_t drnmi_ce_workspace_bytes(void) { return 3LL * kCeBlocks * 8; }
+
+extern "C" int drnmi_ce_loss_f32(const float* logprobs, const int64_t* target, int32_t n, int32_t c, int64_t hw,
+                                 int64_t ignore_index, float* loss, float* count, void* ws, void* stream) {
+  if (logprobs == nullptr || target == nullptr || loss == nullptr || count == nullptr || ws == nullptr || n <= 0 ||
+      c <= 0 || hw <= 0)
+    return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(kCeBlocks), dim3(kThreads), 0, s, logprobs, target, n, c, hw, ignore_index,
+                     reinterpret_cast<double*>(ws));
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return static_cast<int>(e);
+  hipLaunchKernelGGL(ce_final_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const double*>(ws), kCeBlocks, loss,
+                     count);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_ce_loss_bwd_f32(const float* logprobs, const int64_t* target, int32_t n, int32_t c, int64_t hw,
+                                     int64_t ignore_index, const float* dloss, const float* count, float* g_logprobs,
+                                     void* stream) {
+  if (logprobs == nullptr || target == nullptr || dloss == nullptr || count == nullptr || g_logprobs == nullptr ||
+      n <= 0 || c <= 0 || hw <= 0)
+    return DRNMI_EINVAL;
+  hipLaunchKernelGGL(ce_bwd_kernel, dim3(grid_of(static_cast<int64_t>(n) * hw)), dim3(kThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), logprobs, target, n, c, hw, ignore_index, dloss, count,
+                     g_logprobs);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_sgd_step_f32(int32_t ntensors, float* const* params, const float* const* grads,
+                                  float* const* momentum_bufs, const int64_t* numels,
+                                  const uint32_t* const* mask_bits, const int32_t* first_step, float lr,
+                                  float momentum, float dampening, float weight_decay, int32_t nesterov,
+                                  void* stream) {
+  if (ntensors < 0 || (ntensors > 0 && (params == nullptr || grads == nullptr || numels == nullptr)))
+    return DRNMI_EINVAL;
+  if (momentum != 0.f && ntensors > 0 && (momentum_bufs == nullptr || first_step == nullptr)) return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  for (int t0 = 0; t0 < ntensors; t0 += kSgdBatch) {
+    SgdBatch b{};
+    const int cnt = ntensors - t0 < kSgdBatch ? ntensors - t0 : kSgdBatch;
+    int64_t maxn = 0;
+    for (int i = 0; i < cnt; ++i) {
+      const int k = t0 + i;
+      b.w[i] = params[k];
+      b.g[i] = grads[k];
+      b.buf[i] = momentum != 0.f ? momentum_bufs[k] : nullptr;
+      b.mask[i] = mask_bits != nullptr ? mask_bits[k] : nullptr;
+      b.numel[i] = numels[k];
+      b.first[i] = momentum != 0.f ? first_step[k] : 0;
+      if (b.numel[i] < 0) return DRNMI_EINVAL;
+      if (b.numel[i] > 0 && (b.w[i] == nullptr || b.g[i] == nullptr || (momentum != 0.f && b.buf[i] == nullptr)))
+        return DRNMI_EINVAL;
+      maxn = b.numel[i] > maxn ? b.numel[i] : maxn;
+    }
+    if (maxn == 0) continue;
+    unsigned gx = grid_of(maxn);
+    gx = gx > 1024 ? 1024 : gx;
+    hipLaunchKernelGGL(sgd_kernel, dim3(gx, cnt), dim3(kThreads), 0, s, b, lr, momentum, dampening, weight_decay,
+                       nesterov);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  return DRNMI_OK;
+}

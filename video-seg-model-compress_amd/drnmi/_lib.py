@@ -41,8 +41,24 @@ class ConvArgs(ctypes.Structure):
     ]
 
 
+class WgradArgs(ctypes.Structure):
+    """Mirror of drnmi_wgrad_args (include/drnmi.h)."""
+    _fields_ = [
+        ("dy", ctypes.c_void_p),
+        ("x", ctypes.c_void_p),
+        ("dw", ctypes.c_void_p),
+        ("ws", ctypes.c_void_p),
+        ("ws_bytes", ctypes.c_int64),
+        ("n", ctypes.c_int32), ("h", ctypes.c_int32), ("w", ctypes.c_int32), ("cin", ctypes.c_int32),
+        ("cin_stride", ctypes.c_int32), ("ho", ctypes.c_int32), ("wo", ctypes.c_int32),
+        ("cout", ctypes.c_int32), ("dy_stride", ctypes.c_int32),
+        ("ks", ctypes.c_int32), ("stride", ctypes.c_int32), ("pad", ctypes.c_int32), ("dil", ctypes.c_int32),
+        ("accumulate", ctypes.c_int32),
+    ]
+
+
 # Every symbol include/drnmi.h declares, with its ctypes signature.
-_VP, _I32, _I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+_VP, _I32, _I64, _F32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
 SIGNATURES = {
     "drnmi_conv2d_bn_act": (ctypes.c_int, [ctypes.POINTER(ConvArgs), _VP]),
     "drnmi_conv_tile_name": (ctypes.c_char_p, [ctypes.c_int]),
@@ -55,6 +71,21 @@ SIGNATURES = {
     "drnmi_mask_apply_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP]),
     "drnmi_mask_apply_bits_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP]),
     "drnmi_confusion_matrix": (ctypes.c_int, [_VP, _I32, _VP, _I32, _I64, _I32, _VP, _VP]),
+    "drnmi_pack_conv_weight": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _I32, _VP, _VP]),
+    "drnmi_reduce_workspace_bytes": (ctypes.c_int64, [_I64, _I32]),
+    "drnmi_bn_stats_f32": (ctypes.c_int, [_VP, _I64, _I32, _F32, _F32, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "drnmi_bn_act_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _I32, _I64, _I32, _VP, _VP]),
+    "drnmi_bn_act_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _I32, _I64, _I32, _VP, _VP, _I32,
+                                            _VP, _VP, _I32, _VP, _VP]),
+    "drnmi_channel_sum_f32": (ctypes.c_int, [_VP, _I64, _I32, _I32, _VP, _I32, _VP, _VP]),
+    "drnmi_conv_wgrad_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
+    "drnmi_conv_wgrad_f32": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
+    "drnmi_zero_insert_f32": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
+    "drnmi_up8_lsm_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _F32, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
+    "drnmi_ce_workspace_bytes": (ctypes.c_int64, []),
+    "drnmi_ce_loss_f32": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I64, _I64, _VP, _VP, _VP, _VP]),
+    "drnmi_ce_loss_bwd_f32": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I64, _I64, _VP, _VP, _VP, _VP]),
+    "drnmi_sgd_step_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP, _VP, _VP, _F32, _F32, _F32, _F32, _I32, _VP]),
     "drnmi_version": (ctypes.c_char_p, []),
 }
 

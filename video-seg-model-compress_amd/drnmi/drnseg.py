@@ -10,7 +10,8 @@ Reference API (kept): semantic_seg.py:126-164 / lmodels/drnseg.py:268-305
 
 Differences by design:
   * forward runs the fused HIP plan (drnmi.engine) on a ROCm device.  It never falls
-    back to ATen; on CPU, or in train mode, it raises.
+    back to ATen; on CPU it raises.  In train mode it runs the fine-tune path
+    (drnmi.train: batch-stat BN, autograd through the HIP backward kernels, fp32).
   * precision: "fp32" (default; the reference's arithmetic, parity mode, exact-fp32
     MFMA) or "bf16" (perf mode, fp32 accumulation) via set_precision().
   * segment(frames_u8) is the fused seg_video path (seg_video_old_no_plot.py:157-169:
@@ -86,6 +87,14 @@ class DRNSeg(nn.Module):
             yield param
 
     def forward(self, x: torch.Tensor):
+        if self.training:
+            # fine-tune path: batch-stat BN + autograd through the HIP backward kernels
+            if x.device.type != "cuda":
+                raise RuntimeError("drnmi.DRNSeg runs on the HIP engine only (no CPU fallback by design)")
+            if self.precision != "fp32":
+                raise NotImplementedError("the fine-tune path runs in fp32 (the reference's arithmetic)")
+            from .train import train_forward
+            return train_forward(self, x)
         plan, stream = self._prepare(x.shape[0], x.shape[2], x.shape[3], x.device)
         if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] != 3:
             raise ValueError("DRNSeg.forward expects fp32 [B,3,H,W]")
@@ -164,8 +173,8 @@ class DRNSeg(nn.Module):
             raise RuntimeError("drnmi.DRNSeg runs on the HIP engine only: move the model and input "
                                "to a ROCm device (no CPU fallback by design)")
         if self.training:
-            raise NotImplementedError("train-mode forward (batch-stat BN + autograd) is the "
-                                      "fine-tune path, not built yet; call .eval()")
+            raise RuntimeError("predict()/segment() are inference paths: call .eval() first "
+                               "(train-mode forward is DRNSeg.forward)")
         _lib.load()
         key = self._state_key()
         if key != self._pack_key:

@@ -1,0 +1,511 @@
+"""Fine-tune path: train-mode DRNSeg forward/backward, CrossEntropyLoss, SGD — on HIP kernels.
+
+Reference training step (semantic_seg.py:166-230):
+
+    model.train()
+    output = model(input)[0]                      # DRNSeg.forward, BN on batch statistics
+    loss = criterion(output, target)              # CrossEntropyLoss(ignore_index=255), :817
+    optimizer.zero_grad(); loss.backward()        # autograd through ~70 ATen ops
+    optimizer.step()                              # SGD(momentum, weight_decay), :963-966
+    if pruner: pruner.apply_masks(model)          # :213-214
+
+Here the same step keeps that exact user-facing shape: `DRNSeg.forward` in train mode is one
+autograd.Function whose forward runs the fp32 HIP plan (conv -> batch-stat BN -> ReLU/residual
+per node, then up x8 + LogSoftmax) and whose backward runs the HIP backward kernels in reverse
+node order (include/drnmi.h "Fine-tune path"), writing every parameter's .grad directly.  A
+gradient-ready callback per node lets the data-parallel wrapper (drnmi.parallel) launch the
+bucketed RCCL all-reduce of finished buckets while earlier layers are still in backward.
+`CrossEntropyLoss` and `SGD` below are the HIP drop-ins for the criterion and optimizer (the
+optimizer can fuse the pruner's mask into the update: `SGD(..., pruner=p)`).
+
+Precision: fp32 throughout (the reference trains in fp32); activations NHWC with a power-of-two
+channel stride, like the inference engine.  There is no CPU or ATen fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .engine import COUT_ALIGN, K_ALIGN, _conv_out, _pow2_at_least, _round_up
+
+F32 = _lib.DRNMI_F32
+
+
+def _vp(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class _NodeState:
+    """Per-node packed weights (forward / dgrad layouts) cached across steps."""
+
+    __slots__ = ("wf", "wd", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift")
+
+    def __init__(self):
+        self.wf = self.wd = self.shift = None
+
+
+class TrainRunner:
+    """Executes one DRNSeg's train-mode forward and backward on the HIP kernels."""
+
+    def __init__(self, model):
+        self.model = model
+        self.graph = model._graph
+        self.cstride = {"input": 8}
+        for v, c in self.graph.channels.items():
+            if v != "input":
+                self.cstride[v] = _pow2_at_least(c)
+        self.nodes = self.graph.nodes
+        self.state = [_NodeState() for _ in self.nodes]
+        self._red_ws = None
+        self._wg_ws = None
+        self._zeros = None
+        self.grad_ready = None          # callback(list[Parameter]) after each node's grads land
+        self.grad_scale = 1.0           # multiplies dL/dlogprobs (DDP averaging: 1 / world_size)
+        self._flat = None               # flat gradient buffer (views = param.grad)
+        self._flat_params = None
+        self.debug_value_grads = None   # dict -> filled with {value: NHWC grad clone} (diagnostics)
+
+    # ------------------------------------------------------------------ helpers
+    def _ws(self, attr, nbytes, device):
+        buf = getattr(self, attr)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            setattr(self, attr, buf)
+        return buf
+
+    def _zeros_f32(self, n, device):
+        if self._zeros is None or self._zeros.numel() < n:
+            self._zeros = torch.zeros(max(n, 4096), dtype=torch.float32, device=device)
+        return self._zeros
+
+    def ordered_params(self):
+        """Parameters in the order backward finishes them (seg first, then nodes reversed)."""
+        out = []
+        for nd in reversed(self.nodes):
+            ps = [nd.conv.weight] + ([nd.conv.bias] if nd.conv.bias is not None else [])
+            if nd.bn is not None:
+                ps += [nd.bn.weight, nd.bn.bias]
+            out += [p for p in ps if p is not None]
+        return out
+
+    def _ensure_flat_grads(self, device):
+        """param.grad of every trainable parameter is a view of one flat fp32 buffer laid out
+        in backward order (contiguous all-reduce buckets).  Returns {param: accumulate?}."""
+        params = [p for p in self.ordered_params() if p.requires_grad]
+        if self._flat_params is None or [id(p) for p in self._flat_params] != [id(p) for p in params]:
+            total = sum(p.numel() for p in params)
+            self._flat = torch.zeros(total, dtype=torch.float32, device=device)
+            self._flat_params = params
+            self._views = {}
+            off = 0
+            for p in params:
+                self._views[id(p)] = self._flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+        acc = {}
+        for p in params:
+            if p.grad is None:
+                p.grad = self._views[id(p)]
+                acc[id(p)] = False
+            else:
+                if not (p.grad.is_contiguous() and p.grad.dtype == torch.float32 and p.grad.device == p.device):
+                    raise RuntimeError("drnmi train: existing .grad must be contiguous fp32 on the device")
+                acc[id(p)] = True
+        return acc
+
+    def _pack(self, nd, st, device, stream):
+        lib = _lib.load()
+        conv = nd.conv
+        cout, cin, ks, _ = conv.weight.shape
+        cs = self.cstride[nd.src]
+        if st.wf is None:
+            st.k = ks * ks * cs
+            st.k_pad = _round_up(st.k, K_ALIGN)
+            st.cout_pad = _round_up(cout, COUT_ALIGN)
+            st.wf = torch.empty(st.cout_pad, st.k_pad, dtype=torch.float32, device=device)
+            st.shift = torch.zeros(st.cout_pad, dtype=torch.float32, device=device)
+        w = conv.weight.detach()
+        if not (w.is_contiguous() and w.dtype == torch.float32):
+            raise RuntimeError(f"{nd.name}: expected a contiguous fp32 weight")
+        _lib.check(lib.drnmi_pack_conv_weight(_vp(w), cout, cin, ks, cs, st.cout_pad, st.k_pad, 0, None, F32,
+                                              _vp(st.wf), stream), f"pack {nd.name}")
+        if conv.bias is not None:
+            st.shift[:cout].copy_(conv.bias.detach())
+
+    def _pack_dgrad(self, nd, st, device, stream):
+        lib = _lib.load()
+        cout, cin, ks, _ = nd.conv.weight.shape
+        dys = self.cstride[nd.dst] if not nd.out_fp32_nchw else _pow2_at_least(cout)
+        if st.wd is None:
+            st.kd = ks * ks * dys
+            st.kd_pad = _round_up(st.kd, K_ALIGN)
+            st.rows_d = _round_up(cin, COUT_ALIGN)
+            st.wd = torch.empty(st.rows_d, st.kd_pad, dtype=torch.float32, device=device)
+        _lib.check(lib.drnmi_pack_conv_weight(_vp(nd.conv.weight.detach()), cout, cin, ks, dys, st.rows_d,
+                                              st.kd_pad, 1, None, F32, _vp(st.wd), stream), f"pack dgrad {nd.name}")
+        return dys
+
+    def _conv(self, x, cin_stride, h, w, wpk, k, k_pad, cout_pad, cout, ks, stride, pad, dil, y, y_strides,
+              shift, res, n, ho, wo, stream, what):
+        a = _lib.ConvArgs()
+        a.x, a.wgt, a.scale, a.shift = x.data_ptr(), wpk.data_ptr(), None, shift.data_ptr()
+        a.res = res.data_ptr() if res is not None else None
+        a.y = y.data_ptr()
+        a.y_sn, a.y_sp, a.y_sc = y_strides
+        a.n, a.h, a.w, a.cin = n, h, w, cin_stride
+        a.ho, a.wo, a.cout, a.cout_pad = ho, wo, cout, cout_pad
+        a.ks, a.stride, a.pad, a.dil = ks, stride, pad, dil
+        a.k, a.k_pad = k, k_pad
+        a.relu = 0
+        a.dtype = a.out_dtype = F32
+        a.tile, a.algo = -1, _lib.ALGO_IGEMM
+        _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), what)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, save: bool):
+        """Train-mode forward; returns (logprobs, logits, saved) — saved is None if not save."""
+        lib = _lib.load()
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        n, _, h, w = x.shape
+        vals = {}
+        shapes = {"input": (h, w)}
+        xin = torch.empty(n, h, w, 8, dtype=torch.float32, device=dev)
+        _lib.check(lib.drnmi_nchw_to_nhwc(x.data_ptr(), xin.data_ptr(), n, 3, h, w, 8, F32, ctypes.c_void_p(stream)),
+                   "nchw_to_nhwc")
+        vals["input"] = xin
+        per_node = []
+        logits = None
+        for nd, st in zip(self.nodes, self.state):
+            c = nd.conv
+            ih, iw = shapes[nd.src]
+            ks, s, p, d = c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0]
+            oh, ow = _conv_out(ih, ks, s, p, d), _conv_out(iw, ks, s, p, d)
+            shapes[nd.dst] = (oh, ow)
+            self._pack(nd, st, dev, ctypes.c_void_p(stream))
+            cout = c.out_channels
+            cs_in = self.cstride[nd.src]
+            if nd.out_fp32_nchw:        # seg 1x1 + bias -> fp32 NCHW logits
+                logits = torch.empty(n, cout, oh, ow, dtype=torch.float32, device=dev)
+                self._conv(vals[nd.src], cs_in, ih, iw, st.wf, st.k, st.k_pad, st.cout_pad, cout, ks, s, p, d,
+                           logits, (cout * oh * ow, 1, oh * ow), st.shift, None, n, oh, ow, stream, nd.name)
+                vals[nd.dst] = logits
+                per_node.append(None)
+                continue
+            cs = self.cstride[nd.dst]
+            if cs != cout:
+                raise NotImplementedError("train path: channel count must be a power of two")
+            rows = n * oh * ow
+            y = torch.empty(rows, cs, dtype=torch.float32, device=dev)
+            self._conv(vals[nd.src], cs_in, ih, iw, st.wf, st.k, st.k_pad, st.cout_pad, cout, ks, s, p, d,
+                       y, (oh * ow * cs, cs, 1), st.shift, None, n, oh, ow, stream, nd.name)
+            bn = nd.bn
+            if bn.momentum is None or not bn.track_running_stats:
+                raise NotImplementedError("BatchNorm2d with momentum=None / no running stats")
+            mean = torch.empty(cs, dtype=torch.float32, device=dev)
+            invstd = torch.empty(cs, dtype=torch.float32, device=dev)
+            ws = self._ws("_red_ws", lib.drnmi_reduce_workspace_bytes(rows, cs), dev)
+            _lib.check(lib.drnmi_bn_stats_f32(_vp(y), rows, cs, float(bn.eps), float(bn.momentum), _vp(mean),
+                                              _vp(invstd), _vp(bn.running_mean), _vp(bn.running_var),
+                                              _vp(bn.num_batches_tracked), _vp(ws), ctypes.c_void_p(stream)),
+                       f"bn_stats {nd.name}")
+            for b in (bn.running_mean, bn.running_var, bn.num_batches_tracked):
+                torch.autograd.graph.increment_version(b)
+            z = torch.empty(rows, cs, dtype=torch.float32, device=dev)
+            res = vals[nd.res] if nd.res else None
+            _lib.check(lib.drnmi_bn_act_f32(_vp(y), _vp(mean), _vp(invstd), _vp(bn.weight.detach()),
+                                            _vp(bn.bias.detach()), _vp(res), 1 if nd.relu else 0, rows, cs, _vp(z),
+                                            ctypes.c_void_p(stream)), f"bn_act {nd.name}")
+            vals[nd.dst] = z
+            per_node.append((y, mean, invstd) if save else None)
+        lh, lw = shapes["logits"]
+        logprobs = torch.empty(n, logits.shape[1], 8 * lh, 8 * lw, dtype=torch.float32, device=dev)
+        up = self.model._up_plane(dev)
+        _lib.check(lib.drnmi_up8_logsoftmax_argmax(logits.data_ptr(), up.data_ptr(), logprobs.data_ptr(), None,
+                                                   _lib.DRNMI_U8, n, logits.shape[1], lh, lw,
+                                                   ctypes.c_void_p(stream)), "up8_logsoftmax")
+        saved = None
+        if save:
+            saved = {"vals": vals, "shapes": shapes, "nodes": per_node, "n": n, "up": up}
+        return logprobs, logits, saved
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, saved, logprobs, logits, g_lp, g_logits):
+        lib = _lib.load()
+        dev = logprobs.device
+        stream = _lib.stream_ptr(dev)
+        sp = ctypes.c_void_p(stream)
+        vals, shapes, n = saved["vals"], saved["shapes"], saved["n"]
+        acc = self._ensure_flat_grads(dev)
+        ncls, lh, lw = logits.shape[1], logits.shape[2], logits.shape[3]
+        # head: LogSoftmax backward + transpose of the bilinear up-conv
+        dlog = torch.empty_like(logits)
+        du = torch.empty_like(logprobs) if g_lp is not None else None
+        glp = g_lp.contiguous() if g_lp is not None else None
+        glg = g_logits.contiguous() if g_logits is not None else None
+        _lib.check(lib.drnmi_up8_lsm_bwd_f32(_vp(glp), _vp(logprobs) if glp is not None else None, _vp(glg),
+                                             _vp(saved["up"]), float(self.grad_scale), n, ncls, lh, lw, _vp(du),
+                                             _vp(dlog), sp), "up8_lsm_bwd")
+        del du
+        grads = {}          # value -> NHWC fp32 gradient buffer
+        for idx in range(len(self.nodes) - 1, -1, -1):
+            nd, st = self.nodes[idx], self.state[idx]
+            c = nd.conv
+            cout, cin, ks, _ = c.weight.shape
+            s, p, d = c.stride[0], c.padding[0], c.dilation[0]
+            ih, iw = shapes[nd.src]
+            oh, ow = shapes[nd.dst]
+            rows = n * oh * ow
+            done = []
+            if nd.out_fp32_nchw:
+                dys = _pow2_at_least(cout)
+                dy = torch.empty(rows, dys, dtype=torch.float32, device=dev)
+                _lib.check(lib.drnmi_nchw_to_nhwc(dlog.data_ptr(), dy.data_ptr(), n, cout, oh, ow, dys, F32, sp),
+                           "seg grad nhwc")
+                if c.bias is not None and c.bias.requires_grad:
+                    ws = self._ws("_red_ws", lib.drnmi_reduce_workspace_bytes(rows, dys), dev)
+                    _lib.check(lib.drnmi_channel_sum_f32(_vp(dy), rows, dys, cout, _vp(c.bias.grad),
+                                                         1 if acc[id(c.bias)] else 0, _vp(ws), sp), "seg bias grad")
+                    done.append(c.bias)
+            else:
+                dys = self.cstride[nd.dst]
+                dz = grads.pop(nd.dst, None)
+                if dz is None:
+                    raise RuntimeError(f"no gradient reached {nd.name}")
+                if self.debug_value_grads is not None:
+                    self.debug_value_grads[nd.dst] = dz.detach().clone()
+                y, mean, invstd = saved["nodes"][idx]
+                z = vals[nd.dst]
+                bn = nd.bn
+                dres = None
+                dres_acc = 0
+                if nd.res:
+                    dres = grads.get(nd.res)
+                    if dres is None:
+                        dres = torch.empty_like(vals[nd.res])
+                        grads[nd.res] = dres
+                    else:
+                        dres_acc = 1
+                gw, gb = bn.weight, bn.bias
+                ws = self._ws("_red_ws", lib.drnmi_reduce_workspace_bytes(rows, dys), dev)
+                _lib.check(lib.drnmi_bn_act_bwd_f32(
+                    _vp(dz), _vp(z), _vp(y), _vp(mean), _vp(invstd), _vp(gw.detach()), 1 if nd.relu else 0, rows,
+                    dys, _vp(dz), _vp(dres), dres_acc,
+                    _vp(gw.grad) if gw.requires_grad else None, _vp(gb.grad) if gb.requires_grad else None,
+                    1 if (gw.requires_grad and acc[id(gw)]) else 0, _vp(ws), sp), f"bn_bwd {nd.name}")
+                if gw.requires_grad and gb.requires_grad and acc[id(gw)] != acc[id(gb)]:
+                    raise RuntimeError("BN weight/bias grads must be both set or both None")
+                done += [q for q in (gw, gb) if q.requires_grad]
+                dy = dz
+            # weight gradient
+            if c.weight.requires_grad:
+                wa = _lib.WgradArgs()
+                wa.dy, wa.x, wa.dw = dy.data_ptr(), vals[nd.src].data_ptr(), c.weight.grad.data_ptr()
+                wa.n, wa.h, wa.w, wa.cin, wa.cin_stride = n, ih, iw, cin, self.cstride[nd.src]
+                wa.ho, wa.wo, wa.cout, wa.dy_stride = oh, ow, cout, dys
+                wa.ks, wa.stride, wa.pad, wa.dil = ks, s, p, d
+                wa.accumulate = 1 if acc[id(c.weight)] else 0
+                nb = lib.drnmi_conv_wgrad_workspace_bytes(ctypes.byref(wa))
+                if nb < 0:
+                    raise RuntimeError(f"wgrad {nd.name}: bad geometry")
+                ws = self._ws("_wg_ws", nb, dev)
+                wa.ws, wa.ws_bytes = ws.data_ptr(), ws.numel()
+                _lib.check(lib.drnmi_conv_wgrad_f32(ctypes.byref(wa), sp), f"wgrad {nd.name}")
+                done.append(c.weight)
+            if self.grad_ready is not None and done:
+                self.grad_ready(done)
+            # data gradient (not needed for the network input)
+            if nd.src != "input":
+                dys_d = self._pack_dgrad(nd, st, dev, sp)
+                assert dys_d == dys
+                cs_src = self.cstride[nd.src]
+                src = dy
+                hu, wu = oh, ow
+                pad_d = d * (ks - 1) - p
+                if s > 1:
+                    hu, wu = ih + 2 * p - d * (ks - 1), iw + 2 * p - d * (ks - 1)
+                    src = torch.empty(n * hu * wu, dys, dtype=torch.float32, device=dev)
+                    _lib.check(lib.drnmi_zero_insert_f32(_vp(dy), n, oh, ow, dys, s, hu, wu, _vp(src), sp),
+                               f"zero_insert {nd.name}")
+                prev = grads.get(nd.src)
+                out = prev if prev is not None else torch.empty(n * ih * iw, cs_src, dtype=torch.float32, device=dev)
+                self._conv(src, dys, hu, wu, st.wd, st.kd, st.kd_pad, st.rows_d, cin, ks, 1, pad_d, d, out,
+                           (ih * iw * cs_src, cs_src, 1), self._zeros_f32(st.rows_d, dev), prev, n, ih, iw,
+                           stream, f"dgrad {nd.name}")
+                grads[nd.src] = out
+            del dy
+
+
+class _TrainFn(torch.autograd.Function):
+    """DRNSeg train-mode forward as one autograd node; backward = the HIP backward kernels."""
+
+    @staticmethod
+    def forward(ctx, runner, x, *params):
+        ctx.set_materialize_grads(False)
+        lp, logits, saved = runner.forward(x, save=True)
+        ctx.runner = runner
+        ctx.saved = saved
+        ctx.outs = (lp, logits)
+        return lp, logits
+
+    @staticmethod
+    def backward(ctx, g_lp, g_logits):
+        lp, logits = ctx.outs
+        if g_lp is not None or g_logits is not None:
+            ctx.runner.backward(ctx.saved, lp, logits, g_lp, g_logits)
+        ctx.saved = None
+        # parameter grads were written straight into .grad (flat buffer views)
+        return (None,) * len(ctx.needs_input_grad)
+
+
+def train_forward(model, x: torch.Tensor):
+    """DRNSeg.forward in train mode (batch-stat BN, autograd through the HIP backward)."""
+    runner = getattr(model, "_train_runner", None)
+    if runner is None:
+        runner = TrainRunner(model)
+        model._train_runner = runner
+    if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] != 3:
+        raise ValueError("DRNSeg.forward expects fp32 [B,3,H,W]")
+    x = x.contiguous()
+    params = [p for p in runner.ordered_params() if p.requires_grad]
+    if torch.is_grad_enabled() and params:
+        return _TrainFn.apply(runner, x, *params)
+    lp, logits, _ = runner.forward(x, save=False)
+    return lp, logits
+
+
+# ====================================================================== criterion
+class _CEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lp, target, ignore_index):
+        lib = _lib.load()
+        n, c = lp.shape[0], lp.shape[1]
+        hw = lp[0, 0].numel()
+        dev = lp.device
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        count = torch.empty((), dtype=torch.float32, device=dev)
+        ws = torch.empty(lib.drnmi_ce_workspace_bytes(), dtype=torch.uint8, device=dev)
+        sp = ctypes.c_void_p(_lib.stream_ptr(dev))
+        _lib.check(lib.drnmi_ce_loss_f32(_vp(lp), _vp(target), n, c, hw, int(ignore_index), _vp(loss), _vp(count),
+                                         _vp(ws), sp), "ce_loss")
+        ctx.save_for_backward(lp, target, count)
+        ctx.ignore_index = ignore_index
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        lp, target, count = ctx.saved_tensors
+        lib = _lib.load()
+        n, c = lp.shape[0], lp.shape[1]
+        hw = lp[0, 0].numel()
+        glp = torch.empty_like(lp)
+        g = g.contiguous().to(torch.float32)
+        _lib.check(lib.drnmi_ce_loss_bwd_f32(_vp(lp), _vp(target), n, c, hw, int(ctx.ignore_index), _vp(g),
+                                             _vp(count), _vp(glp), ctypes.c_void_p(_lib.stream_ptr(lp.device))),
+                   "ce_loss_bwd")
+        return glp, None, None
+
+
+class CrossEntropyLoss(torch.nn.Module):
+    """nn.CrossEntropyLoss(ignore_index=255) drop-in (semantic_seg.py:817) on the HIP kernels.
+
+    Like the reference it is applied to DRNSeg's log-probs (model(x)[0]), i.e. it computes
+    mean over target != ignore_index of logsumexp(lp) - lp[target] (a second log-softmax,
+    semantic_seg.py:197-198).  Only mean reduction and no class weights (the reference's use)."""
+
+    def __init__(self, weight=None, ignore_index: int = -100, reduction: str = "mean"):
+        super().__init__()
+        if weight is not None or reduction != "mean":
+            raise NotImplementedError("class weights / reduction != 'mean' are not used by the reference")
+        self.ignore_index = ignore_index
+
+    def forward(self, logprobs: torch.Tensor, target: torch.Tensor):
+        if not logprobs.is_cuda:
+            raise RuntimeError("drnmi CrossEntropyLoss runs on the HIP kernels (no CPU fallback)")
+        if logprobs.dtype != torch.float32:
+            raise ValueError("expected fp32 log-probs")
+        if target.dtype != torch.int64:
+            raise ValueError("expected int64 targets (semantic_seg.py:195 target.long())")
+        if target.shape != (logprobs.shape[0],) + tuple(logprobs.shape[2:]):
+            raise ValueError(f"target shape {tuple(target.shape)} does not match {tuple(logprobs.shape)}")
+        return _CEFn.apply(logprobs.contiguous(), target.contiguous(), self.ignore_index)
+
+
+# ====================================================================== optimizer
+class SGD(torch.optim.Optimizer):
+    """torch.optim.SGD drop-in (semantic_seg.py:963-966) whose step is one multi-tensor HIP
+    launch per 48 parameters.  With `pruner=` the pruner's masks are applied inside the same
+    pass (replacing the separate Pruner.apply_masks after optimizer.step(), :213-214);
+    state['momentum_buffer'] matches torch's, so state_dict()/load_state_dict() interoperate."""
+
+    def __init__(self, params, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False, pruner=None,
+                 model=None):
+        if lr < 0 or momentum < 0 or weight_decay < 0:
+            raise ValueError("invalid SGD hyper-parameters")
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        super().__init__(params, dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                                      nesterov=nesterov))
+        self.pruner = pruner
+        self._mask_of = {}
+        if pruner is not None:
+            if model is None:
+                raise ValueError("SGD(pruner=...) needs model= to resolve mask keys to parameters")
+            self.attach_pruner(pruner, model)
+
+    def attach_pruner(self, pruner, model):
+        self.pruner = pruner
+        named = dict(model.named_parameters())
+        self._mask_of = {}
+        for key in pruner.mask_dict:
+            for cand in (key, "module." + key, key[len("module."):] if key.startswith("module.") else None):
+                if cand is not None and cand in named:
+                    self._mask_of[id(named[cand])] = key
+                    break
+            else:
+                raise KeyError(key)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = _lib.load()
+        for group in self.param_groups:
+            ps, gs, bs, ns, ms, fs = [], [], [], [], [], []
+            mom = group["momentum"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous() or not p.grad.is_contiguous():
+                    raise RuntimeError("drnmi SGD: parameters/grads must be contiguous fp32 on the ROCm device")
+                st = self.state[p]
+                first = 0
+                if mom != 0:
+                    buf = st.get("momentum_buffer")
+                    if buf is None:
+                        buf = torch.empty_like(p)
+                        st["momentum_buffer"] = buf
+                        first = 1
+                    bs.append(buf)
+                ps.append(p)
+                gs.append(p.grad)
+                ns.append(p.numel())
+                fs.append(first)
+                key = self._mask_of.get(id(p))
+                ms.append(self.pruner._mask_bits(key, p.device) if key is not None else None)
+            if not ps:
+                continue
+            k = len(ps)
+            arr = lambda ts: (ctypes.c_void_p * k)(*[t.data_ptr() if t is not None else None for t in ts])
+            mask_arr = arr(ms) if any(m is not None for m in ms) else None
+            _lib.check(lib.drnmi_sgd_step_f32(
+                k, arr(ps), arr(gs), arr(bs) if mom != 0 else None, (ctypes.c_int64 * k)(*ns), mask_arr,
+                (ctypes.c_int32 * k)(*fs), float(group["lr"]), float(mom), float(group["dampening"]),
+                float(group["weight_decay"]), 1 if group["nesterov"] else 0,
+                ctypes.c_void_p(_lib.stream_ptr(ps[0].device))), "sgd_step")
+            for p in ps:
+                torch.autograd.graph.increment_version(p)
+        return loss
