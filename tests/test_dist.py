@@ -59,3 +59,46 @@ def test_gloo_world2_shards_cover_once_and_reduce():
         assert cover == [1] * 37          # every frame processed by exactly one rank
         assert slowest == 1.5             # max over ranks
         assert h00 == 3                   # 1 + 2 summed
+
+
+def _reducer_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from drnmi.parallel import BucketReducer
+        sizes = [300, 50, 700, 10, 10, 400, 1000, 3]          # "parameters" in backward order
+        params = [torch.empty(n) for n in sizes]
+        flat = torch.arange(sum(sizes), dtype=torch.float32) * (rank + 1)
+        r = BucketReducer(flat, params, bucket_cap_bytes=1024 * 4)    # 1024-element buckets
+        bounds = [(s, e) for s, e, _ in r.buckets]
+        r.mark_ready(params[:2])
+        early = list(r.launch_order)                          # nothing complete yet
+        r.mark_ready(params[2:3])                             # closes bucket 0 (>= 1024 elements)
+        after_first = list(r.launch_order)
+        r.mark_ready(params[3:])
+        r.finalize()
+        q.put((rank, bounds, early, after_first, flat.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bucket_reducer():
+    """Buckets are contiguous slices in backward order, launched as soon as complete, and the
+    result is the SUM over ranks (the runner pre-scales by 1/world, so this is DDP's mean)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reducer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total = 2473
+    expect = [3.0 * i for i in range(total)]
+    for rank, bounds, early, after_first, flat in out:
+        assert bounds[0] == (0, 1050) and bounds[-1][1] == total
+        assert all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
+        assert early == [] and after_first == [0]
+        assert flat == expect
