@@ -41,7 +41,46 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
+    ap.add_argument("--prune", default="", help="block:BHxBW:SPARSITY — BlockPruner masks (collapse_tensor "
+                    "False, BlockPruner.py:139-241) on every conv with >=16 input channels (config C3)")
+    ap.add_argument("--block-sparse", action="store_true", help="unit-skipping MFMA kernels on pruned weights "
+                    "(opt-in; the dense kernel is faster below ~60%% zero 16x32 units)")
     return ap.parse_args()
+
+
+def pruned_model(args, dev):
+    """BASELINE config C3: hash-initialised weights + BlockPruner masks, applied once
+    (semantic_seg.py:1063), then the eval engine (which skips the all-zero weight units)."""
+    import json
+    import tempfile
+
+    import torch
+    from drnmi.drnseg import DRNSeg
+    from drnmi.pruners import BlockPruner
+    from drnmi.weights import synth_state_dict
+    kind, shape, sp = args.prune.split(":")
+    if kind != "block":
+        raise SystemExit("--prune: only block:BHxBW:SPARSITY")
+    bh, bw = (int(v) for v in shape.lower().split("x"))
+    m = DRNSeg(args.arch, 19, pretrained=False)
+    m.load_state_dict(synth_state_dict(m, 0))
+    layers = [k for k, v in m.state_dict().items() if k.startswith("layer.") and k.endswith(".weight")
+              and v.dim() == 4 and v.shape[1] >= 16 and v.shape[0] % bh == 0 and v.shape[1] % bw == 0]
+    cfg = {"pruner_type": "block", "configs": [{"layer_set": layers, "sparsity": float(sp), "block_height": bh,
+                                                "block_width": bw, "sub_rows": -1, "sub_cols": -1,
+                                                "collapse_tensor": False}]}
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(cfg, f)
+    pr = BlockPruner(f.name, on_gpu=False)
+    pr.generate_masks(m, is_static=False)
+    os.unlink(f.name)
+    with torch.no_grad():
+        sd = m.state_dict()
+        for k, mk in pr.mask_dict.items():
+            sd[k].mul_(mk)
+    m = m.to(dev).eval().set_precision(args.precision)
+    m.set_block_sparse(args.block_sparse)
+    return m, len(layers)
 
 
 def cpu_baseline(args, seconds):
@@ -104,7 +143,10 @@ def main():
     from drnmi.drnseg import INFO_MEAN, INFO_STD, build
     from drnmi.roofline import MFMA_PEAK, network_roofline, node_work
 
-    model = build(args.arch, 19, seed=0, device=dev, precision=args.precision)
+    if args.prune:
+        model, n_pruned = pruned_model(args, dev)
+    else:
+        model = build(args.arch, 19, seed=0, device=dev, precision=args.precision)
     B, H, W = args.batch, args.height, args.width
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     frames = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
@@ -122,6 +164,10 @@ def main():
         return lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
 
     names = [launched_name(i) for i in range(len(plan.args))]
+    # useful work of block-sparse launches: dense FLOPs x (1 - fraction of skipped zero units)
+    nodes = plan.packed.graph.nodes
+    works = [(w[0], w[1] * (1.0 - nodes[i].zero_unit_frac if nodes[i].unit_mask is not None else 1.0), w[2])
+             if i < len(nodes) else w for i, w in enumerate(works)]
     events = []
     pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * len(names) * args.steps)]
 
@@ -178,12 +224,20 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.precision,
-        "data": "synthetic uint8 RGB frames resident in HBM; hash-initialised DRN-D-22 weights (no checkpoint)",
+        "data": f"synthetic uint8 RGB frames resident in HBM; hash-initialised {args.arch} weights (no checkpoint)"
+                + (f"; BlockPruner {args.prune} masks" if args.prune else ""),
         "config": {"workload": f"{args.arch} dense inference, seg_video loop (uint8 frame -> uint8 labels) "
                                f"{H}x{W}, {B} frames/GPU/step",
                    "arch": args.arch, "height": H, "width": W, "frames_per_gpu_step": B,
                    "global_batch": B * world, "parallelism": f"dp{world} (frames sharded, no data-path collective)"},
     }
+    if args.prune:
+        sparse = [nd for nd in plan.packed.graph.nodes if nd.unit_mask is not None]
+        out["config"]["workload"] = out["config"]["workload"].replace("dense inference", f"{args.prune} pruned inference")
+        out["config"]["block_sparse"] = {"pruned_layers": n_pruned, "sparse_launches": len(sparse),
+                                         "mean_zero_unit_frac": round(sum(nd.zero_unit_frac for nd in sparse)
+                                                                      / max(len(sparse), 1), 4),
+                                         "kernels": "unit-skipping" if args.block_sparse else "dense"}
     traffic, traffic_src = pmc_traffic(args, dominant) if durs else (None, None)
     if durs:
         avg_d = sum(durs) / len(durs)

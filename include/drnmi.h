@@ -64,6 +64,11 @@ typedef struct drnmi_conv_args {
   int32_t src_u8;           /* PATCH only: x is uint8 HWC3 frames, normalised on load */
   int32_t bgr;              /* src_u8: swap channel 0 and 2 on read                  */
   float mean[3], std[3];    /* src_u8: (u8 / 255 - mean[c]) / std[c], fp32          */
+  const uint32_t* unit_mask; /* optional block-sparsity map of wgt (drnmi_weight_unit_mask):  */
+                             /* bit (rb, ku) = 0 -> rows 16rb..16rb+15 x packed K columns   */
+                             /* 32ku..32ku+31 are all zero and their MFMAs are skipped      */
+                             /* (bf16 LDS-DMA kernels; NULL = dense).  Results are bit-     */
+                             /* identical to the dense kernel on the same weights.          */
 } drnmi_conv_args;
 
 /* Algorithms behind drnmi_conv2d_bn_act:
@@ -84,6 +89,17 @@ typedef struct drnmi_conv_args {
 enum drnmi_algo { DRNMI_ALGO_IGEMM = 0, DRNMI_ALGO_PATCH = 1 };
 
 int drnmi_conv2d_bn_act(const drnmi_conv_args* args, void* stream);
+
+/* Block-sparsity map of packed weights [rows_pad][k_pad] (dtype F32 or BF16): one bit per
+ * 16-row x 32-column unit, bit = 1 iff any element of the unit is nonzero (+-0 count as zero);
+ * layout: row-block rb owns words [rb*W, rb*W + W), W = ceil(k_pad / 32 / 32), unit ku at bit
+ * ku % 32 of word ku / 32.  mask must hold (rows_pad / 16) * W words; *nonzero_units (device
+ * int32, NULL-able) receives the count of nonzero units.  This is how pruner masks reach the
+ * MFMA path: MFMA runs only on the dense-within-block sub-tiles (BlockPruner blocks of whole
+ * kernels, BlockPruner.py:139-241, with block_width a multiple of 32 input channels map 1:1 to
+ * units; narrower blocks skip where neighbouring blocks are both pruned). */
+int drnmi_weight_unit_mask(const void* wgt, int32_t dtype, int32_t rows_pad, int32_t k_pad, uint32_t* mask,
+                           int32_t* nonzero_units, void* stream);
 
 /* Name of the kernel (template instance) drnmi_conv2d_bn_act would launch for these
  * arguments, e.g. "conv_big_kernel<3, 128, 2, 2>"; NULL if none.  No launch, no GPU needed.

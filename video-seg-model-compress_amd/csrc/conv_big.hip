@@ -72,14 +72,15 @@ __device__ __forceinline__ int xcd_remap2(int bid, int nwg) {
 // Accumulator start value.  With a NULL scale (BN scale pre-folded into the weights) the
 // tile starts from shift + residual: the residual loads go out with the prologue DMA and
 // hide under it, and the epilogue is a plain ReLU + convert + store.
-template <int FM, int WCO>
-__device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)[FM][4], int px0, int co0,
+template <int FM, int WCO, int FN = 4>
+__device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)[FM][FN], int px0, int co0,
                                           int wc, int wp, int fr, int fq) {
+  constexpr int PXW = 16 * FN;   // pixels per wave
   if (p.scale != nullptr) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     return;
   }
   const int M = p.n * p.ho * p.wo;
@@ -89,47 +90,52 @@ __device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)
     const int co = co0 + wc * WCO + fm * 16 + fq * 4;
     const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);   // padded to cout_pad
 #pragma unroll
-    for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = f32x4{sh.x, sh.y, sh.z, sh.w};
+    for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = f32x4{sh.x, sh.y, sh.z, sh.w};
   }
   if (res == nullptr) return;
-  uint2 rv[FM][4];
+  // residual loads in groups of 4 pixel fragments (bounds the live registers to FM x 4 uint2)
 #pragma unroll
-  for (int fn = 0; fn < 4; ++fn) {
-    const int m = px0 + wp * 64 + fn * 16 + fr;
+  for (int g = 0; g < FN; g += 4) {
+    uint2 rv[FM][4];
 #pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
-      const int co = co0 + wc * WCO + fm * 16 + fq * 4;
-      rv[fm][fn] = make_uint2(0, 0);
-      if (m < M && co + 3 < p.cout) rv[fm][fn] = *reinterpret_cast<const uint2*>(res + static_cast<int64_t>(m) * p.cout + co);
-      else if (m < M) {
-        uint16_t t[4] = {0, 0, 0, 0};
-        for (int j = 0; j < 4; ++j)
-          if (co + j < p.cout) t[j] = res[static_cast<int64_t>(m) * p.cout + co + j];
-        rv[fm][fn] = make_uint2(t[0] | (static_cast<uint32_t>(t[1]) << 16), t[2] | (static_cast<uint32_t>(t[3]) << 16));
+    for (int f4 = 0; f4 < 4; ++f4) {
+      const int m = px0 + wp * PXW + (g + f4) * 16 + fr;
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) {
+        const int co = co0 + wc * WCO + fm * 16 + fq * 4;
+        rv[fm][f4] = make_uint2(0, 0);
+        if (m < M && co + 3 < p.cout) rv[fm][f4] = *reinterpret_cast<const uint2*>(res + static_cast<int64_t>(m) * p.cout + co);
+        else if (m < M) {
+          uint16_t t[4] = {0, 0, 0, 0};
+          for (int j = 0; j < 4; ++j)
+            if (co + j < p.cout) t[j] = res[static_cast<int64_t>(m) * p.cout + co + j];
+          rv[fm][f4] = make_uint2(t[0] | (static_cast<uint32_t>(t[1]) << 16), t[2] | (static_cast<uint32_t>(t[3]) << 16));
+        }
       }
     }
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int f4 = 0; f4 < 4; ++f4) {
+        acc[fm][g + f4][0] += bf16_to_f32(static_cast<uint16_t>(rv[fm][f4].x & 0xffff));
+        acc[fm][g + f4][1] += bf16_to_f32(static_cast<uint16_t>(rv[fm][f4].x >> 16));
+        acc[fm][g + f4][2] += bf16_to_f32(static_cast<uint16_t>(rv[fm][f4].y & 0xffff));
+        acc[fm][g + f4][3] += bf16_to_f32(static_cast<uint16_t>(rv[fm][f4].y >> 16));
+      }
   }
-#pragma unroll
-  for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-    for (int fn = 0; fn < 4; ++fn) {
-      acc[fm][fn][0] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x & 0xffff));
-      acc[fm][fn][1] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x >> 16));
-      acc[fm][fn][2] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y & 0xffff));
-      acc[fm][fn][3] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y >> 16));
-    }
 }
 
-template <int FM, int WCO>
-__device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4 (&acc)[FM][4], int cur_px0,
+template <int FM, int WCO, int FN = 4>
+__device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4 (&acc)[FM][FN], int cur_px0,
                                            int cur_co0, int wc, int wp, int fr, int fq) {
+  constexpr int PXW = 16 * FN;
   const int M = p.n * p.ho * p.wo;
   const int hw_o = p.ho * p.wo;
   const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
   const bool nhwc16 = p.out_dtype == DRNMI_BF16 && p.y_sc == 1;
 #pragma unroll
-  for (int fn = 0; fn < 4; ++fn) {
-    const int m = cur_px0 + wp * 64 + fn * 16 + fr;
+  for (int fn = 0; fn < FN; ++fn) {
+    const int m = cur_px0 + wp * PXW + fn * 16 + fr;
     if (m >= M) continue;
     const int n = m / hw_o;
     const int q = m - n * hw_o;
@@ -183,11 +189,13 @@ __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4
   }
 }
 
-template <int WCO, int WC, int NST, int BK>
+template <int WCO, int WC, int NST, int BK, int NWP = 4>
 struct BigCfg {
   static constexpr int BCO = WCO * WC;              // output channels per tile
   static constexpr int FM = WCO / 16;               // channel fragments per wave
-  static constexpr int NW = 4 * WC;                 // waves (WC channel columns x 4 pixel rows)
+  static constexpr int NW = NWP * WC;               // waves (WC channel columns x NWP pixel rows)
+  static constexpr int PXW = kBPX / NWP;            // pixels per wave
+  static constexpr int FN = PXW / 16;               // pixel fragments per wave
   static constexpr int THREADS = 64 * NW;
   static constexpr int ROWB = BK * 2;               // bytes per LDS row
   static constexpr int CPR = ROWB / 16;             // 16-B chunks per row
@@ -206,17 +214,17 @@ struct BigCfg {
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST>
-__global__ void __launch_bounds__(64 * 4 * WC, 1)
+template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE>
+__global__ void __launch_bounds__(64 * NWP * WC, 1)
 conv_big_kernel(const drnmi_conv_args p) {
-  using C = BigCfg<WCO, WC, NST, BK>;
+  using C = BigCfg<WCO, WC, NST, BK, NWP>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wc = wave / 4;          // channel column of the tile
-  const int wp = wave % 4;          // 64-pixel quarter of the tile
+  const int wc = wave / NWP;        // channel column of the tile
+  const int wp = wave % NWP;        // PXW-pixel slice of the tile
   const int M = p.n * p.ho * p.wo;
   const int hw_o = p.ho * p.wo;
   const int nco = (p.cout + C::BCO - 1) / C::BCO;
@@ -301,16 +309,31 @@ conv_big_kernel(const drnmi_conv_args p) {
     for (int i = 0; i < C::GLDS; ++i) issue_piece(sp, stage, i);
   };
 
-  f32x4 acc[C::FM][4];
+
+  f32x4 acc[C::FM][C::FN];
   int tl = blockIdx.x;
   int tile = xcd_remap2(tl, ntiles);
   int px0 = (tile / nco) * kBPX;
   int co0 = (tile % nco) * C::BCO;
   setup(px0, co0);
-  init_tile<C::FM, WCO>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
+  auto live_bits = [&](int kt) -> uint32_t {
+    const int ku0 = step_params(kt).k0 >> 5;
+    const int wpr = (p.k_pad + 1023) >> 10;                 // mask words per row-block
+    uint32_t bits = 0;
+#pragma unroll
+    for (int fm = 0; fm < C::FM; ++fm) {
+      const int rb = (co0 + wc * WCO + fm * 16) >> 4;
+      const uint32_t word = __builtin_amdgcn_readfirstlane(p.unit_mask[rb * wpr + (ku0 >> 5)]);
+      bits |= ((word >> (ku0 & 31)) & ((1u << C::SUB) - 1)) << (fm * C::SUB);
+    }
+    return bits;
+  };
+  uint32_t live_next = 0xffffffffu;
+  init_tile<C::FM, WCO, C::FN>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
   for (int t = 0; t < NST - 1 && t < nk; ++t) issue(t, t);
 
   while (true) {
+    if constexpr (SPARSE) live_next = live_bits(0);
 
     for (int t = 0; t < nk; ++t) {
       const int cur = t % NST;
@@ -325,24 +348,36 @@ conv_big_kernel(const drnmi_conv_args p) {
       const char* sa = smem + cur * C::STAGE;
       const char* sb = sa + C::A_BYTES;
       constexpr int NG = C::SUB * C::GR;
+      // block sparsity: bit (fm * SUB + sub) = unit (row-block of fragment fm, K unit of substep
+      // sub) has a nonzero weight; wave-uniform (scalar loads, scalar branches).  The bits of step
+      // t+1 are loaded while step t computes.
+      uint32_t live = 0xffffffffu;
+      if constexpr (SPARSE) {
+        live = live_next;
+        if (t + 1 < nk) live_next = live_bits(t + 1);
+      }
       constexpr int PPG = (C::GLDS + C::GR - 1) / C::GR;   // DMA pieces per group (first substep)
       const bool nxt = (DRNMI_ABLATE & 1) ? false : t + NST - 1 < nk;
       const StepP sp = step_params(t + NST - 1);
       const int nst = (t + NST - 1) % NST;
-      bf16x8 af[2][C::FPG], bfr[2][4];
+      bf16x8 af[2][C::FPG], bfr[2][C::FN];
+      auto unit_live = [&](int q, int h) {
+        return !SPARSE || ((live >> ((((q % C::GR) * C::FPG + h) * C::SUB) + q / C::GR)) & 1u) != 0;
+      };
       auto load_a = [&](bf16x8 (&dst)[C::FPG], int q) {
         const int c = (q / C::GR) * 4 + fq;
 #pragma unroll
         for (int h = 0; h < C::FPG; ++h) {
           const int r = wc * WCO + ((q % C::GR) * C::FPG + h) * 16 + fr;
+          // unconditional: a branch around an LDS read makes the compiler fall back to lgkmcnt(0)
           dst[h] = *reinterpret_cast<const bf16x8*>(sa + r * C::ROWB + swz<BK>(r, c) * 16);
         }
       };
-      auto load_b = [&](bf16x8 (&dst)[4], int sub) {
+      auto load_b = [&](bf16x8 (&dst)[C::FN], int sub) {
         const int c = sub * 4 + fq;
 #pragma unroll
-        for (int fn = 0; fn < 4; ++fn) {
-          const int r = wp * 64 + fn * 16 + fr;
+        for (int fn = 0; fn < C::FN; ++fn) {
+          const int r = wp * C::PXW + fn * 16 + fr;
           dst[fn] = *reinterpret_cast<const bf16x8*>(sb + r * C::ROWB + swz<BK>(r, c) * 16);
         }
       };
@@ -358,14 +393,16 @@ conv_big_kernel(const drnmi_conv_args p) {
 #pragma unroll
           for (int h = 0; h < C::FPG; ++h)
 #pragma unroll
-            for (int fn = 0; fn < 4; ++fn) asm volatile("" :: "v"(af[q & 1][h]), "v"(bfr[(q / C::GR) & 1][fn]));
+            for (int fn = 0; fn < C::FN; ++fn) asm volatile("" :: "v"(af[q & 1][h]), "v"(bfr[(q / C::GR) & 1][fn]));
         } else {
 #pragma unroll
-        for (int h = 0; h < C::FPG; ++h)
+        for (int h = 0; h < C::FPG; ++h) {
+          if (!unit_live(q, h)) continue;        // all-zero 16 x 32 weight unit: no MFMA
 #pragma unroll
-          for (int fn = 0; fn < 4; ++fn)
+          for (int fn = 0; fn < C::FN; ++fn)
             acc[(q % C::GR) * C::FPG + h][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 af[q & 1][h], bfr[(q / C::GR) & 1][fn], acc[(q % C::GR) * C::FPG + h][fn], 0, 0, 0);
+        }
         }
         if (q < C::GR && nxt) {
 #pragma unroll
@@ -392,9 +429,9 @@ conv_big_kernel(const drnmi_conv_args p) {
       }
     }
 
-    store_tile<C::FM, WCO>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+    store_tile<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
     if (!more) break;
-    init_tile<C::FM, WCO>(p, acc, px0, co0, wc, wp, fr, fq);
+    init_tile<C::FM, WCO, C::FN>(p, acc, px0, co0, wc, wp, fr, fq);
   }
 }
 
@@ -610,13 +647,13 @@ hipError_t launch_pp(const drnmi_conv_args& p, hipStream_t s) {
 
 int g_num_cus = 0;
 
-template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST>
+template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP = 4, bool SPARSE = false>
 hipError_t launch_big(const drnmi_conv_args& p, hipStream_t s) {
-  using C = BigCfg<WCO, WC, NST, BK>;
+  using C = BigCfg<WCO, WC, NST, BK, NWP>;
   static bool attr_set = false;
   if (!attr_set) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_big_kernel<KS, WCO, WC, NST, BK, PERSIST>),
+        reinterpret_cast<const void*>(&conv_big_kernel<KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -635,7 +672,7 @@ hipError_t launch_big(const drnmi_conv_args& p, hipStream_t s) {
     const int64_t cap = g_num_cus * (per_cu > 0 ? per_cu : 1);
     blocks = blocks < cap ? blocks : cap;
   }
-  hipLaunchKernelGGL((conv_big_kernel<KS, WCO, WC, NST, BK, PERSIST>), dim3(static_cast<unsigned>(blocks)),
+  hipLaunchKernelGGL((conv_big_kernel<KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE>), dim3(static_cast<unsigned>(blocks)),
                      dim3(C::THREADS), C::LDS, s, p);
   return hipGetLastError();
 }
@@ -648,18 +685,18 @@ struct Variant {
 
 // tile ids 4 + v in drnmi_conv_args.tile
 constexpr Variant kVariants[] = {
-    {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, false>", "conv_big_kernel<1, 128, 1, 3, 64, false>"},
-    {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, false>", "conv_big_kernel<1, 128, 2, 2, 64, false>"},
-    {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, false>", "conv_big_kernel<1, 64, 1, 4, 32, false>"},
-    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, false>", "conv_big_kernel<1, 32, 1, 3, 64, false>"},
-    {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, false>", "conv_big_kernel<1, 128, 2, 4, 32, false>"},
-    {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, false>", "conv_big_kernel<1, 128, 1, 4, 32, false>"},
-    {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, true>", "conv_big_kernel<1, 128, 1, 3, 64, true>"},
-    {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, true>", "conv_big_kernel<1, 128, 2, 2, 64, true>"},
-    {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, true>", "conv_big_kernel<1, 64, 1, 4, 32, true>"},
-    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, true>", "conv_big_kernel<1, 32, 1, 3, 64, true>"},
-    {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, true>", "conv_big_kernel<1, 128, 2, 4, 32, true>"},
-    {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, true>", "conv_big_kernel<1, 128, 1, 4, 32, true>"},
+    {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, false, 4, false>", "conv_big_kernel<1, 128, 1, 3, 64, false, 4, false>"},
+    {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, false, 4, false>", "conv_big_kernel<1, 128, 2, 2, 64, false, 4, false>"},
+    {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, false, 4, false>", "conv_big_kernel<1, 64, 1, 4, 32, false, 4, false>"},
+    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, false, 4, false>", "conv_big_kernel<1, 32, 1, 3, 64, false, 4, false>"},
+    {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, false, 4, false>", "conv_big_kernel<1, 128, 2, 4, 32, false, 4, false>"},
+    {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, false, 4, false>", "conv_big_kernel<1, 128, 1, 4, 32, false, 4, false>"},
+    {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, true, 4, false>", "conv_big_kernel<1, 128, 1, 3, 64, true, 4, false>"},
+    {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, true, 4, false>", "conv_big_kernel<1, 128, 2, 2, 64, true, 4, false>"},
+    {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, true, 4, false>", "conv_big_kernel<1, 64, 1, 4, 32, true, 4, false>"},
+    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, true, 4, false>", "conv_big_kernel<1, 32, 1, 3, 64, true, 4, false>"},
+    {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, true, 4, false>", "conv_big_kernel<1, 128, 2, 4, 32, true, 4, false>"},
+    {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, true, 4, false>", "conv_big_kernel<1, 128, 1, 4, 32, true, 4, false>"},
     {256, 64, "conv_pp_kernel<3>", "conv_pp_kernel<1>"},
 };
 constexpr int kPingPong = 12;
@@ -679,9 +716,62 @@ hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
   }
 }
 
+template <int KS>
+hipError_t launch_sparse(const drnmi_conv_args& p, int base, hipStream_t s) {
+  switch (base) {
+    case 0: return launch_big<KS, 128, 1, 3, 64, false, 4, true>(p, s);
+    case 1: return launch_big<KS, 128, 2, 2, 64, false, 4, true>(p, s);
+    case 4: return launch_big<KS, 128, 2, 4, 32, false, 4, true>(p, s);
+    case 5: return launch_big<KS, 128, 1, 4, 32, false, 4, true>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+const char* sparse_name(int ks, int base) {
+  static const char* n3[6] = {"conv_big_kernel<3, 128, 1, 3, 64, false, 4, true>",
+                              "conv_big_kernel<3, 128, 2, 2, 64, false, 4, true>", nullptr, nullptr,
+                              "conv_big_kernel<3, 128, 2, 4, 32, false, 4, true>",
+                              "conv_big_kernel<3, 128, 1, 4, 32, false, 4, true>"};
+  static const char* n1[6] = {"conv_big_kernel<1, 128, 1, 3, 64, false, 4, true>",
+                              "conv_big_kernel<1, 128, 2, 2, 64, false, 4, true>", nullptr, nullptr,
+                              "conv_big_kernel<1, 128, 2, 4, 32, false, 4, true>",
+                              "conv_big_kernel<1, 128, 1, 4, 32, false, 4, true>"};
+  return ks == 3 ? n3[base] : n1[base];
+}
+
 int auto_variant(const drnmi_conv_args& p) {
   if (p.cin < 64) return p.cout % 256 == 0 ? 4 : p.cout % 128 == 0 ? 5 : 2;   // K steps of 32
   return p.cout % 256 == 0 ? 1 : p.cout % 128 == 0 ? 0 : p.cout > 32 ? 2 : 3;
+}
+
+// one lane per 16 x 32 unit; lanes 0-31 / 32-63 of a wave cover the 32 units of two mask words
+template <typename T>
+__global__ void __launch_bounds__(256)
+unit_mask_kernel(const T* __restrict__ w, int rows_pad, int k_pad, int wpr, uint32_t* __restrict__ mask,
+                 int* __restrict__ count) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t word = gid >> 5;
+  const int bit = static_cast<int>(gid & 31);
+  const int rb = static_cast<int>(word / wpr);
+  const int ku = static_cast<int>(word % wpr) * 32 + bit;
+  const int nku = k_pad >> 5;
+  bool nz = false;
+  if (rb < rows_pad / 16 && ku < nku) {
+    for (int r = 0; r < 16 && !nz; ++r) {
+      const T* row = w + static_cast<int64_t>(rb * 16 + r) * k_pad + ku * 32;
+      for (int c = 0; c < 32; ++c) {
+        if constexpr (sizeof(T) == 2) nz |= (row[c] & 0x7fff) != 0;
+        else nz |= (__float_as_uint(row[c]) & 0x7fffffffu) != 0;
+      }
+    }
+  }
+  const uint64_t b = __ballot(nz);
+  const int lane = threadIdx.x & 63;
+  if (rb < rows_pad / 16) {
+    if (lane == 0) mask[word] = static_cast<uint32_t>(b & 0xffffffffu);
+    if (lane == 32) mask[word] = static_cast<uint32_t>(b >> 32);
+  }
+  if (count != nullptr && nz) atomicAdd(count, 1);
 }
 
 }  // namespace
@@ -693,6 +783,7 @@ bool big_conv_supported(const drnmi_conv_args& p) {
 }
 
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
+  // the halo kernel (cin/cout 64-128) stays dense: it beats unit skipping on those shapes
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_dispatch(p, s);
   if (!big_conv_supported(p)) return DRNMI_ENOTSUP;
   if (variant < 0) variant = auto_variant(p);
@@ -709,6 +800,10 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   }
   const int base = variant % 6;
   const bool persist = variant >= 6;
+  if (p.unit_mask != nullptr && !persist && sparse_name(p.ks, base) != nullptr) {
+    e = p.ks == 3 ? launch_sparse<3>(p, base, s) : launch_sparse<1>(p, base, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
   if (p.ks == 3) e = persist ? launch_base<3, true>(p, base, s) : launch_base<3, false>(p, base, s);
   else e = persist ? launch_base<1, true>(p, base, s) : launch_base<1, false>(p, base, s);
   return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
@@ -718,9 +813,32 @@ const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_name(p);
   if (variant < 0) variant = auto_variant(p);
   if (variant >= kNumVariants) return nullptr;
+  if (p.unit_mask != nullptr && variant < 6 && sparse_name(p.ks, variant) != nullptr) return sparse_name(p.ks, variant);
   return p.ks == 3 ? kVariants[variant].name3 : kVariants[variant].name1;
 }
 
 int big_conv_num_variants() { return kNumVariants; }
+
+int weight_unit_mask(const void* wgt, int dtype, int rows_pad, int k_pad, uint32_t* mask, int* count,
+                     hipStream_t s) {
+  if (wgt == nullptr || mask == nullptr || rows_pad <= 0 || rows_pad % 16 != 0 || k_pad <= 0 || k_pad % 32 != 0)
+    return DRNMI_EINVAL;
+  const int wpr = (k_pad + 1023) / 1024;
+  const int64_t lanes = static_cast<int64_t>(rows_pad / 16) * wpr * 32;
+  const unsigned blocks = static_cast<unsigned>((lanes + 255) / 256);
+  if (count != nullptr) {
+    const hipError_t e = hipMemsetAsync(count, 0, sizeof(int), s);
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  if (dtype == DRNMI_BF16)
+    hipLaunchKernelGGL(unit_mask_kernel<uint16_t>, dim3(blocks), dim3(256), 0, s,
+                       reinterpret_cast<const uint16_t*>(wgt), rows_pad, k_pad, wpr, mask, count);
+  else if (dtype == DRNMI_F32)
+    hipLaunchKernelGGL(unit_mask_kernel<float>, dim3(blocks), dim3(256), 0, s, reinterpret_cast<const float*>(wgt),
+                       rows_pad, k_pad, wpr, mask, count);
+  else
+    return DRNMI_EINVAL;
+  return static_cast<int>(hipGetLastError());
+}
 
 }  // namespace drnmi

@@ -352,6 +352,11 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   return static_cast<int>(e);
 }
 
+extern "C" int drnmi_weight_unit_mask(const void* wgt, int32_t dtype, int32_t rows_pad, int32_t k_pad,
+                                      uint32_t* mask, int32_t* nonzero_units, void* stream) {
+  return weight_unit_mask(wgt, dtype, rows_pad, k_pad, mask, nonzero_units, reinterpret_cast<hipStream_t>(stream));
+}
+
 extern "C" const char* drnmi_conv_kernel_name(const drnmi_conv_args* a) {
   if (a == nullptr) return nullptr;
   const drnmi_conv_args& p = *a;

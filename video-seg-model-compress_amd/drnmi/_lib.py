@@ -38,6 +38,7 @@ class ConvArgs(ctypes.Structure):
         ("bgr", ctypes.c_int32),
         ("mean", ctypes.c_float * 3),
         ("std", ctypes.c_float * 3),
+        ("unit_mask", ctypes.c_void_p),
     ]
 
 
@@ -86,6 +87,7 @@ SIGNATURES = {
     "drnmi_ce_loss_f32": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I64, _I64, _VP, _VP, _VP, _VP]),
     "drnmi_ce_loss_bwd_f32": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I64, _I64, _VP, _VP, _VP, _VP]),
     "drnmi_sgd_step_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP, _VP, _VP, _F32, _F32, _F32, _F32, _I32, _VP]),
+    "drnmi_weight_unit_mask": (ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP]),
     "drnmi_version": (ctypes.c_char_p, []),
 }
 

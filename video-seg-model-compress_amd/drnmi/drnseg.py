@@ -74,6 +74,7 @@ class DRNSeg(nn.Module):
         self.model_name = model_name
         self.classes = classes
         self.precision = "fp32"
+        self.block_sparse = False    # opt-in: measured slower than dense below ~60 % zero units
         self._graph = lower_drnseg(self.layer, self.seg)
         self._packed = {}
         self._plans = {}
@@ -143,6 +144,16 @@ class DRNSeg(nn.Module):
         self.precision = precision
         return self
 
+    def set_block_sparse(self, enabled: bool) -> "DRNSeg":
+        """bf16: let pruned (all-zero) 16 x 32 weight units skip their MFMAs (opt-in; results are
+        bit-identical either way; layers with < SPARSE_MIN_ZERO_UNITS zero units stay dense).
+        Takes effect at the next pack."""
+        self.block_sparse = bool(enabled)
+        for pk in self._packed.values():
+            pk.block_sparse = self.block_sparse
+        self._pack_key = None
+        return self
+
     def plan(self, n, h, w, device=None, keep_all=False) -> Plan:
         device = device or next(self.parameters()).device
         plan, _ = self._prepare(n, h, w, torch.device(device), keep_all=keep_all)
@@ -186,7 +197,7 @@ class DRNSeg(nn.Module):
             self._pack_key = key
         pk = self._packed.get(self.precision)
         if pk is None:
-            pk = PackedNet(self._graph, self.precision, device)
+            pk = PackedNet(self._graph, self.precision, device, block_sparse=self.block_sparse)
             self._packed[self.precision] = pk
         pkey = (self.precision, n, h, w, keep_all)
         plan = self._plans.get(pkey)

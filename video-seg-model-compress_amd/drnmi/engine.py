@@ -68,6 +68,8 @@ class ConvNode:
     k_pad: int = 0
     cout_pad: int = 0
     scale_folded: bool = False   # BN scale multiplied into wpk; launched with scale = NULL
+    unit_mask: torch.Tensor | None = None   # block-sparsity map of wpk (MFMA skips zero units)
+    zero_unit_frac: float = 0.0
 
 
 @dataclass
@@ -154,8 +156,9 @@ def _fold_bn(bn: nn.BatchNorm2d):
 class PackedNet:
     """Device-resident packed weights for one precision."""
 
-    def __init__(self, graph: Graph, precision: str, device):
+    def __init__(self, graph: Graph, precision: str, device, block_sparse: bool = True):
         self.graph = graph
+        self.block_sparse = block_sparse
         self.precision = precision
         self.tdtype, self.code = DTYPES[precision]
         self.device = device
@@ -197,6 +200,9 @@ class PackedNet:
                 nd.scale_folded = self.precision == "bf16" and _fused_init_route(nd, cs)
                 if nd.scale_folded:
                     nd.wpk = (full * scale[:, None]).to(self.tdtype).contiguous()
+                nd.unit_mask, nd.zero_unit_frac = None, 0.0
+                if nd.scale_folded and self.block_sparse:
+                    nd.unit_mask, nd.zero_unit_frac = _unit_mask(nd.wpk, self.code)
             # fused-ingest stem weights (bf16 patch kernel reads uint8 frames directly)
             self.stem_u8_w = None
             stem = self.graph.nodes[0]
@@ -207,6 +213,27 @@ class PackedNet:
                 full = torch.zeros(stem.cout_pad, STEM_U8_K, device=self.device, dtype=torch.float32)
                 full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
                 self.stem_u8_w = full.to(self.tdtype).contiguous()
+
+
+# Below this fraction of all-zero 16 x 32 units the dense kernel is used: skipping costs scalar
+# flag loads and breaks the MFMA/LDS interleave, measured break-even near 50 %.
+SPARSE_MIN_ZERO_UNITS = 0.5
+
+
+def _unit_mask(wpk: torch.Tensor, code: int):
+    """Block-sparsity map of packed weights (include/drnmi.h drnmi_weight_unit_mask): one bit per
+    16 x 32 unit.  Returned only when enough units are all-zero (pruned) to pay for the
+    per-step flag loads; the count is read back once per (re)pack, never in the launch loop."""
+    rows, kp = wpk.shape
+    wpr = (kp + 1023) // 1024
+    mask = torch.empty((rows // 16) * wpr, dtype=torch.int32, device=wpk.device)
+    cnt = torch.empty(1, dtype=torch.int32, device=wpk.device)
+    lib = _lib.load()
+    _lib.check(lib.drnmi_weight_unit_mask(wpk.data_ptr(), code, rows, kp, mask.data_ptr(), cnt.data_ptr(),
+                                          ctypes.c_void_p(_lib.stream_ptr(wpk.device))), "weight_unit_mask")
+    units = (rows // 16) * (kp // 32)
+    zero = 1.0 - int(cnt.item()) / units
+    return (mask, zero) if zero >= SPARSE_MIN_ZERO_UNITS else (None, zero)
 
 
 def _uses_patch(nd: ConvNode, cin_stride: int, precision: str) -> bool:
@@ -321,6 +348,7 @@ class Plan:
         a.dtype = pk.code
         a.tile = -1
         a.algo = _lib.ALGO_PATCH if _uses_patch(nd, nd.cin_stride, pk.precision) else _lib.ALGO_IGEMM
+        a.unit_mask = nd.unit_mask.data_ptr() if nd.unit_mask is not None else None
         return a
 
     def _stem_u8_args(self) -> _lib.ConvArgs | None:
@@ -341,6 +369,7 @@ class Plan:
             a.wgt = nd.wpk.data_ptr()
             a.scale = None if nd.scale_folded else nd.scale.data_ptr()
             a.shift = nd.shift.data_ptr()
+            a.unit_mask = nd.unit_mask.data_ptr() if nd.unit_mask is not None else None
         if self.stem_u8 is not None:
             nd = self.packed.graph.nodes[0]
             self.stem_u8.wgt = self.packed.stem_u8_w.data_ptr()
