@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-enum drnmi_dtype { DRNMI_F32 = 0, DRNMI_BF16 = 1, DRNMI_U8 = 2, DRNMI_I64 = 3 };
+enum drnmi_dtype { DRNMI_F32 = 0, DRNMI_BF16 = 1, DRNMI_U8 = 2, DRNMI_I64 = 3, DRNMI_I8 = 4 };
 
 enum drnmi_status {
   DRNMI_OK = 0,
@@ -69,6 +69,14 @@ typedef struct drnmi_conv_args {
                              /* 32ku..32ku+31 are all zero and their MFMAs are skipped      */
                              /* (bf16 LDS-DMA kernels; NULL = dense).  Results are bit-     */
                              /* identical to the dense kernel on the same weights.          */
+  /* W8A8 (dtype DRNMI_I8: x, wgt, res int8; per-tensor symmetric activations, per-channel  */
+  /* weights; BASELINE config C5).  acc = int32 sum; v = float(acc) * scale[c] + shift[c];  */
+  /* v += float(res) * res_scale; ReLU; out_dtype DRNMI_I8 stores                           */
+  /* clamp(rint(v * out_scale), -127, 127), BF16 / F32 store v.  Each step is one fp32        */
+  /* rounding (no fused multiply-add), so a scalar restatement reproduces it bit for bit.  */
+  /* scale must be non-NULL for int8.  Ignored for other dtypes.                             */
+  float res_scale;
+  float out_scale;            /* 1 / (scale of the int8 output activation)                */
 } drnmi_conv_args;
 
 /* Algorithms behind drnmi_conv2d_bn_act:
@@ -100,6 +108,15 @@ int drnmi_conv2d_bn_act(const drnmi_conv_args* args, void* stream);
  * units; narrower blocks skip where neighbouring blocks are both pruned). */
 int drnmi_weight_unit_mask(const void* wgt, int32_t dtype, int32_t rows_pad, int32_t k_pad, uint32_t* mask,
                            int32_t* nonzero_units, void* stream);
+
+/* W8A8 helpers (BASELINE config C5; csrc/quant.hip).  The reference has no quantisation code
+ * (SURVEY.md C5 row): the scheme is ours.  Activations are per-tensor symmetric int8.
+ *   drnmi_quantize_i8: y[i] = clamp(rint(x[i] * inv_scale), -127, 127) over n elements
+ *     (x BF16 or F32, n % 8 == 0; one fp32 multiply, round-half-even) -- the bf16 -> int8
+ *     boundary in front of the first int8 conv.
+ *   drnmi_absmax: *out = max |x[i]| (device float; calibration of the activation scales). */
+int drnmi_quantize_i8(const void* x, int32_t dtype, int8_t* y, int64_t n, float inv_scale, void* stream);
+int drnmi_absmax(const void* x, int32_t dtype, int64_t n, float* out, void* stream);
 
 /* Name of the kernel (template instance) drnmi_conv2d_bn_act would launch for these
  * arguments, e.g. "conv_big_kernel<3, 128, 2, 2>"; NULL if none.  No launch, no GPU needed.

@@ -37,6 +37,10 @@
 #ifndef DRNMI_ABLATE
 #define DRNMI_ABLATE 0
 #endif
+// LDS fragment prefetch distance in MFMA groups (1 or 2)
+#ifndef DRNMI_PFD
+#define DRNMI_PFD 1
+#endif
 
 namespace drnmi {
 namespace {
@@ -72,11 +76,13 @@ __device__ __forceinline__ int xcd_remap2(int bid, int nwg) {
 // Accumulator start value.  With a NULL scale (BN scale pre-folded into the weights) the
 // tile starts from shift + residual: the residual loads go out with the prologue DMA and
 // hide under it, and the epilogue is a plain ReLU + convert + store.
-template <int FM, int WCO, int FN = 4>
+// DEFER: start from zero and add shift + residual in store_tile (keeps the accumulators free of
+// VALU work so the compiler can hold them in AGPRs — the 128 x 128-per-wave tiles need that).
+template <int FM, int WCO, int FN = 4, bool DEFER = false>
 __device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)[FM][FN], int px0, int co0,
                                           int wc, int wp, int fr, int fq) {
   constexpr int PXW = 16 * FN;   // pixels per wave
-  if (p.scale != nullptr) {
+  if (DEFER || p.scale != nullptr) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -125,7 +131,7 @@ __device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)
   }
 }
 
-template <int FM, int WCO, int FN = 4>
+template <int FM, int WCO, int FN = 4, bool DEFER = false>
 __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4 (&acc)[FM][FN], int cur_px0,
                                            int cur_co0, int wc, int wp, int fr, int fq) {
   constexpr int PXW = 16 * FN;
@@ -153,8 +159,14 @@ __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4
         v[1] = v[1] * sc.y + sh.y;
         v[2] = v[2] * sc.z + sh.z;
         v[3] = v[3] * sc.w + sh.w;
+      } else if (DEFER) {
+        const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+        v[0] += sh.x;
+        v[1] += sh.y;
+        v[2] += sh.z;
+        v[3] += sh.w;
       }
-      if (p.scale != nullptr && res != nullptr) {
+      if ((DEFER || p.scale != nullptr) && res != nullptr) {
         if (full) {
           const uint2 rv = *reinterpret_cast<const uint2*>(res + static_cast<int64_t>(m) * p.cout + co);
           v[0] += bf16_to_f32(static_cast<uint16_t>(rv.x & 0xffff));
@@ -329,7 +341,8 @@ conv_big_kernel(const drnmi_conv_args p) {
     return bits;
   };
   uint32_t live_next = 0xffffffffu;
-  init_tile<C::FM, WCO, C::FN>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
+  constexpr bool DEFER = NWP < 4;
+  init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
   for (int t = 0; t < NST - 1 && t < nk; ++t) issue(t, t);
 
   while (true) {
@@ -360,7 +373,9 @@ conv_big_kernel(const drnmi_conv_args p) {
       const bool nxt = (DRNMI_ABLATE & 1) ? false : t + NST - 1 < nk;
       const StepP sp = step_params(t + NST - 1);
       const int nst = (t + NST - 1) % NST;
-      bf16x8 af[2][C::FPG], bfr[2][C::FN];
+      constexpr int PFD = DRNMI_PFD;
+      constexpr int NAF = PFD + 1;               // A-fragment ring depth
+      bf16x8 af[NAF][C::FPG], bfr[2][C::FN];
       auto unit_live = [&](int q, int h) {
         return !SPARSE || ((live >> ((((q % C::GR) * C::FPG + h) * C::SUB) + q / C::GR)) & 1u) != 0;
       };
@@ -382,18 +397,22 @@ conv_big_kernel(const drnmi_conv_args p) {
         }
       };
       load_b(bfr[0], 0);
-      load_a(af[0], 0);
+#pragma unroll
+      for (int q = 0; q < PFD && q < NG; ++q) {
+        load_a(af[q % NAF], q);
+        if (q > 0 && q % C::GR == 0) load_b(bfr[(q / C::GR) & 1], q / C::GR);
+      }
 #pragma unroll
       for (int q = 0; q < NG; ++q) {
-        if (q + 1 < NG) {
-          load_a(af[(q + 1) & 1], q + 1);
-          if ((q + 1) % C::GR == 0) load_b(bfr[((q + 1) / C::GR) & 1], (q + 1) / C::GR);
+        if (q + PFD < NG) {
+          load_a(af[(q + PFD) % NAF], q + PFD);
+          if ((q + PFD) % C::GR == 0) load_b(bfr[((q + PFD) / C::GR) & 1], (q + PFD) / C::GR);
         }
         if constexpr ((DRNMI_ABLATE & 2) != 0) {
 #pragma unroll
           for (int h = 0; h < C::FPG; ++h)
 #pragma unroll
-            for (int fn = 0; fn < C::FN; ++fn) asm volatile("" :: "v"(af[q & 1][h]), "v"(bfr[(q / C::GR) & 1][fn]));
+            for (int fn = 0; fn < C::FN; ++fn) asm volatile("" :: "v"(af[q % NAF][h]), "v"(bfr[(q / C::GR) & 1][fn]));
         } else {
 #pragma unroll
         for (int h = 0; h < C::FPG; ++h) {
@@ -401,7 +420,7 @@ conv_big_kernel(const drnmi_conv_args p) {
 #pragma unroll
           for (int fn = 0; fn < C::FN; ++fn)
             acc[(q % C::GR) * C::FPG + h][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                af[q & 1][h], bfr[(q / C::GR) & 1][fn], acc[(q % C::GR) * C::FPG + h][fn], 0, 0, 0);
+                af[q % NAF][h], bfr[(q / C::GR) & 1][fn], acc[(q % C::GR) * C::FPG + h][fn], 0, 0, 0);
         }
         }
         if (q < C::GR && nxt) {
@@ -429,9 +448,9 @@ conv_big_kernel(const drnmi_conv_args p) {
       }
     }
 
-    store_tile<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+    store_tile<C::FM, WCO, C::FN, DEFER>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
     if (!more) break;
-    init_tile<C::FM, WCO, C::FN>(p, acc, px0, co0, wc, wp, fr, fq);
+    init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);
   }
 }
 
@@ -715,6 +734,10 @@ hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
     default: return hipErrorInvalidValue;
   }
 }
+
+#ifdef DRNMI_WIDE_TEST
+template hipError_t launch_big<3, 128, 2, 2, 64, false, 2, false>(const drnmi_conv_args&, hipStream_t);
+#endif
 
 template <int KS>
 hipError_t launch_sparse(const drnmi_conv_args& p, int base, hipStream_t s) {

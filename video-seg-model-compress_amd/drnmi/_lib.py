@@ -10,7 +10,7 @@ import os
 
 from .build import LIB_PATH
 
-DRNMI_F32, DRNMI_BF16, DRNMI_U8, DRNMI_I64 = 0, 1, 2, 3
+DRNMI_F32, DRNMI_BF16, DRNMI_U8, DRNMI_I64, DRNMI_I8 = 0, 1, 2, 3, 4
 ALGO_IGEMM, ALGO_PATCH = 0, 1
 
 _STATUS = {-1: "DRNMI_EINVAL (bad shape/stride/dtype)", -2: "DRNMI_ENOTSUP (no kernel for this config)"}
@@ -39,6 +39,8 @@ class ConvArgs(ctypes.Structure):
         ("mean", ctypes.c_float * 3),
         ("std", ctypes.c_float * 3),
         ("unit_mask", ctypes.c_void_p),
+        ("res_scale", ctypes.c_float),
+        ("out_scale", ctypes.c_float),
     ]
 
 
@@ -88,6 +90,8 @@ SIGNATURES = {
     "drnmi_ce_loss_bwd_f32": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I64, _I64, _VP, _VP, _VP, _VP]),
     "drnmi_sgd_step_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP, _VP, _VP, _F32, _F32, _F32, _F32, _I32, _VP]),
     "drnmi_weight_unit_mask": (ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _VP, _VP]),
+    "drnmi_quantize_i8": (ctypes.c_int, [_VP, _I32, _VP, _I64, _F32, _VP]),
+    "drnmi_absmax": (ctypes.c_int, [_VP, _I32, _I64, _VP, _VP]),
     "drnmi_version": (ctypes.c_char_p, []),
 }
 
