@@ -37,12 +37,16 @@ def parse():
     ap.add_argument("--arch", default="drn_d_22")
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--width", type=int, default=2048)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "int8"],
+                    help="int8: W8A8 for the cin >= 64 convs (config C5), scales calibrated on 2 "
+                         "synthetic frames before the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
     ap.add_argument("--prune", default="", help="block:BHxBW:SPARSITY — BlockPruner masks (collapse_tensor "
-                    "False, BlockPruner.py:139-241) on every conv with >=16 input channels (config C3)")
+                    "False, BlockPruner.py:139-241) on every conv with >=16 input channels (config C3); "
+                    "json:PATH — any pruner config (pruner_type dispatch, e.g. the srmbrep D-22 configs "
+                    "of config C5)")
     ap.add_argument("--block-sparse", action="store_true", help="unit-skipping MFMA kernels on pruned weights "
                     "(opt-in; the dense kernel is faster below ~60%% zero 16x32 units)")
     return ap.parse_args()
@@ -58,29 +62,46 @@ def pruned_model(args, dev):
     from drnmi.drnseg import DRNSeg
     from drnmi.pruners import BlockPruner
     from drnmi.weights import synth_state_dict
-    kind, shape, sp = args.prune.split(":")
-    if kind != "block":
-        raise SystemExit("--prune: only block:BHxBW:SPARSITY")
-    bh, bw = (int(v) for v in shape.lower().split("x"))
     m = DRNSeg(args.arch, 19, pretrained=False)
     m.load_state_dict(synth_state_dict(m, 0))
-    layers = [k for k, v in m.state_dict().items() if k.startswith("layer.") and k.endswith(".weight")
-              and v.dim() == 4 and v.shape[1] >= 16 and v.shape[0] % bh == 0 and v.shape[1] % bw == 0]
-    cfg = {"pruner_type": "block", "configs": [{"layer_set": layers, "sparsity": float(sp), "block_height": bh,
-                                                "block_width": bw, "sub_rows": -1, "sub_cols": -1,
-                                                "collapse_tensor": False}]}
-    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
-        json.dump(cfg, f)
-    pr = BlockPruner(f.name, on_gpu=False)
-    pr.generate_masks(m, is_static=False)
-    os.unlink(f.name)
+    if args.prune.startswith("json:"):
+        from drnmi.pruners import make_pruner
+        pr = make_pruner(args.prune[len("json:"):], on_gpu=False)
+        pr.generate_masks(m, is_static=False)
+        layers = list(pr.mask_dict)
+    else:
+        kind, shape, sp = args.prune.split(":")
+        if kind != "block":
+            raise SystemExit("--prune: block:BHxBW:SPARSITY or json:PATH")
+        bh, bw = (int(v) for v in shape.lower().split("x"))
+        layers = [k for k, v in m.state_dict().items() if k.startswith("layer.") and k.endswith(".weight")
+                  and v.dim() == 4 and v.shape[1] >= 16 and v.shape[0] % bh == 0 and v.shape[1] % bw == 0]
+        cfg = {"pruner_type": "block", "configs": [{"layer_set": layers, "sparsity": float(sp), "block_height": bh,
+                                                    "block_width": bw, "sub_rows": -1, "sub_cols": -1,
+                                                    "collapse_tensor": False}]}
+        with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+            json.dump(cfg, f)
+        pr = BlockPruner(f.name, on_gpu=False)
+        pr.generate_masks(m, is_static=False)
+        os.unlink(f.name)
     with torch.no_grad():
         sd = m.state_dict()
         for k, mk in pr.mask_dict.items():
             sd[k].mul_(mk)
-    m = m.to(dev).eval().set_precision(args.precision)
+    m = m.to(dev).eval().set_precision("bf16" if args.precision == "int8" else args.precision)
     m.set_block_sparse(args.block_sparse)
     return m, len(layers)
+
+
+def calibrate(model, args, dev):
+    """int8: activation scales from 2 synthetic frames (a different stream than the timed
+    frames), then switch the engine to W8A8 (DRNSeg.calibrate_int8)."""
+    import torch
+    g = torch.Generator(device=dev).manual_seed(77)
+    calib = torch.randint(0, 256, (2, args.height, args.width, 3), dtype=torch.uint8, device=dev, generator=g)
+    model.calibrate_int8(calib)
+    model.set_precision("int8")
+    return model
 
 
 def cpu_baseline(args, seconds):
@@ -146,7 +167,10 @@ def main():
     if args.prune:
         model, n_pruned = pruned_model(args, dev)
     else:
-        model = build(args.arch, 19, seed=0, device=dev, precision=args.precision)
+        model = build(args.arch, 19, seed=0, device=dev,
+                      precision="bf16" if args.precision == "int8" else args.precision)
+    if args.precision == "int8":
+        model = calibrate(model, args, dev)
     B, H, W = args.batch, args.height, args.width
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     frames = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
@@ -225,7 +249,8 @@ def main():
         "vs_baseline": None,
         "dtype": args.precision,
         "data": f"synthetic uint8 RGB frames resident in HBM; hash-initialised {args.arch} weights (no checkpoint)"
-                + (f"; BlockPruner {args.prune} masks" if args.prune else ""),
+                + (f"; pruner masks {args.prune}" if args.prune else "")
+                + ("; int8 activation scales calibrated on 2 other synthetic frames" if args.precision == "int8" else ""),
         "config": {"workload": f"{args.arch} dense inference, seg_video loop (uint8 frame -> uint8 labels) "
                                f"{H}x{W}, {B} frames/GPU/step",
                    "arch": args.arch, "height": H, "width": W, "frames_per_gpu_step": B,
@@ -243,7 +268,7 @@ def main():
         avg_d = sum(durs) / len(durs)
         avg_f = sum(flops) / len(flops)
         ach = avg_f / avg_d / 1e12
-        peak = MFMA_PEAK[args.precision] / 1e12
+        peak = MFMA_PEAK["int8" if dominant.startswith("conv_i8") else plan.packed.base] / 1e12
         out["roofline"] = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 2), "peak": peak,
                            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
                            "traffic_unit": "bytes/launch", "traffic_source": traffic_src,

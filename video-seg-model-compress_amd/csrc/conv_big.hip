@@ -53,11 +53,38 @@ __device__ uint4 g_zero_page[64];   // zero-initialised: the source of padded ta
 constexpr int kBPX = 256;     // pixels per tile
 constexpr int kMinCin = 32;   // every K step lies inside one tap
 
-template <int BK>
-__device__ __forceinline__ int swz(int row, int chunk) {
-  if constexpr (BK == 64) return chunk ^ ((row >> 1) & 7);   // 128-B rows
-  else return chunk ^ ((row >> 2) & 3);                      //  64-B rows
+template <int ROWB>
+__device__ __forceinline__ int swzb(int row, int chunk) {
+  if constexpr (ROWB == 128) return chunk ^ ((row >> 1) & 7);   // 128-B rows
+  else return chunk ^ ((row >> 2) & 3);                        //  64-B rows
 }
+template <int BK>
+__device__ __forceinline__ int swz(int row, int chunk) { return swzb<BK * 2>(row, chunk); }   // bf16 rows
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Element traits of the LDS-DMA pipeline.  Both MFMAs consume 64 B of a row per lane group
+// (bf16 16x16x32: 32 elements; int8 16x16x64: 64 elements), so the LDS image, swizzle and
+// fragment reads are byte-identical; only the element count per K step and the MFMA differ.
+// (A and B fragments come from the same row layout, so the dot product does not depend on
+// the instruction's k order within the 64-B block.)
+template <typename T> struct KT;
+template <> struct KT<uint16_t> {
+  typedef bf16x8 frag;
+  typedef f32x4 acc;
+  static constexpr int ESZ = 2;
+  __device__ __forceinline__ static acc mma(frag a, frag b, acc c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct KT<int8_t> {
+  typedef i32x4 frag;
+  typedef i32x4 acc;
+  static constexpr int ESZ = 1;
+  __device__ __forceinline__ static acc mma(frag a, frag b, acc c) {
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+  }
+};
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
@@ -201,7 +228,96 @@ __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4
   }
 }
 
-template <int WCO, int WC, int NST, int BK, int NWP = 4>
+template <int FM, int FN>
+__device__ __forceinline__ void zero_tile(i32x4 (&acc)[FM][FN]) {
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = i32x4{0, 0, 0, 0};
+}
+
+// W8A8 epilogue (include/drnmi.h drnmi_conv_args, int8 fields): one fp32 rounding per step,
+// no contraction (fp contract off), so oracle/int8_oracle.py reproduces it bit for bit.
+template <int FM, int WCO, int FN>
+__device__ __forceinline__ void store_tile_i8(const drnmi_conv_args& p, const i32x4 (&acc)[FM][FN], int cur_px0,
+                                              int cur_co0, int wc, int wp, int fr, int fq) {
+#pragma clang fp contract(off)   // hipcc contracts a*b+c into v_fma by default (also inside inlined
+                                 // __fmul_rn / __fadd_rn): the epilogue is fmul then fadd
+  constexpr int PXW = 16 * FN;
+  const int M = p.n * p.ho * p.wo;
+  const int hw_o = p.ho * p.wo;
+  const int8_t* __restrict__ res = reinterpret_cast<const int8_t*>(p.res);
+  const bool packed4 = p.out_dtype == DRNMI_I8 && p.y_sc == 1;
+  const bool res4 = (p.cout & 3) == 0;
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    const int m = cur_px0 + wp * PXW + fn * 16 + fr;
+    if (m >= M) continue;
+    const int n = m / hw_o;
+    const int q = m - n * hw_o;
+    const int64_t ybase = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int co = cur_co0 + wc * WCO + fm * 16 + fq * 4;
+      if (co >= p.cout) continue;
+      const bool full = co + 3 < p.cout;
+      const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);   // padded to cout_pad
+      const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+      float v[4];
+      v[0] = static_cast<float>(acc[fm][fn][0]) * sc.x + sh.x;
+      v[1] = static_cast<float>(acc[fm][fn][1]) * sc.y + sh.y;
+      v[2] = static_cast<float>(acc[fm][fn][2]) * sc.z + sh.z;
+      v[3] = static_cast<float>(acc[fm][fn][3]) * sc.w + sh.w;
+      if (res != nullptr) {
+        int8_t r[4] = {0, 0, 0, 0};
+        const int8_t* rp = res + static_cast<int64_t>(m) * p.cout + co;
+        if (full && res4) {
+          const uint32_t rw = *reinterpret_cast<const uint32_t*>(rp);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] = static_cast<int8_t>((rw >> (8 * j)) & 0xff);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (co + j < p.cout) r[j] = rp[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = v[j] + static_cast<float>(r[j]) * p.res_scale;
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
+      if (p.out_dtype == DRNMI_I8) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float t = fminf(fmaxf(rintf(v[j] * p.out_scale), -127.f), 127.f);
+          o |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(t)))) << (8 * j);
+        }
+        int8_t* y = reinterpret_cast<int8_t*>(p.y);
+        if (packed4 && full) {
+          *reinterpret_cast<uint32_t*>(y + ybase + co) = o;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (co + j >= p.cout) break;
+            y[ybase + static_cast<int64_t>(co + j) * p.y_sc] = static_cast<int8_t>((o >> (8 * j)) & 0xff);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (co + j >= p.cout) break;
+          const int64_t off = ybase + static_cast<int64_t>(co + j) * p.y_sc;
+          if (p.out_dtype == DRNMI_BF16) reinterpret_cast<uint16_t*>(p.y)[off] = f32_to_bf16(v[j]);
+          else reinterpret_cast<float*>(p.y)[off] = v[j];
+        }
+      }
+    }
+  }
+}
+
+template <int WCO, int WC, int NST, int BK, int NWP = 4, int ESZ = 2>
 struct BigCfg {
   static constexpr int BCO = WCO * WC;              // output channels per tile
   static constexpr int FM = WCO / 16;               // channel fragments per wave
@@ -209,10 +325,10 @@ struct BigCfg {
   static constexpr int PXW = kBPX / NWP;            // pixels per wave
   static constexpr int FN = PXW / 16;               // pixel fragments per wave
   static constexpr int THREADS = 64 * NW;
-  static constexpr int ROWB = BK * 2;               // bytes per LDS row
+  static constexpr int ROWB = BK * ESZ;             // bytes per LDS row
   static constexpr int CPR = ROWB / 16;             // 16-B chunks per row
   static constexpr int RPI = 1024 / ROWB;           // rows per 1-KB DMA wave instruction
-  static constexpr int SUB = BK / 32;               // 32-deep MFMA substeps per step
+  static constexpr int SUB = ROWB / 64;             // 64-B MFMA substeps per step
   static constexpr int A_BYTES = BCO * ROWB;
   static constexpr int B_BYTES = kBPX * ROWB;
   static constexpr int STAGE = A_BYTES + B_BYTES;
@@ -226,10 +342,12 @@ struct BigCfg {
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE>
-__global__ void __launch_bounds__(64 * NWP * WC, 1)
-conv_big_kernel(const drnmi_conv_args p) {
-  using C = BigCfg<WCO, WC, NST, BK, NWP>;
+template <typename T, int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE>
+__device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
+  using K = KT<T>;
+  using C = BigCfg<WCO, WC, NST, BK, NWP, K::ESZ>;
+  static_assert(!SPARSE || K::ESZ == 2, "unit skipping: bf16 only");
+  constexpr int CE = 16 / K::ESZ;   // elements per 16-B chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
@@ -246,11 +364,11 @@ conv_big_kernel(const drnmi_conv_args p) {
   const int cin = p.cin;
   const int lc = 31 - __builtin_clz(cin);
   const int H = p.h, W = p.w, dil = p.dil;
-  const uint16_t* __restrict__ x = reinterpret_cast<const uint16_t*>(p.x);
-  const uint16_t* __restrict__ wt = reinterpret_cast<const uint16_t*>(p.wgt);
+  const T* __restrict__ x = reinterpret_cast<const T*>(p.x);
+  const T* __restrict__ wt = reinterpret_cast<const T*>(p.wgt);
   const int nk = p.k_pad / BK;
   const int fr = lane & 15;       // fragment row (channel or pixel within a 16-block)
-  const int fq = lane >> 4;       // 8-element k chunk within a 32-deep substep
+  const int fq = lane >> 4;       // 16-B k chunk within a 64-B substep
 
   // --- DMA assignment.  One wave instruction fills RPI LDS rows (1 KB); lane l fills row
   // RPI*j + l / CPR, slot l % CPR.  Wave w fills A instructions [w*A_INSTR, ...) (weights)
@@ -259,14 +377,14 @@ conv_big_kernel(const drnmi_conv_args p) {
   const int lslot = lane % C::CPR;
   int a_src_off[C::A_INSTR];
   int b_ih0[C::B_INSTR], b_iw0[C::B_INSTR];
-  const uint16_t* b_base[C::B_INSTR];
+  const T* b_base[C::B_INSTR];
   const char* zero_src = reinterpret_cast<const char*>(g_zero_page) + lane * 16;
 
   auto setup = [&](int px0, int co0) {
 #pragma unroll
     for (int i = 0; i < C::A_INSTR; ++i) {
       const int r = (wave * C::A_INSTR + i) * C::RPI + lrow;
-      a_src_off[i] = (co0 + r) * p.k_pad + swz<BK>(r, lslot) * 8;
+      a_src_off[i] = (co0 + r) * p.k_pad + swzb<C::ROWB>(r, lslot) * CE;
     }
     // pixel rows: (ih0, iw0) of tap (0,0) and a base pointer at that tap's chunk (only
     // dereferenced when the tap lies inside the image)
@@ -284,7 +402,7 @@ conv_big_kernel(const drnmi_conv_args p) {
         const int ow = q - oh * p.wo;
         b_ih0[i] = oh * p.stride - p.pad;
         b_iw0[i] = ow * p.stride - p.pad;
-        b_base[i] = x + ((static_cast<int64_t>(n) * H + b_ih0[i]) * W + b_iw0[i]) * cin + swz<BK>(r, lslot) * 8;
+        b_base[i] = x + ((static_cast<int64_t>(n) * H + b_ih0[i]) * W + b_iw0[i]) * cin + swzb<C::ROWB>(r, lslot) * CE;
       }
     }
   };
@@ -322,7 +440,7 @@ conv_big_kernel(const drnmi_conv_args p) {
   };
 
 
-  f32x4 acc[C::FM][C::FN];
+  typename K::acc acc[C::FM][C::FN];
   int tl = blockIdx.x;
   int tile = xcd_remap2(tl, ntiles);
   int px0 = (tile / nco) * kBPX;
@@ -342,7 +460,8 @@ conv_big_kernel(const drnmi_conv_args p) {
   };
   uint32_t live_next = 0xffffffffu;
   constexpr bool DEFER = NWP < 4;
-  init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
+  if constexpr (K::ESZ == 2) init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
+  else zero_tile(acc);
   for (int t = 0; t < NST - 1 && t < nk; ++t) issue(t, t);
 
   while (true) {
@@ -375,25 +494,25 @@ conv_big_kernel(const drnmi_conv_args p) {
       const int nst = (t + NST - 1) % NST;
       constexpr int PFD = DRNMI_PFD;
       constexpr int NAF = PFD + 1;               // A-fragment ring depth
-      bf16x8 af[NAF][C::FPG], bfr[2][C::FN];
+      typename K::frag af[NAF][C::FPG], bfr[2][C::FN];
       auto unit_live = [&](int q, int h) {
         return !SPARSE || ((live >> ((((q % C::GR) * C::FPG + h) * C::SUB) + q / C::GR)) & 1u) != 0;
       };
-      auto load_a = [&](bf16x8 (&dst)[C::FPG], int q) {
+      auto load_a = [&](typename K::frag (&dst)[C::FPG], int q) {
         const int c = (q / C::GR) * 4 + fq;
 #pragma unroll
         for (int h = 0; h < C::FPG; ++h) {
           const int r = wc * WCO + ((q % C::GR) * C::FPG + h) * 16 + fr;
           // unconditional: a branch around an LDS read makes the compiler fall back to lgkmcnt(0)
-          dst[h] = *reinterpret_cast<const bf16x8*>(sa + r * C::ROWB + swz<BK>(r, c) * 16);
+          dst[h] = *reinterpret_cast<const typename K::frag*>(sa + r * C::ROWB + swzb<C::ROWB>(r, c) * 16);
         }
       };
-      auto load_b = [&](bf16x8 (&dst)[C::FN], int sub) {
+      auto load_b = [&](typename K::frag (&dst)[C::FN], int sub) {
         const int c = sub * 4 + fq;
 #pragma unroll
         for (int fn = 0; fn < C::FN; ++fn) {
           const int r = wp * C::PXW + fn * 16 + fr;
-          dst[fn] = *reinterpret_cast<const bf16x8*>(sb + r * C::ROWB + swz<BK>(r, c) * 16);
+          dst[fn] = *reinterpret_cast<const typename K::frag*>(sb + r * C::ROWB + swzb<C::ROWB>(r, c) * 16);
         }
       };
       load_b(bfr[0], 0);
@@ -419,8 +538,8 @@ conv_big_kernel(const drnmi_conv_args p) {
           if (!unit_live(q, h)) continue;        // all-zero 16 x 32 weight unit: no MFMA
 #pragma unroll
           for (int fn = 0; fn < C::FN; ++fn)
-            acc[(q % C::GR) * C::FPG + h][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                af[q % NAF][h], bfr[(q / C::GR) & 1][fn], acc[(q % C::GR) * C::FPG + h][fn], 0, 0, 0);
+            acc[(q % C::GR) * C::FPG + h][fn] = K::mma(
+                af[q % NAF][h], bfr[(q / C::GR) & 1][fn], acc[(q % C::GR) * C::FPG + h][fn]);
         }
         }
         if (q < C::GR && nxt) {
@@ -448,10 +567,27 @@ conv_big_kernel(const drnmi_conv_args p) {
       }
     }
 
-    store_tile<C::FM, WCO, C::FN, DEFER>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+    if constexpr (K::ESZ == 2) store_tile<C::FM, WCO, C::FN, DEFER>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+    else store_tile_i8<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
     if (!more) break;
-    init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);
+    if constexpr (K::ESZ == 2) init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);
+    else zero_tile(acc);
   }
+}
+
+template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE>
+__global__ void __launch_bounds__(64 * NWP * WC, 1)
+conv_big_kernel(const drnmi_conv_args p) {
+  conv_big_body<uint16_t, KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE>(p);
+}
+
+// W8A8 (config C5): the same LDS-DMA pipeline over int8 elements, BK int8 channels per K step
+// (128-B LDS rows for cin >= 128, 64-B rows for cin == 64), v_mfma_i32_16x16x64_i8 into int32
+// accumulators, store_tile_i8 epilogue.
+template <int KS, int WCO, int WC, int NST, int BK>
+__global__ void __launch_bounds__(64 * 4 * WC, 1)
+conv_i8_kernel(const drnmi_conv_args p) {
+  conv_big_body<int8_t, KS, WCO, WC, NST, BK, false, 4, false>(p);
 }
 
 // --- Ping-pong 256 x 256 schedule (variant "pp256").
@@ -735,6 +871,53 @@ hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
   }
 }
 
+template <int KS, int WCO, int WC, int NST, int BK>
+hipError_t launch_i8(const drnmi_conv_args& p, hipStream_t s) {
+  using C = BigCfg<WCO, WC, NST, BK, 4, 1>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_i8_kernel<KS, WCO, WC, NST, BK>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const int64_t blocks = ((M + kBPX - 1) / kBPX) * ((p.cout + C::BCO - 1) / C::BCO);
+  hipLaunchKernelGGL((conv_i8_kernel<KS, WCO, WC, NST, BK>), dim3(static_cast<unsigned>(blocks)), dim3(C::THREADS),
+                     C::LDS, s, p);
+  return hipGetLastError();
+}
+
+// int8 variants: 0 = 256 x 256 tile / 128-B rows, 1 = 128 x 256 / 128-B, 2 = 256 x 256 / 64-B,
+// 3 = 128 x 256 / 64-B (K steps of 128 or 64 int8 channels)
+struct I8Variant {
+  int bco;
+  const char* name3;
+  const char* name1;
+};
+constexpr I8Variant kI8Variants[] = {
+    {256, "conv_i8_kernel<3, 128, 2, 2, 128>", "conv_i8_kernel<1, 128, 2, 2, 128>"},
+    {128, "conv_i8_kernel<3, 128, 1, 3, 128>", "conv_i8_kernel<1, 128, 1, 3, 128>"},
+    {256, "conv_i8_kernel<3, 128, 2, 4, 64>", "conv_i8_kernel<1, 128, 2, 4, 64>"},
+    {128, "conv_i8_kernel<3, 128, 1, 4, 64>", "conv_i8_kernel<1, 128, 1, 4, 64>"},
+};
+
+int i8_variant(const drnmi_conv_args& p) {
+  const int wide = p.cout % 256 == 0 ? 0 : 1;
+  return (p.cin >= 128 ? 0 : 2) + wide;
+}
+
+template <int KS>
+hipError_t launch_i8_variant(const drnmi_conv_args& p, int v, hipStream_t s) {
+  switch (v) {
+    case 0: return launch_i8<KS, 128, 2, 2, 128>(p, s);   // 2 x 64 KB
+    case 1: return launch_i8<KS, 128, 1, 3, 128>(p, s);   // 3 x 48 KB
+    case 2: return launch_i8<KS, 128, 2, 4, 64>(p, s);    // 4 x 32 KB
+    case 3: return launch_i8<KS, 128, 1, 4, 64>(p, s);    // 4 x 24 KB
+    default: return hipErrorInvalidValue;
+  }
+}
+
 #ifdef DRNMI_WIDE_TEST
 template hipError_t launch_big<3, 128, 2, 2, 64, false, 2, false>(const drnmi_conv_args&, hipStream_t);
 #endif
@@ -798,6 +981,27 @@ unit_mask_kernel(const T* __restrict__ w, int rows_pad, int k_pad, int wpr, uint
 }
 
 }  // namespace
+
+bool i8_conv_supported(const drnmi_conv_args& p) {
+  return p.dtype == DRNMI_I8 && p.scale != nullptr && p.cin >= 64 && (p.cin & (p.cin - 1)) == 0 &&
+         p.cout_pad % 128 == 0 && (p.ks == 1 || p.ks == 3) && p.k == p.ks * p.ks * p.cin && p.k_pad == p.k &&
+         static_cast<int64_t>(p.n) * p.h * p.w * p.cin < (int64_t(1) << 31) &&
+         (p.out_dtype == DRNMI_F32 || p.out_dtype == DRNMI_BF16 || p.out_dtype == DRNMI_I8);
+}
+
+int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
+  if (!i8_conv_supported(p)) return DRNMI_ENOTSUP;
+  const int v = i8_variant(p);
+  if ((p.cout + kI8Variants[v].bco - 1) / kI8Variants[v].bco * kI8Variants[v].bco > p.cout_pad) return DRNMI_EINVAL;
+  const hipError_t e = p.ks == 3 ? launch_i8_variant<3>(p, v, s) : launch_i8_variant<1>(p, v, s);
+  return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+}
+
+const char* i8_conv_name(const drnmi_conv_args& p) {
+  if (!i8_conv_supported(p)) return nullptr;
+  const int v = i8_variant(p);
+  return p.ks == 3 ? kI8Variants[v].name3 : kI8Variants[v].name1;
+}
 
 bool big_conv_supported(const drnmi_conv_args& p) {
   return p.dtype == DRNMI_BF16 && p.cin >= kMinCin && (p.cin & (p.cin - 1)) == 0 && p.cout_pad % 128 == 0 &&

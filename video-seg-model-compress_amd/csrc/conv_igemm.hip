@@ -333,13 +333,17 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (p.k_pad < p.k || p.k_pad % kBK != 0 || p.stride <= 0 || p.dil <= 0 || p.pad < 0) return DRNMI_EINVAL;
   if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.shift == nullptr)
     return DRNMI_EINVAL;
-  if ((p.dtype != DRNMI_BF16 && p.dtype != DRNMI_F32) ||
-      (p.out_dtype != DRNMI_BF16 && p.out_dtype != DRNMI_F32))
+  if (p.dtype == DRNMI_I8) {
+    if (p.out_dtype != DRNMI_I8 && p.out_dtype != DRNMI_BF16 && p.out_dtype != DRNMI_F32) return DRNMI_EINVAL;
+  } else if ((p.dtype != DRNMI_BF16 && p.dtype != DRNMI_F32) ||
+             (p.out_dtype != DRNMI_BF16 && p.out_dtype != DRNMI_F32)) {
     return DRNMI_EINVAL;
+  }
   // Output geometry must be the conv's: ho = (h + 2 pad - dil (ks-1) - 1) / stride + 1.
   if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
       p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
     return DRNMI_EINVAL;
+  if (p.dtype == DRNMI_I8) return i8_conv_dispatch(p, reinterpret_cast<hipStream_t>(stream));   // int8: one kernel family
   if (p.tile >= 4 || (p.tile < 0 && (big_conv_supported(p) || halo_conv_supported(p))))
     return big_conv_dispatch(p, p.tile < 0 ? -1 : p.tile - 4, reinterpret_cast<hipStream_t>(stream));
   const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;
@@ -361,6 +365,7 @@ extern "C" const char* drnmi_conv_kernel_name(const drnmi_conv_args* a) {
   if (a == nullptr) return nullptr;
   const drnmi_conv_args& p = *a;
   if (p.algo == DRNMI_ALGO_PATCH) return patch_conv_name(p);
+  if (p.dtype == DRNMI_I8) return i8_conv_name(p);
   if (p.tile >= 4 || (p.tile < 0 && (big_conv_supported(p) || halo_conv_supported(p))))
     return big_conv_name(p, p.tile < 0 ? -1 : p.tile - 4);
   const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;

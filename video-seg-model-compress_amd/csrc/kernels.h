@@ -11,6 +11,10 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s);  //
 const char* big_conv_name(const drnmi_conv_args& p, int variant);
 const char* patch_conv_name(const drnmi_conv_args& p);
 int weight_unit_mask(const void* wgt, int dtype, int rows_pad, int k_pad, uint32_t* mask, int* count, hipStream_t s);
+// W8A8 LDS-DMA implicit GEMM (conv_big.hip, config C5): dtype DRNMI_I8, cin >= 64.
+bool i8_conv_supported(const drnmi_conv_args& p);
+int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
+const char* i8_conv_name(const drnmi_conv_args& p);
 // Halo-patch 3x3 stride-1 conv, cin/cout 64 or 128 (conv_halo.hip).
 bool halo_conv_supported(const drnmi_conv_args& p);
 int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);

@@ -13,7 +13,9 @@ Differences by design:
     back to ATen; on CPU it raises.  In train mode it runs the fine-tune path
     (drnmi.train: batch-stat BN, autograd through the HIP backward kernels, fp32).
   * precision: "fp32" (default; the reference's arithmetic, parity mode, exact-fp32
-    MFMA) or "bf16" (perf mode, fp32 accumulation) via set_precision().
+    MFMA), "bf16" (perf mode, fp32 accumulation) or "int8" (W8A8 for the cin >= 64 convs,
+    config C5; needs calibrate_int8() first — the reference has no quantisation, so this
+    mode is ours) via set_precision().
   * segment(frames_u8) is the fused seg_video path (seg_video_old_no_plot.py:157-169:
     normalise -> model(img)[0] -> torch.max(final, 1)) producing uint8 labels without
     materialising the 19-plane log-prob tensor.
@@ -76,6 +78,7 @@ class DRNSeg(nn.Module):
         self.precision = "fp32"
         self.block_sparse = False    # opt-in: measured slower than dense below ~60 % zero units
         self._graph = lower_drnseg(self.layer, self.seg)
+        self._act_scales = None      # int8: per-value activation scales (calibrate_int8)
         self._packed = {}
         self._plans = {}
         self._pack_key = None
@@ -139,10 +142,42 @@ class DRNSeg(nn.Module):
 
     # ----------------------------------------------------------------- configuration
     def set_precision(self, precision: str) -> "DRNSeg":
-        if precision not in ("fp32", "bf16"):
-            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if precision not in ("fp32", "bf16", "int8"):
+            raise ValueError("precision must be 'fp32', 'bf16' or 'int8'")
         self.precision = precision
         return self
+
+    @torch.no_grad()
+    def calibrate_int8(self, frames_u8: torch.Tensor, mean=INFO_MEAN, std=INFO_STD, bgr: bool = False):
+        """Per-tensor activation scales for precision "int8": the bf16 engine runs the
+        calibration frames (uint8 [B,H,W,3] on the GPU) and every activation's scale is
+        absmax / 127 (drnmi_absmax on the HBM buffer).  Re-packs the int8 weights."""
+        import ctypes
+        prev = self.precision
+        self.precision = "bf16"
+        try:
+            plan, stream = self._prepare(frames_u8.shape[0], frames_u8.shape[1], frames_u8.shape[2],
+                                         frames_u8.device, keep_all=True)
+            plan.ingest_u8(frames_u8.contiguous(), mean, std, bgr, stream)
+            plan.run_backbone(stream)
+            lib = _lib.load()
+            amax = torch.empty(1, dtype=torch.float32, device=frames_u8.device)
+            scales = {}
+            for v, buf in plan.bufs.items():
+                if v in ("input", "logits"):
+                    continue
+                _lib.check(lib.drnmi_absmax(buf.data_ptr(), _lib.DRNMI_BF16, buf.numel(), amax.data_ptr(),
+                                            ctypes.c_void_p(stream)), "absmax")
+                a = float(amax.item())
+                scales[v] = a / 127.0 if a > 0 else 1.0
+        finally:
+            self.precision = prev
+            self._plans = {k: p for k, p in self._plans.items() if not k[-1]}   # drop the keep_all plan
+        self._act_scales = scales
+        self._packed.pop("int8", None)
+        self._plans = {k: p for k, p in self._plans.items() if k[0] != "int8"}
+        self._pack_key = None
+        return scales
 
     def set_block_sparse(self, enabled: bool) -> "DRNSeg":
         """bf16: let pruned (all-zero) 16 x 32 weight units skip their MFMAs (opt-in; results are
@@ -195,9 +230,12 @@ class DRNSeg(nn.Module):
                     if p == self.precision:
                         plan.refresh_weight_ptrs()
             self._pack_key = key
+        if self.precision == "int8" and self._act_scales is None:
+            raise RuntimeError("precision 'int8' needs activation scales: call calibrate_int8(frames) first")
         pk = self._packed.get(self.precision)
         if pk is None:
-            pk = PackedNet(self._graph, self.precision, device, block_sparse=self.block_sparse)
+            pk = PackedNet(self._graph, self.precision, device, block_sparse=self.block_sparse,
+                           act_scales=self._act_scales)
             self._packed[self.precision] = pk
         pkey = (self.precision, n, h, w, keep_all)
         plan = self._plans.get(pkey)

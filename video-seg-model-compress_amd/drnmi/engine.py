@@ -30,6 +30,11 @@ K_ALIGN = 32
 COUT_ALIGN = 128
 
 DTYPES = {"fp32": (torch.float32, _lib.DRNMI_F32), "bf16": (torch.bfloat16, _lib.DRNMI_BF16)}
+TORCH_OF_CODE = {_lib.DRNMI_F32: torch.float32, _lib.DRNMI_BF16: torch.bfloat16, _lib.DRNMI_I8: torch.int8}
+# W8A8 (config C5): convs whose input channel stride is >= this run on the int8 MFMA kernel
+# (conv_i8_kernel: K steps of 64/128 int8 channels); the full-resolution small-channel layers
+# (stem, layer1-3: ~5 % of D-22's FLOPs) stay bf16.
+INT8_MIN_CIN = 64
 
 # (cin_stride, cout, ks, stride, dil) served by the LDS-patch kernel (bf16 only; include/drnmi.h)
 # (32 -> 64 stride 2 runs faster on the K-32 LDS-DMA implicit GEMM: 67 vs 108 us per 4 frames)
@@ -70,6 +75,12 @@ class ConvNode:
     scale_folded: bool = False   # BN scale multiplied into wpk; launched with scale = NULL
     unit_mask: torch.Tensor | None = None   # block-sparsity map of wpk (MFMA skips zero units)
     zero_unit_frac: float = 0.0
+    # W8A8 (precision "int8"): int8 wpk, scale = weight scale x input scale x BN scale
+    i8: bool = False
+    x_val: str = ""              # value the launch reads (src, or "q:src" = its int8 copy)
+    r_val: str | None = None
+    res_scale: float = 0.0
+    out_scale: float = 0.0       # 1 / scale of an int8 output (0: bf16 / fp32 output)
 
 
 @dataclass
@@ -156,21 +167,66 @@ def _fold_bn(bn: nn.BatchNorm2d):
 class PackedNet:
     """Device-resident packed weights for one precision."""
 
-    def __init__(self, graph: Graph, precision: str, device, block_sparse: bool = True):
+    def __init__(self, graph: Graph, precision: str, device, block_sparse: bool = True,
+                 act_scales: dict | None = None):
         self.graph = graph
         self.block_sparse = block_sparse
         self.precision = precision
-        self.tdtype, self.code = DTYPES[precision]
+        # int8 nets run their small-channel layers in bf16: "base" is that precision
+        self.base = "bf16" if precision == "int8" else precision
+        self.tdtype, self.code = DTYPES[self.base]
         self.device = device
         self.cstride = {"input": 8}
         for v, c in graph.channels.items():
             if v != "input":
                 self.cstride[v] = _pow2_at_least(c)
+        self.act_scales = dict(act_scales or {})
+        self.vcode = {}            # value -> dtype code where it differs from self.code
+        self.quant_after = {}      # node index -> values quantised (bf16 -> "q:" int8) after it
+        self.i8_nodes = set()
+        if precision == "int8":
+            self._int8_layout()
         self.pack()
+
+    def _int8_layout(self):
+        """Which launches run W8A8 and which values are int8 in HBM.  A value is int8 when an
+        int8 launch produces it and only int8 launches read it; a bf16 value read by an int8
+        launch gets an int8 copy "q:<value>" quantised right after its producer."""
+        g = self.graph
+        # (cout >= 128 too: the int8 tiles are 128 channels wide; the 64-channel layer3 convs keep
+        # the bf16 halo kernel)
+        elig = {i for i, nd in enumerate(g.nodes)
+                if self.cstride[nd.src] >= INT8_MIN_CIN and nd.conv.kernel_size[0] in (1, 3)
+                and (nd.conv.out_channels >= 128 or nd.out_fp32_nchw)}
+        readers = {}
+        for i, nd in enumerate(g.nodes):
+            for v in (nd.src, nd.res):
+                if v:
+                    readers.setdefault(v, []).append(i)
+        for i in elig:
+            nd = g.nodes[i]
+            if not nd.out_fp32_nchw and readers.get(nd.dst) and all(j in elig for j in readers[nd.dst]):
+                self.vcode[nd.dst] = _lib.DRNMI_I8
+        producer = {nd.dst: i for i, nd in enumerate(g.nodes)}
+        need = {v for i in elig for v in (g.nodes[i].src, g.nodes[i].res) if v}
+        missing = sorted(v for v in need | set(self.vcode) if v not in self.act_scales)
+        if missing:
+            raise RuntimeError(f"int8: no calibrated activation scale for {missing} (DRNSeg.calibrate_int8)")
+        for v in sorted(need):
+            if self.vcode.get(v) != _lib.DRNMI_I8:
+                if v == "input":
+                    raise NotImplementedError("int8 launch reading the network input")
+                self.quant_after.setdefault(producer[v], []).append(v)
+        self.i8_nodes = elig
+
+    def value_code(self, v: str) -> int:
+        if v.startswith("q:"):
+            return _lib.DRNMI_I8
+        return self.vcode.get(v, self.code)
 
     def pack(self):
         with torch.no_grad():
-            for nd in self.graph.nodes:
+            for ni, nd in enumerate(self.graph.nodes):
                 conv = nd.conv
                 w = conv.weight.detach().to(self.device, torch.float32)
                 cout, cin, kh, kw = w.shape
@@ -195,9 +251,13 @@ class PackedNet:
                 elif conv.bias is not None:
                     shift[:cout] = conv.bias.detach().to(self.device, torch.float32)
                 nd.scale, nd.shift = scale.contiguous(), shift.contiguous()
+                nd.i8, nd.x_val, nd.r_val, nd.res_scale, nd.out_scale = False, nd.src, nd.res, 0.0, 0.0
+                if ni in self.i8_nodes:
+                    self._pack_int8(nd, full, scale, cout)
+                    continue
                 # bf16 LDS-DMA kernels: fold the BN scale into the weights so the kernel starts its
                 # accumulators from shift + residual (include/drnmi.h: scale may be NULL)
-                nd.scale_folded = self.precision == "bf16" and _fused_init_route(nd, cs)
+                nd.scale_folded = self.base == "bf16" and _fused_init_route(nd, cs)
                 if nd.scale_folded:
                     nd.wpk = (full * scale[:, None]).to(self.tdtype).contiguous()
                 nd.unit_mask, nd.zero_unit_frac = None, 0.0
@@ -207,12 +267,34 @@ class PackedNet:
             self.stem_u8_w = None
             stem = self.graph.nodes[0]
             w = stem.conv.weight.detach().to(self.device, torch.float32)
-            if self.precision == "bf16" and tuple(w.shape[1:]) == (3, 7, 7):
+            if self.base == "bf16" and tuple(w.shape[1:]) == (3, 7, 7):
                 wp = torch.zeros(w.shape[0], 7, 8, 4, device=self.device, dtype=torch.float32)
                 wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
                 full = torch.zeros(stem.cout_pad, STEM_U8_K, device=self.device, dtype=torch.float32)
                 full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
                 self.stem_u8_w = full.to(self.tdtype).contiguous()
+
+
+    def _pack_int8(self, nd: ConvNode, full: torch.Tensor, bn_scale: torch.Tensor, cout: int):
+        """Per-output-channel symmetric int8 weights (oracle/int8_oracle.py quantize_weight_rows):
+        s_w = absmax / 127, q = clamp(rint(w * 127 / absmax)); the epilogue scale is
+        s_w * s_x * bn_scale, so acc * scale is the dequantised, BN-scaled conv output."""
+        a = full.abs().amax(dim=1)
+        pos = a > 0
+        inv = torch.where(pos, 127.0 / torch.where(pos, a, torch.ones_like(a)), torch.ones_like(a))
+        nd.wpk = torch.round(full * inv[:, None]).clamp_(-127, 127).to(torch.int8).contiguous()
+        sw = torch.where(pos, a / 127.0, torch.ones_like(a))
+        sx = float(self.act_scales[nd.src])
+        nd.scale = (sw * sx * bn_scale).float().contiguous()
+        nd.scale_folded = False
+        nd.unit_mask, nd.zero_unit_frac = None, 0.0
+        nd.i8 = True
+        nd.x_val = nd.src if self.vcode.get(nd.src) == _lib.DRNMI_I8 else "q:" + nd.src
+        if nd.res:
+            nd.r_val = nd.res if self.vcode.get(nd.res) == _lib.DRNMI_I8 else "q:" + nd.res
+            nd.res_scale = float(self.act_scales[nd.res])
+        if self.vcode.get(nd.dst) == _lib.DRNMI_I8:
+            nd.out_scale = 1.0 / float(self.act_scales[nd.dst])
 
 
 # Below this fraction of all-zero 16 x 32 units the dense kernel is used: skipping costs scalar
@@ -237,6 +319,8 @@ def _unit_mask(wpk: torch.Tensor, code: int):
 
 
 def _uses_patch(nd: ConvNode, cin_stride: int, precision: str) -> bool:
+    if nd.i8:
+        return False
     c = nd.conv
     shape = (cin_stride, c.out_channels, c.kernel_size[0], c.stride[0], c.dilation[0])
     return precision == "bf16" and shape in PATCH_SHAPES and nd.res is None and not nd.out_fp32_nchw
@@ -286,31 +370,38 @@ class Plan:
         lh, lw = self.shapes["logits"]
         self.out_hw = (8 * lh, 8 * lw)
 
-        # Liveness-based buffer reuse (exact-size pool).
+        # Liveness-based buffer reuse (exact-size, per-dtype pool).  Launches read nd.x_val /
+        # nd.r_val (an int8 copy "q:<v>" of a bf16 value in int8 nets).
+        for nd in g.nodes:
+            if not nd.x_val:
+                nd.x_val, nd.r_val = nd.src, nd.res
         last_use = {}
         for i, nd in enumerate(g.nodes):
-            last_use[nd.src] = i
-            if nd.res:
-                last_use[nd.res] = i
+            last_use[nd.x_val] = i
+            if nd.r_val:
+                last_use[nd.r_val] = i
         self.bufs = {}
         pool = {}
-        esz = torch.tensor([], dtype=packed.tdtype).element_size()
         self.bufs["input"] = torch.empty(n * h * w * 8, dtype=packed.tdtype, device=dev)
+
+        def alloc(v, numel):
+            td = TORCH_OF_CODE[packed.value_code(v)]
+            lst = pool.get((numel, td))
+            self.bufs[v] = lst.pop() if lst else torch.empty(numel, dtype=td, device=dev)
+
         for i, nd in enumerate(g.nodes):
+            oh, ow = self.shapes[nd.dst]
             if nd.out_fp32_nchw:
-                oh, ow = self.shapes[nd.dst]
                 self.bufs[nd.dst] = torch.empty(n, nd.conv.out_channels, oh, ow, dtype=torch.float32, device=dev)
             else:
-                oh, ow = self.shapes[nd.dst]
-                numel = n * oh * ow * packed.cstride[nd.dst]
-                key = numel * esz
-                lst = pool.get(key)
-                self.bufs[nd.dst] = lst.pop() if lst else torch.empty(numel, dtype=packed.tdtype, device=dev)
+                alloc(nd.dst, n * oh * ow * packed.cstride[nd.dst])
+            for v in packed.quant_after.get(i, []):
+                alloc("q:" + v, n * oh * ow * packed.cstride[v])
             if not keep_all:
-                for v in {nd.src, nd.res} - {None, "input"}:
+                for v in {nd.x_val, nd.r_val} - {None, "input"}:
                     if last_use.get(v) == i and v in self.bufs and v != nd.dst:
                         t = self.bufs[v]
-                        pool.setdefault(t.numel() * esz, []).append(t)
+                        pool.setdefault((t.numel(), t.dtype), []).append(t)
         self.keep_all = keep_all
         self.args = [self._conv_args(nd) for nd in g.nodes]
         self.stem_u8 = self._stem_u8_args()
@@ -322,11 +413,11 @@ class Plan:
         ih, iw = self.shapes[nd.src]
         oh, ow = self.shapes[nd.dst]
         a = _lib.ConvArgs()
-        a.x = self.bufs[nd.src].data_ptr()
+        a.x = self.bufs[nd.x_val].data_ptr()
         a.wgt = nd.wpk.data_ptr()
         a.scale = None if nd.scale_folded else nd.scale.data_ptr()
         a.shift = nd.shift.data_ptr()
-        a.res = self.bufs[nd.res].data_ptr() if nd.res else None
+        a.res = self.bufs[nd.r_val].data_ptr() if nd.r_val else None
         a.y = self.bufs[nd.dst].data_ptr()
         cout = c.out_channels
         if nd.out_fp32_nchw:
@@ -337,7 +428,7 @@ class Plan:
             if nd.res and pk.cstride[nd.res] != cout:
                 raise NotImplementedError("residual channel stride must equal cout")
             a.y_sn, a.y_sp, a.y_sc = oh * ow * cs, cs, 1
-            a.out_dtype = pk.code
+            a.out_dtype = pk.value_code(nd.dst)
             if cs != cout:
                 raise NotImplementedError("activation channel padding beyond the stem input")
         a.n, a.h, a.w, a.cin = self.n, ih, iw, nd.cin_stride
@@ -345,9 +436,10 @@ class Plan:
         a.ks, a.stride, a.pad, a.dil = c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0]
         a.k, a.k_pad = nd.k, nd.k_pad
         a.relu = 1 if nd.relu else 0
-        a.dtype = pk.code
+        a.dtype = pk.value_code(nd.x_val)
         a.tile = -1
-        a.algo = _lib.ALGO_PATCH if _uses_patch(nd, nd.cin_stride, pk.precision) else _lib.ALGO_IGEMM
+        a.algo = _lib.ALGO_PATCH if _uses_patch(nd, nd.cin_stride, pk.base) else _lib.ALGO_IGEMM
+        a.res_scale, a.out_scale = nd.res_scale, nd.out_scale
         a.unit_mask = nd.unit_mask.data_ptr() if nd.unit_mask is not None else None
         return a
 
@@ -387,6 +479,15 @@ class Plan:
             _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), f"conv {nd.name}")
             if timing_hook is not None:
                 timing_hook(i, nd, False)
+            for v in self.packed.quant_after.get(i, ()):
+                self._quantize(lib, v, stream)
+
+    def _quantize(self, lib, v: str, stream: int):
+        """bf16 value -> its int8 copy "q:<v>" (include/drnmi.h drnmi_quantize_i8)."""
+        src, dst = self.bufs[v], self.bufs["q:" + v]
+        _lib.check(lib.drnmi_quantize_i8(src.data_ptr(), self.packed.value_code(v), dst.data_ptr(), dst.numel(),
+                                         1.0 / float(self.packed.act_scales[v]), ctypes.c_void_p(stream)),
+                   f"quantize_i8 {v}")
 
     def ingest_nchw(self, x: torch.Tensor, stream: int):
         self.src = "nchw"
@@ -433,13 +534,18 @@ class Plan:
             lab_dtype, n, c, lh, lw, ctypes.c_void_p(stream)), "up8_logsoftmax_argmax")
 
     def stage_nchw(self, value: str) -> torch.Tensor:
-        """fp32 NCHW copy of an intermediate activation (parity taps; keep_all plans)."""
+        """fp32 NCHW copy of an intermediate activation (parity taps; keep_all plans).  int8
+        values come back dequantised (q * scale) -- a test-side view, not a launch."""
         lib = _lib.load()
         c = self.packed.graph.channels[value]
         oh, ow = self.shapes[value]
+        if self.packed.value_code(value) == _lib.DRNMI_I8:
+            cs = self.packed.cstride[value]
+            q = self.bufs[value].view(self.n, oh, ow, cs)[..., :c]
+            return (q.float() * float(self.packed.act_scales[value])).permute(0, 3, 1, 2).contiguous()
         out = torch.empty(self.n, c, oh, ow, dtype=torch.float32, device=self.packed.device)
         _lib.check(lib.drnmi_nhwc_to_nchw(self.bufs[value].data_ptr(), out.data_ptr(), self.n, c, oh, ow,
-                                          self.packed.cstride[value], self.packed.code,
+                                          self.packed.cstride[value], self.packed.value_code(value),
                                           ctypes.c_void_p(_lib.stream_ptr())), "nhwc_to_nchw")
         return out
 

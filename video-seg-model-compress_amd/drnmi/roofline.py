@@ -11,15 +11,16 @@ f32-input MFMA 157.3 TFLOP/s.
 from __future__ import annotations
 
 HBM_PEAK_BPS = 8.0e12
-MFMA_PEAK = {"bf16": 2.5e15, "fp32": 157.3e12}
+MFMA_PEAK = {"bf16": 2.5e15, "fp32": 157.3e12, "int8": 5.0e15}   # int8: dense i8 MFMA = 2x bf16
 
 
 def node_work(plan):
     """[(name, flops, bytes)] for every conv node, plus the head (up+argmax)."""
     pk = plan.packed
-    esz = 2 if pk.precision == "bf16" else 4
+    base = 2 if pk.base == "bf16" else 4
     out = []
     for nd in pk.graph.nodes:
+        esz = 1 if nd.i8 else base          # int8 launches: int8 activations and weights
         c = nd.conv
         ih, iw = plan.shapes[nd.src]
         oh, ow = plan.shapes[nd.dst]
@@ -43,15 +44,21 @@ def node_work(plan):
     return out
 
 
+def node_peaks(plan):
+    """MFMA peak per row of node_work (int8 launches at the i8 rate)."""
+    pk = plan.packed
+    base = MFMA_PEAK[pk.base]
+    return [MFMA_PEAK["int8"] if nd.i8 else base for nd in pk.graph.nodes] + [base]
+
+
 def network_roofline(plan):
-    prec = plan.packed.precision
-    peak = MFMA_PEAK[prec]
     rows = node_work(plan)
-    t_star = sum(max(f / peak, b / HBM_PEAK_BPS) for _, f, b in rows)
+    peaks = node_peaks(plan)
+    t_star = sum(max(f / pk_, b / HBM_PEAK_BPS) for (_, f, b), pk_ in zip(rows, peaks))
     return {
         "flops": sum(f for _, f, _ in rows),
         "bytes": sum(b for _, _, b in rows),
         "t_star_s": t_star,
-        "t_mfma_s": sum(f for _, f, _ in rows) / peak,
+        "t_mfma_s": sum(f / pk_ for (_, f, _), pk_ in zip(rows, peaks)),
         "t_hbm_s": sum(b for _, _, b in rows) / HBM_PEAK_BPS,
     }
