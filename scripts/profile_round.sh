@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round profile set (GPU box): GPU test suite, kernel-trace stats of the default bench and of the
+# int8 bench, PMC HBM-traffic passes for both.  usage: bash scripts/profile_round.sh OUTNAME
+set -u
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$1
+mkdir -p $OUT
+timeout -k 10 500 python -u -m pytest $R/tests -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $OUT/pytest_gpu.log; tail -3 $OUT/pytest_gpu.log
+[ $rc -ne 0 ] && exit $rc
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_bf16 -o run --output-format csv -- \
+  python3 $R/bench.py --no-cpu-baseline > $OUT/bench_bf16_under_rocprof.log 2>&1) || { echo "trace bf16 failed"; exit 1; }
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_int8 -o run --output-format csv -- \
+  python3 $R/bench.py --no-cpu-baseline --precision int8 > $OUT/bench_int8_under_rocprof.log 2>&1) || { echo "trace int8 failed"; exit 1; }
+bash $R/scripts/pmc_traffic.sh $1/pmc_bf16 > /dev/null || exit 1
+bash $R/scripts/pmc_traffic.sh $1/pmc_int8 --precision int8 > /dev/null || exit 1
+echo done
