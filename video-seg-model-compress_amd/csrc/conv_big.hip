@@ -375,16 +375,21 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   // and B instructions [w*B_INSTR, ...) (pixels).
   const int lrow = lane / C::CPR;
   const int lslot = lane % C::CPR;
-  int a_src_off[C::A_INSTR];
-  int b_ih0[C::B_INSTR], b_iw0[C::B_INSTR];
-  const T* b_base[C::B_INSTR];
+  // weight rows: the swizzle of row (wave*A_INSTR + i)*RPI + lrow depends on i only through its
+  // parity, so two offsets + a scalar i*RPI*k_pad cover every piece
+  int a_par[2];
+  // pixel row i: (ih0, iw0) of tap (0,0) packed as two int16 (ih0 = -16384: no pixel) and the
+  // int32 element offset of that tap's chunk (only dereferenced when the tap is inside the
+  // image; big_conv_supported / i8_conv_supported bound n*h*w*cin < 2^31 and h, w < 16384)
+  uint32_t b_hw[C::B_INSTR];
+  int b_off[C::B_INSTR];
   const char* zero_src = reinterpret_cast<const char*>(g_zero_page) + lane * 16;
 
   auto setup = [&](int px0, int co0) {
 #pragma unroll
-    for (int i = 0; i < C::A_INSTR; ++i) {
+    for (int i = 0; i < 2; ++i) {
       const int r = (wave * C::A_INSTR + i) * C::RPI + lrow;
-      a_src_off[i] = (co0 + r) * p.k_pad + swzb<C::ROWB>(r, lslot) * CE;
+      a_par[i] = (co0 + r) * p.k_pad + swzb<C::ROWB>(r, lslot) * CE - i * C::RPI * p.k_pad;
     }
     // pixel rows: (ih0, iw0) of tap (0,0) and a base pointer at that tap's chunk (only
     // dereferenced when the tap lies inside the image)
@@ -392,17 +397,17 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
     for (int i = 0; i < C::B_INSTR; ++i) {
       const int r = (wave * C::B_INSTR + i) * C::RPI + lrow;
       const int m = px0 + r;
-      b_ih0[i] = -(1 << 28);
-      b_iw0[i] = -(1 << 28);
-      b_base[i] = x;
+      b_hw[i] = 0xC000C000u;
+      b_off[i] = 0;
       if (m < M) {
         const int n = m / hw_o;
         const int q = m - n * hw_o;
         const int oh = q / p.wo;
         const int ow = q - oh * p.wo;
-        b_ih0[i] = oh * p.stride - p.pad;
-        b_iw0[i] = ow * p.stride - p.pad;
-        b_base[i] = x + ((static_cast<int64_t>(n) * H + b_ih0[i]) * W + b_iw0[i]) * cin + swzb<C::ROWB>(r, lslot) * CE;
+        const int ih0 = oh * p.stride - p.pad;
+        const int iw0 = ow * p.stride - p.pad;
+        b_hw[i] = (static_cast<uint32_t>(ih0) << 16) | (static_cast<uint32_t>(iw0) & 0xffffu);
+        b_off[i] = ((n * H + ih0) * W + iw0) * cin + swzb<C::ROWB>(r, lslot) * CE;
       }
     }
   };
@@ -424,12 +429,14 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   auto issue_piece = [&](const StepP& sp, int stage, int i) {
     char* sa = smem + stage * C::STAGE;
     if (i < C::A_INSTR) {
-      glds16(wt + a_src_off[i] + sp.k0, sa + (wave * C::A_INSTR + i) * 1024);
+      glds16(wt + (a_par[i & 1] + i * C::RPI * p.k_pad + sp.k0), sa + (wave * C::A_INSTR + i) * 1024);
     } else {
       const int j = i - C::A_INSTR;
-      const bool ok = static_cast<unsigned>(b_ih0[j] + sp.dh) < static_cast<unsigned>(H) &&
-                      static_cast<unsigned>(b_iw0[j] + sp.dw) < static_cast<unsigned>(W);
-      const void* src = ok ? static_cast<const void*>(b_base[j] + sp.toff) : static_cast<const void*>(zero_src);
+      const int ih0 = static_cast<int>(b_hw[j]) >> 16;
+      const int iw0 = static_cast<int16_t>(b_hw[j] & 0xffffu);
+      const bool ok = static_cast<unsigned>(ih0 + sp.dh) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(iw0 + sp.dw) < static_cast<unsigned>(W);
+      const void* src = ok ? static_cast<const void*>(x + (b_off[j] + sp.toff)) : static_cast<const void*>(zero_src);
       glds16(src, sa + C::A_BYTES + (wave * C::B_INSTR + j) * 1024);
     }
   };
@@ -862,7 +869,11 @@ template <int KS, bool PERSIST>
 hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
   switch (base) {
     case 0: return launch_big<KS, 128, 1, 3, 64, PERSIST>(p, s);   // 128 x 256 tile, 4 waves, 3 x 48 KB
+#ifdef DRNMI_WIDE_TEST   // diagnostic builds only: 4 waves of 128 x 128
+    case 1: return launch_big<KS, 128, 2, 2, 64, PERSIST, 2>(p, s);
+#else
     case 1: return launch_big<KS, 128, 2, 2, 64, PERSIST>(p, s);   // 256 x 256 tile, 8 waves, 2 x 64 KB
+#endif
     case 2: return launch_big<KS, 64, 1, 4, 32, PERSIST>(p, s);    //  64 x 256 tile, 4 waves, 4 x 20 KB
     case 3: return launch_big<KS, 32, 1, 3, 64, PERSIST>(p, s);    //  32 x 256 tile, 4 waves, 3 x 36 KB
     case 4: return launch_big<KS, 128, 2, 4, 32, PERSIST>(p, s);   // 256 x 256 tile, 8 waves, 4 x 32 KB
@@ -918,9 +929,6 @@ hipError_t launch_i8_variant(const drnmi_conv_args& p, int v, hipStream_t s) {
   }
 }
 
-#ifdef DRNMI_WIDE_TEST
-template hipError_t launch_big<3, 128, 2, 2, 64, false, 2, false>(const drnmi_conv_args&, hipStream_t);
-#endif
 
 template <int KS>
 hipError_t launch_sparse(const drnmi_conv_args& p, int base, hipStream_t s) {
@@ -985,7 +993,7 @@ unit_mask_kernel(const T* __restrict__ w, int rows_pad, int k_pad, int wpr, uint
 bool i8_conv_supported(const drnmi_conv_args& p) {
   return p.dtype == DRNMI_I8 && p.scale != nullptr && p.cin >= 64 && (p.cin & (p.cin - 1)) == 0 &&
          p.cout_pad % 128 == 0 && (p.ks == 1 || p.ks == 3) && p.k == p.ks * p.ks * p.cin && p.k_pad == p.k &&
-         static_cast<int64_t>(p.n) * p.h * p.w * p.cin < (int64_t(1) << 31) &&
+         static_cast<int64_t>(p.n) * p.h * p.w * p.cin < (int64_t(1) << 31) && p.h < 16384 && p.w < 16384 &&
          (p.out_dtype == DRNMI_F32 || p.out_dtype == DRNMI_BF16 || p.out_dtype == DRNMI_I8);
 }
 
@@ -1004,7 +1012,8 @@ const char* i8_conv_name(const drnmi_conv_args& p) {
 }
 
 bool big_conv_supported(const drnmi_conv_args& p) {
-  return p.dtype == DRNMI_BF16 && p.cin >= kMinCin && (p.cin & (p.cin - 1)) == 0 && p.cout_pad % 128 == 0 &&
+  return static_cast<int64_t>(p.n) * p.h * p.w * p.cin < (int64_t(1) << 31) && p.h < 16384 && p.w < 16384 &&
+         p.dtype == DRNMI_BF16 && p.cin >= kMinCin && (p.cin & (p.cin - 1)) == 0 && p.cout_pad % 128 == 0 &&
          (p.ks == 1 || p.ks == 3) && p.k == p.ks * p.ks * p.cin && p.k_pad == p.k &&
          (p.out_dtype == DRNMI_F32 || (p.y_sc == 1 && p.y_sp == p.cout));
 }
