@@ -869,8 +869,10 @@ template <int KS, bool PERSIST>
 hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
   switch (base) {
     case 0: return launch_big<KS, 128, 1, 3, 64, PERSIST>(p, s);   // 128 x 256 tile, 4 waves, 3 x 48 KB
-#ifdef DRNMI_WIDE_TEST   // diagnostic builds only: 4 waves of 128 x 128
+#if defined(DRNMI_WIDE_TEST)   // diagnostic builds only: 4 waves of 128 x 128
     case 1: return launch_big<KS, 128, 2, 2, 64, PERSIST, 2>(p, s);
+#elif defined(DRNMI_W16_TEST)  // diagnostic builds only: 16 waves of 64 x 64
+    case 1: return launch_big<KS, 64, 4, 2, 64, PERSIST, 4>(p, s);
 #else
     case 1: return launch_big<KS, 128, 2, 2, 64, PERSIST>(p, s);   // 256 x 256 tile, 8 waves, 2 x 64 KB
 #endif
@@ -953,8 +955,12 @@ const char* sparse_name(int ks, int base) {
   return ks == 3 ? n3[base] : n1[base];
 }
 
+#ifndef DRNMI_AUTO_PERSIST
+#define DRNMI_AUTO_PERSIST 0
+#endif
 int auto_variant(const drnmi_conv_args& p) {
   if (p.cin < 64) return p.cout % 256 == 0 ? 4 : p.cout % 128 == 0 ? 5 : 2;   // K steps of 32
+  if (DRNMI_AUTO_PERSIST && p.cout % 256 == 0) return 7;
   return p.cout % 256 == 0 ? 1 : p.cout % 128 == 0 ? 0 : p.cout > 32 ? 2 : 3;
 }
 
