@@ -41,6 +41,13 @@
 #ifndef DRNMI_PFD
 #define DRNMI_PFD 1
 #endif
+// Pin the main-loop schedule: fragment reads for group q+PFD go out before group q's MFMAs
+// (sched_barrier between groups) and the next step's DMA pieces are issued without a branch
+// (the last steps re-fetch a clamped step into the idle stage).  Without the pins the compiler
+// sinks each read next to its MFMAs and waits lgkmcnt(0) on it (no LDS latency hiding).
+#ifndef DRNMI_PIN
+#define DRNMI_PIN 1
+#endif
 
 namespace drnmi {
 namespace {
@@ -496,8 +503,8 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         if (t + 1 < nk) live_next = live_bits(t + 1);
       }
       constexpr int PPG = (C::GLDS + C::GR - 1) / C::GR;   // DMA pieces per group (first substep)
-      const bool nxt = (DRNMI_ABLATE & 1) ? false : t + NST - 1 < nk;
-      const StepP sp = step_params(t + NST - 1);
+      const bool nxt = (DRNMI_ABLATE & 1) ? false : (DRNMI_PIN ? true : t + NST - 1 < nk);
+      const StepP sp = step_params(DRNMI_PIN ? (t + NST - 1 < nk ? t + NST - 1 : nk - 1) : t + NST - 1);
       const int nst = (t + NST - 1) % NST;
       constexpr int PFD = DRNMI_PFD;
       constexpr int NAF = PFD + 1;               // A-fragment ring depth
@@ -530,10 +537,15 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       }
 #pragma unroll
       for (int q = 0; q < NG; ++q) {
+        // group q's fragments (issued a group ago) land before the next reads go out, so the
+        // compiler's wait in front of the MFMAs does not also cover the fresh reads
+        // (s_waitcnt lgkmcnt(0) with vmcnt/expcnt at their maxima: LDS-DMA stays in flight)
+        if constexpr (DRNMI_PIN >= 2) __builtin_amdgcn_s_waitcnt(0xC07F);
         if (q + PFD < NG) {
           load_a(af[(q + PFD) % NAF], q + PFD);
           if ((q + PFD) % C::GR == 0) load_b(bfr[((q + PFD) / C::GR) & 1], (q + PFD) / C::GR);
         }
+        if constexpr (DRNMI_PIN) __builtin_amdgcn_sched_barrier(0);
         if constexpr ((DRNMI_ABLATE & 2) != 0) {
 #pragma unroll
           for (int h = 0; h < C::FPG; ++h)
@@ -554,6 +566,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
           for (int k = 0; k < PPG; ++k)
             if (q * PPG + k < C::GLDS) issue_piece(sp, nst, q * PPG + k);
         }
+        if constexpr (DRNMI_PIN) __builtin_amdgcn_sched_barrier(0);
       }
     }
 
@@ -567,7 +580,8 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         tile = xcd_remap2(tl, ntiles);
         px0 = (tile / nco) * kBPX;
         co0 = (tile % nco) * C::BCO;
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every wave done with the ring
+        // every wave done with the ring, and (DRNMI_PIN) the clamped re-fetches have landed
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         setup(px0, co0);
         for (int t = 0; t < NST - 1 && t < nk; ++t) issue(t, t);
