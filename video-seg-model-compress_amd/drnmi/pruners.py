@@ -105,20 +105,75 @@ class Pruner:
         hit = self._bits_cache.get(layer)
         if hit is not None and hit[0] == key:
             return hit[1]
-        flat = (m.detach().reshape(-1) != 0).cpu().numpy()
-        pad = (-flat.size) % 32
-        if pad:
-            flat = np.concatenate([flat, np.zeros(pad, dtype=bool)])
-        words = np.packbits(flat.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").astype(np.uint32).reshape(-1)
+        words = _pack_bits((m.detach().reshape(-1) != 0).cpu().numpy())
         bits = torch.from_numpy(words.view(np.int32).copy()).to(device)
         self._bits_cache[layer] = (key, bits)
         return bits
+
+    # -- compact on-disk masks (the reference never persists masks,
+    #    semantic_seg.py:1085-1092, so an SRMB run cannot be resumed with the same masks)
+    def save_masks(self, path):
+        """Write mask_dict as 1 bit per weight (the apply kernel's word layout) to an .npz.
+
+        Masks must be 0/1 valued (every reference pruner stores 0./1. floats); anything else
+        raises ValueError rather than being silently binarised."""
+        arrays = {"format": np.array([MASK_FORMAT_VERSION], dtype=np.int64),
+                  "layers": np.array(list(self.mask_dict), dtype=np.str_)}
+        for i, (layer, m) in enumerate(self.mask_dict.items()):
+            a = m.detach().cpu().numpy()
+            nz = a != 0
+            if not np.array_equal(a[nz], np.ones(int(nz.sum()), dtype=a.dtype)):
+                raise ValueError(f"{layer}: mask is not 0/1 valued; the bit format cannot hold it")
+            arrays[f"bits{i}"] = _pack_bits(nz.reshape(-1))
+            arrays[f"shape{i}"] = np.array(a.shape, dtype=np.int64)
+            arrays[f"dtype{i}"] = np.array([str(a.dtype)], dtype=np.str_)
+        with open(path, "wb") as f:
+            np.savez_compressed(f, **arrays)
+
+    def load_masks(self, path):
+        """Restore mask_dict from save_masks() output; seeds the bit cache so the next
+        apply_masks uploads no fp32 mask at all."""
+        with np.load(path, allow_pickle=False) as z:
+            if int(z["format"][0]) != MASK_FORMAT_VERSION:
+                raise ValueError(f"{path}: mask format {int(z['format'][0])} != {MASK_FORMAT_VERSION}")
+            self.mask_dict = collections.OrderedDict()
+            self._bits_cache = {}
+            for i, layer in enumerate(z["layers"].tolist()):
+                words, shape = z[f"bits{i}"], tuple(int(s) for s in z[f"shape{i}"])
+                n = int(np.prod(shape))
+                if words.dtype != np.uint32 or words.size != (n + 31) // 32:
+                    raise ValueError(f"{path}: {layer}: {words.size} words for {n} weights")
+                mask = _unpack_bits(words, n).reshape(shape).astype(str(z[f"dtype{i}"][0]))
+                self._store(layer, mask)
+                if self.on_gpu:
+                    m = self.mask_dict[layer]
+                    self._bits_cache[layer] = ((m.data_ptr(), m._version, str(m.device)),
+                                               torch.from_numpy(words.view(np.int32).copy()).to(m.device))
+        return self
 
     def print_stats(self):
         for layer in self.mask_dict:
             mask_np = self.mask_dict[layer].cpu().numpy()
             sp = 1.0 - np.count_nonzero(mask_np) / mask_np.size
             print(layer, "sparsity = {}".format(sp * 100))
+
+
+MASK_FORMAT_VERSION = 1
+
+
+def _pack_bits(flat: np.ndarray) -> np.ndarray:
+    """bool[n] -> uint32[ceil(n/32)], weight i is bit (i % 32) of word i // 32 (LSB first) —
+    the layout drnmi_mask_apply_bits_f32 reads."""
+    flat = np.asarray(flat, dtype=bool)
+    pad = (-flat.size) % 32
+    if pad:
+        flat = np.concatenate([flat, np.zeros(pad, dtype=bool)])
+    return np.packbits(flat.reshape(-1, 32), axis=1, bitorder="little").view("<u4").astype(np.uint32).reshape(-1)
+
+
+def _unpack_bits(words: np.ndarray, n: int) -> np.ndarray:
+    b = np.unpackbits(np.ascontiguousarray(words, dtype="<u4").view(np.uint8), bitorder="little")
+    return b[:n].astype(bool)
 
 
 def _resolve_tensors(model, layers):
