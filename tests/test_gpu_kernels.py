@@ -147,8 +147,8 @@ def test_up8_logsoftmax_argmax(h, w):
     assert torch.equal(lab8.cpu().long(), lab.cpu())
 
 
-@pytest.mark.parametrize("use_bits", [False, True])
-def test_mask_apply_bit_exact(use_bits, tmp_path):
+@pytest.mark.parametrize("use_bits,from_disk", [(False, False), (True, False), (True, True)])
+def test_mask_apply_bit_exact(use_bits, from_disk, tmp_path):
     """Pruner.apply_masks through the HIP kernel == w * m on the CPU, bit for bit (incl. -0.0)."""
     import json
     from drnmi import pruners as P
@@ -163,6 +163,10 @@ def test_mask_apply_bit_exact(use_bits, tmp_path):
     jp.write_text(json.dumps(cfg))
     pr = P.BlockPruner(str(jp), on_gpu=True)
     pr.generate_masks(m)
+    if from_disk:   # 1-bit on-disk masks: load seeds the bit cache the kernel reads directly
+        pr.save_masks(tmp_path / "m.npz")
+        pr = P.BlockPruner(str(jp), on_gpu=True).load_masks(tmp_path / "m.npz")
+        assert set(pr._bits_cache) == set(layers)
     before = {k: v.clone() for k, v in m.state_dict().items()}
     ref = O.apply_masks({k: before[k] for k in layers}, {k: pr.mask_dict[k].cpu() for k in layers})
     m = m.to(DEV)
