@@ -45,6 +45,10 @@
 // (sched_barrier between groups) and the next step's DMA pieces are issued without a branch
 // (the last steps re-fetch a clamped step into the idle stage).  Without the pins the compiler
 // sinks each read next to its MFMAs and waits lgkmcnt(0) on it (no LDS latency hiding).
+#ifndef DRNMI_PRIO
+#define DRNMI_PRIO 0   // diagnostic: 1 raises wave priority across each MFMA group, 2 across
+                       // each group's fragment reads and DMA issue (both measured slower)
+#endif
 #ifndef DRNMI_PIN
 #define DRNMI_PIN 1
 #endif
@@ -541,11 +545,14 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         // compiler's wait in front of the MFMAs does not also cover the fresh reads
         // (s_waitcnt lgkmcnt(0) with vmcnt/expcnt at their maxima: LDS-DMA stays in flight)
         if constexpr (DRNMI_PIN >= 2) __builtin_amdgcn_s_waitcnt(0xC07F);
+        if constexpr (DRNMI_PRIO == 2) if (q == 0) __builtin_amdgcn_s_setprio(1);
         if (q + PFD < NG) {
           load_a(af[(q + PFD) % NAF], q + PFD);
           if ((q + PFD) % C::GR == 0) load_b(bfr[((q + PFD) / C::GR) & 1], (q + PFD) / C::GR);
         }
         if constexpr (DRNMI_PIN) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (DRNMI_PRIO == 1) { __builtin_amdgcn_s_setprio(1); __builtin_amdgcn_sched_barrier(0); }
+        if constexpr (DRNMI_PRIO == 2) { __builtin_amdgcn_s_setprio(0); __builtin_amdgcn_sched_barrier(0); }
         if constexpr ((DRNMI_ABLATE & 2) != 0) {
 #pragma unroll
           for (int h = 0; h < C::FPG; ++h)
@@ -561,6 +568,8 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
                 af[q % NAF][h], bfr[(q / C::GR) & 1][fn], acc[(q % C::GR) * C::FPG + h][fn]);
         }
         }
+        if constexpr (DRNMI_PRIO == 1) { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_setprio(0); }
+        if constexpr (DRNMI_PRIO == 2) { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_setprio(1); }
         if (q < C::GR && nxt) {
 #pragma unroll
           for (int k = 0; k < PPG; ++k)
