@@ -984,7 +984,9 @@ const char* sparse_name(int ks, int base) {
 int auto_variant(const drnmi_conv_args& p) {
   if (p.cin < 64) return p.cout % 256 == 0 ? 4 : p.cout % 128 == 0 ? 5 : 2;   // K steps of 32
   if (DRNMI_AUTO_PERSIST && p.cout % 256 == 0) return 7;
-  return p.cout % 256 == 0 ? 1 : p.cout % 128 == 0 ? 0 : p.cout > 32 ? 2 : 3;
+  // cout <= 32 (the seg 1x1) also takes the 64-wide BK-32 tile: 57 vs 66 us on the D-22 seg conv
+  // at batch 8 (scripts/conv_micro.py) — two workgroups fit per CU where the 32-wide 3 x 36 KB ring fits one
+  return p.cout % 256 == 0 ? 1 : p.cout % 128 == 0 ? 0 : 2;
 }
 
 // one lane per 16 x 32 unit; lanes 0-31 / 32-63 of a wave cover the 32 units of two mask words
