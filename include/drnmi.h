@@ -157,6 +157,14 @@ int drnmi_up8_logsoftmax_argmax(const float* logits, const float* up_w, float* l
                                 void* labels, int32_t label_dtype, int32_t n, int32_t c,
                                 int32_t h, int32_t w, void* stream);
 
+/* Same head for DRNSeg(use_torch_up=True): nn.UpsamplingBilinear2d(scale_factor=8) (bilinear,
+ * align_corners=True; lmodels/drnseg.py:285-287) + LogSoftmax + argmax.  Source index and
+ * weights follow ATen's CPU kernel: scale = (in-1)/(out-1) in fp32, i0 = floor(scale*dst),
+ * i1 = i0 + (i0 < in-1), l1 = scale*dst - i0.  Output [n][c][8h][8w]. */
+int drnmi_up8_bilinear_logsoftmax_argmax(const float* logits, float* logprobs, void* labels,
+                                         int32_t label_dtype, int32_t n, int32_t c, int32_t h, int32_t w,
+                                         void* stream);
+
 /* Multi-tensor in-place mask apply: w[t][i] *= m[t][i] for every tensor t.
  * Replaces Pruner.apply_masks (pruners/Pruner.py:17-20, same body BlockPruner.py:27-30,
  * SRMBRepMasker.py:20-23): one launch for all masked layers instead of one ATen mul_ per
@@ -249,12 +257,18 @@ int drnmi_zero_insert_f32(const float* dy, int32_t n, int32_t ho, int32_t wo, in
                           int32_t hu, int32_t wu, float* out, void* stream);
 
 /* Head backward: du = grad_scale * (g_lp - exp(lp) * sum_c g_lp) (LogSoftmax, dim 1), then
- * dlogits = up^T(du) [+ g_logits] — the transpose of the fixed bilinear ConvTranspose2d(k16,
+ * dlogits = up^T(du) [+ grad_scale * g_logits] — the transpose of the fixed bilinear ConvTranspose2d(k16,
  * s8, p4) (lmodels/drnseg.py:285-299).  g_logprobs/logprobs/du_ws: NCHW [n][c][8h][8w];
  * dlogits/g_logits: [n][c][h][w]; g_logprobs NULL = logits-only gradient. */
 int drnmi_up8_lsm_bwd_f32(const float* g_logprobs, const float* logprobs, const float* g_logits,
                           const float* up_w, float grad_scale, int32_t n, int32_t c, int32_t h,
                           int32_t w, float* du_ws, float* dlogits, void* stream);
+
+/* Head backward of the use_torch_up head (bilinear align_corners=True x8): du as above, then
+ * dlogits = bilinear^T(du) [+ grad_scale * g_logits] (a fixed-order gather, no atomics). */
+int drnmi_up8_bilinear_lsm_bwd_f32(const float* g_logprobs, const float* logprobs, const float* g_logits,
+                                   float grad_scale, int32_t n, int32_t c, int32_t h, int32_t w, float* du_ws,
+                                   float* dlogits, void* stream);
 
 /* CrossEntropyLoss(ignore_index) applied to log-probs [n][c][hw] with int64 targets [n][hw]:
  * loss[0] = mean over target != ignore of (logsumexp(lp) - lp[target]) (NaN if a target is out

@@ -137,7 +137,12 @@ def backbone(sd, arch, x, prefix="layer"):
 
 def up_logsoftmax(sd, logits):
     """up = depthwise ConvTranspose2d(C, C, 16, stride 8, pad 4) + LogSoftmax(dim 1)
-    (lmodels/drnseg.py:285-299)."""
+    (lmodels/drnseg.py:285-299).  Without "up.weight" in sd (DRNSeg(use_torch_up=True)): up =
+    nn.UpsamplingBilinear2d(scale_factor=8) (lmodels/drnseg.py:285-287), i.e. bilinear with
+    align_corners=True."""
+    if "up.weight" not in sd:
+        y = F.interpolate(logits, scale_factor=8, mode="bilinear", align_corners=True)
+        return F.log_softmax(y, dim=1)
     c = logits.shape[1]
     y = F.conv_transpose2d(logits, sd["up.weight"], None, stride=8, padding=4, groups=c)
     return F.log_softmax(y, dim=1)
@@ -145,7 +150,8 @@ def up_logsoftmax(sd, logits):
 
 @torch.no_grad()
 def drnseg_forward(sd, arch, x):
-    """(log_probs, logits, stages) of DRNSeg.forward for a state_dict (keys layer.*/seg.*/up.*)."""
+    """(log_probs, logits, stages) of DRNSeg.forward for a state_dict (keys layer.*/seg.*/up.*;
+    no up.weight = the use_torch_up head)."""
     sd = {k: v.float() for k, v in sd.items()}
     feat, stages = backbone(sd, arch, x.float())
     logits = _conv(sd, "seg", feat, bias=True)

@@ -35,10 +35,17 @@ def _fresh_model():
     return m.cuda().train()
 
 
-def _local_grads(x, t):
+def _loss(out, t):
+    """CE on the log-probs plus a term on the logits output (model(x)[1]): DDP must average
+    the gradient reaching the network through either output."""
     from drnmi.train import CrossEntropyLoss
+    lp, logits = out
+    return CrossEntropyLoss(ignore_index=255)(lp, t.cuda()) + 1e-3 * (logits * logits).mean()
+
+
+def _local_grads(x, t):
     m = _fresh_model()
-    loss = CrossEntropyLoss(ignore_index=255)(m(x.cuda())[0], t.cuda())
+    loss = _loss(m(x.cuda()), t)
     loss.backward()
     return {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters() if p.grad is not None}
 
@@ -51,12 +58,12 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from drnmi.parallel import DistributedDataParallel
-        from drnmi.train import SGD, CrossEntropyLoss
+        from drnmi.train import SGD
         m = _fresh_model()
         ddp = DistributedDataParallel(m, device_ids=[0], bucket_cap_mb=8)
         opt = SGD(ddp.optim_parameters(), 0.001, momentum=0.9, weight_decay=1e-4)
         x, t = _inputs(rank)
-        loss = CrossEntropyLoss(ignore_index=255)(ddp(x.cuda())[0], t.cuda())
+        loss = _loss(ddp(x.cuda()), t)
         opt.zero_grad()
         loss.backward()
         grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters() if p.grad is not None}

@@ -1,10 +1,11 @@
 """Whole-network parity: drnmi.DRNSeg (HIP engine) vs the reference goldens and the oracle.
 
 north_star gate (fp32 parity mode): logits within 1e-3 max-abs of the reference PyTorch-CPU
-forward; argmax label maps identical.  Label identity is asserted on every pixel whose
-reference top-2 log-prob margin exceeds 1e-4 (below that an fp32 reordering of the same
-sums can legitimately swap the order); the number of pixels under that margin is reported.
-bf16 perf mode: gated by argmax agreement and a relative logit error bound.
+forward; argmax label maps identical on EVERY pixel of the golden cases (measured: no pixel
+differs; the pixels whose reference top-2 log-prob margin is <= 1e-4, where an fp32
+reordering of the same sums could legitimately swap the order, are counted and reported).
+bf16 perf mode: argmax agreement >= 0.98 and relative logit error <= 0.03 (measured
+0.989-0.993 and ~1.2e-2 in round 1).
 """
 import numpy as np
 import pytest
@@ -45,9 +46,9 @@ def test_fp32_forward_matches_reference(case, golden_forward):
     ref_lab = golden_forward[case + "/labels"]
     margin = golden_forward[case + "/top2_margin"]
     diff = labels != ref_lab
-    assert not np.any(diff & (margin > 1e-4)), f"{int(diff.sum())} label mismatches"
     print(f"{case}: logit max-abs {err:.2e}, labels differ {int(diff.sum())} px "
           f"({int((margin <= 1e-4).sum())} px with margin <= 1e-4)")
+    assert int(diff.sum()) == 0, f"{int(diff.sum())} label mismatches"
 
 
 @pytest.mark.parametrize("case", ["d22_2x128x256", "d54_1x64x128"])
@@ -90,8 +91,8 @@ def test_bf16_forward_agreement(case, golden_forward):
     labels = torch.max(lp, 1)[1].cpu().numpy()
     agree = (labels == golden_forward[case + "/labels"]).mean()
     print(f"{case} bf16: logit rel err {rel:.3e}, argmax agreement {agree:.4f}")
-    assert rel <= 0.15
-    assert agree >= 0.90
+    assert rel <= 0.03
+    assert agree >= 0.98
 
 
 def test_weights_repack_after_mask_apply(golden_forward, tmp_path):
@@ -129,4 +130,4 @@ def test_bf16_segment_matches_bf16_forward_labels(golden_forward):
     ref = torch.from_numpy(golden_forward[case + "/labels"]).long().to(DEV)
     agree_ref = (lab_seg == ref).float().mean().item()
     print(f"bf16 segment vs predict agreement {agree:.4f}, vs reference {agree_ref:.4f}")
-    assert agree >= 0.98 and agree_ref >= 0.95
+    assert agree >= 0.98 and agree_ref >= 0.98

@@ -245,6 +245,73 @@ up8_lsm_quad_kernel(const float* __restrict__ logits, const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- bilinear x8 (use_torch_up)
+// nn.UpsamplingBilinear2d(scale_factor=8) (lmodels/drnseg.py:285-287): bilinear with
+// align_corners=True, output 8h x 8w.  Source index and weights as ATen's CPU kernel:
+// scale = (in - 1) / (out - 1) in fp32, src = scale * dst, i0 = floor(src), i1 = i0 + (i0 < in-1),
+// l1 = src - i0, l0 = 1 - l1; value = l0h * (l0w * x00 + l1w * x01) + l1h * (l0w * x10 + l1w * x11).
+__device__ __forceinline__ void bilinear_ac_index(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  const float scale = out > 1 ? static_cast<float>(in - 1) / static_cast<float>(out - 1) : 0.f;
+  const float src = scale * static_cast<float>(dst);
+  i0 = static_cast<int>(floorf(src));
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = fminf(fmaxf(src - static_cast<float>(i0), 0.f), 1.f);
+  l0 = 1.f - l1;
+}
+
+template <int LABEL_DTYPE>
+__global__ void __launch_bounds__(256)
+up8_bilinear_lsm_kernel(const float* __restrict__ logits, float* __restrict__ logprobs, void* __restrict__ labels,
+                        int c, int h, int w) {
+  const int H = h * 8, W = w * 8;
+  const int ox = blockIdx.x * blockDim.x + threadIdx.x;
+  const int oy = blockIdx.y;
+  const int n = blockIdx.z;
+  if (ox >= W) return;
+  int y0, y1, x0, x1;
+  float hy0, hy1, wx0, wx1;
+  bilinear_ac_index(oy, h, H, y0, y1, hy0, hy1);
+  bilinear_ac_index(ox, w, W, x0, x1, wx0, wx1);
+  const int64_t plane = static_cast<int64_t>(h) * w;
+  const float* src = logits + static_cast<int64_t>(n) * c * plane;
+  float v[kMaxClasses];
+  float vmax = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < kMaxClasses; ++k) {
+    if (k < c) {
+      const float* s = src + k * plane;
+      const float top = wx0 * s[y0 * w + x0] + wx1 * s[y0 * w + x1];
+      const float bot = wx0 * s[y1 * w + x0] + wx1 * s[y1 * w + x1];
+      const float a = hy0 * top + hy1 * bot;
+      v[k] = a;
+      vmax = fmaxf(vmax, a);
+    }
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxClasses; ++k) {
+    if (k < c) sum += expf(v[k] - vmax);
+  }
+  const float lse = logf(sum);
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int64_t pix = static_cast<int64_t>(oy) * W + ox;
+  float best = -INFINITY;
+  int arg = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxClasses; ++k) {
+    if (k < c) {
+      const float lp = (v[k] - vmax) - lse;
+      if (logprobs != nullptr) logprobs[(static_cast<int64_t>(n) * c + k) * HW + pix] = lp;
+      if (lp > best) { best = lp; arg = k; }
+    }
+  }
+  if (labels != nullptr) {
+    if (LABEL_DTYPE == DRNMI_U8) reinterpret_cast<uint8_t*>(labels)[static_cast<int64_t>(n) * HW + pix] = static_cast<uint8_t>(arg);
+    else reinterpret_cast<int64_t*>(labels)[static_cast<int64_t>(n) * HW + pix] = arg;
+  }
+}
+
 // ---------------------------------------------------------------- mask apply
 constexpr int kMaskBatch = 32;
 
@@ -421,6 +488,23 @@ extern "C" int drnmi_up8_logsoftmax_argmax(const float* logits, const float* up_
   } else {
     hipLaunchKernelGGL(up8_lsm_kernel<DRNMI_U8>, grid, dim3(256), 0, s, logits, up_w, logprobs, labels, c, h, w);
   }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_up8_bilinear_logsoftmax_argmax(const float* logits, float* logprobs, void* labels,
+                                                    int32_t label_dtype, int32_t n, int32_t c, int32_t h, int32_t w,
+                                                    void* stream) {
+  if (logits == nullptr || n <= 0 || h <= 0 || w <= 0) return DRNMI_EINVAL;
+  if (c <= 0 || c > kMaxClasses) return DRNMI_ENOTSUP;
+  if (labels != nullptr && label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64) return DRNMI_EINVAL;
+  if (static_cast<int64_t>(h) * 8 > 65535 || n > 65535) return DRNMI_EINVAL;
+  const int W = w * 8;
+  dim3 grid(static_cast<unsigned>((W + 255) / 256), static_cast<unsigned>(h * 8), static_cast<unsigned>(n));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (label_dtype == DRNMI_I64)
+    hipLaunchKernelGGL(up8_bilinear_lsm_kernel<DRNMI_I64>, grid, dim3(256), 0, s, logits, logprobs, labels, c, h, w);
+  else
+    hipLaunchKernelGGL(up8_bilinear_lsm_kernel<DRNMI_U8>, grid, dim3(256), 0, s, logits, logprobs, labels, c, h, w);
   return static_cast<int>(hipGetLastError());
 }
 

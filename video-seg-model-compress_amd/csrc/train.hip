@@ -504,11 +504,12 @@ lsm_bwd_kernel(const float* __restrict__ g, const float* __restrict__ lp, int ni
   }
 }
 
-// dlogits[n][c][i][j] = sum_{ky,kx} W[ky][kx] * du[n][c][8i-4+ky][8j-4+kx] (+ g_logits); the
-// transpose of ConvTranspose2d(k16, s8, p4) (lmodels/drnseg.py:285-293).
+// dlogits[n][c][i][j] = sum_{ky,kx} W[ky][kx] * du[n][c][8i-4+ky][8j-4+kx] (+ gscale * g_logits); the
+// transpose of ConvTranspose2d(k16, s8, p4) (lmodels/drnseg.py:285-293).  du == NULL: logits-only
+// gradient (no log-prob term).
 __global__ void __launch_bounds__(kThreads)
 up8_bwd_kernel(const float* __restrict__ du, const float* __restrict__ upw, const float* __restrict__ glog,
-               int nc, int h, int w, float* __restrict__ dlog) {
+               float gscale, int nc, int h, int w, float* __restrict__ dlog) {
   __shared__ float wk[256];
   wk[threadIdx.x] = upw[threadIdx.x];
   __syncthreads();
@@ -521,7 +522,7 @@ up8_bwd_kernel(const float* __restrict__ du, const float* __restrict__ upw, cons
     const int64_t plane = i / (static_cast<int64_t>(w) * h);
     const float* src = du + plane * H * W;
     float s = 0.f;
-    for (int ky = 0; ky < 16; ++ky) {
+    for (int ky = 0; ky < 16 && du != nullptr; ++ky) {
       const int y = 8 * ii - 4 + ky;
       if (static_cast<unsigned>(y) >= static_cast<unsigned>(H)) continue;
       const float* row = src + static_cast<int64_t>(y) * W;
@@ -530,7 +531,67 @@ up8_bwd_kernel(const float* __restrict__ du, const float* __restrict__ upw, cons
         if (static_cast<unsigned>(x) < static_cast<unsigned>(W)) s += wk[ky * 16 + kx] * row[x];
       }
     }
-    if (glog != nullptr) s += glog[i];
+    if (glog != nullptr) s += gscale * glog[i];   // the logits output's gradient, DDP-averaged like du
+    dlog[i] = s;
+  }
+}
+
+// Transpose of nn.UpsamplingBilinear2d(scale_factor=8) (align_corners=True, lmodels/drnseg.py:
+// 285-287): dlogits[i][j] = sum_{oy,ox} wy(oy, i) * wx(ox, j) * du[oy][ox] (+ gscale * g_logits),
+// gathered (no atomics, fixed order).  Output row oy touches input rows i0(oy) and i1(oy) with
+// i0 non-decreasing in oy, so input row i gathers from the oy window whose i0 is i-1 or i; the
+// window is found with the forward's own index arithmetic.
+__device__ __forceinline__ void bil_ac(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  const float scale = out > 1 ? static_cast<float>(in - 1) / static_cast<float>(out - 1) : 0.f;
+  const float src = scale * static_cast<float>(dst);
+  i0 = static_cast<int>(floorf(src));
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = fminf(fmaxf(src - static_cast<float>(i0), 0.f), 1.f);
+  l0 = 1.f - l1;
+}
+
+__device__ __forceinline__ float bil_weight(int o, int i, int in, int out) {
+  int i0, i1;
+  float l0, l1;
+  bil_ac(o, in, out, i0, i1, l0, l1);
+  return (i0 == i ? l0 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
+__global__ void __launch_bounds__(kThreads)
+up8_bilinear_bwd_kernel(const float* __restrict__ du, const float* __restrict__ glog, float gscale, int nc, int h,
+                        int w, float* __restrict__ dlog) {
+  const int H = 8 * h, W = 8 * w;
+  const int64_t total = static_cast<int64_t>(nc) * h * w;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int j = static_cast<int>(i % w);
+    const int ii = static_cast<int>((i / w) % h);
+    const int64_t plane = i / (static_cast<int64_t>(w) * h);
+    float s = 0.f;
+    if (du != nullptr) {
+      const float* src = du + plane * H * W;
+      // candidate windows: o with i0(o) in {i-1, i}, i.e. o*(in-1)/(out-1) in [i-1, i+1), +-2 for
+      // rounding; bil_weight() then applies the forward's exact index test
+      const float ry = h > 1 ? static_cast<float>(H - 1) / static_cast<float>(h - 1) : static_cast<float>(H);
+      const float rx = w > 1 ? static_cast<float>(W - 1) / static_cast<float>(w - 1) : static_cast<float>(W);
+      const int oy_lo = max(0, static_cast<int>(floorf((ii - 1) * ry)) - 2);
+      const int oy_hi = min(H - 1, static_cast<int>(ceilf((ii + 1) * ry)) + 2);
+      const int ox_lo = max(0, static_cast<int>(floorf((j - 1) * rx)) - 2);
+      const int ox_hi = min(W - 1, static_cast<int>(ceilf((j + 1) * rx)) + 2);
+      for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+        const float wy = bil_weight(oy, ii, h, H);
+        if (wy == 0.f) continue;
+        const float* row = src + static_cast<int64_t>(oy) * W;
+        float r = 0.f;
+        for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+          const float wx = bil_weight(ox, j, w, W);
+          if (wx != 0.f) r += wx * row[ox];
+        }
+        s += wy * r;
+      }
+    }
+    if (glog != nullptr) s += gscale * glog[i];
     dlog[i] = s;
   }
 }
@@ -845,13 +906,32 @@ extern "C" int drnmi_up8_lsm_bwd_f32(const float* g_logprobs, const float* logpr
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);
     hipLaunchKernelGGL(up8_bwd_kernel, dim3(grid_of(static_cast<int64_t>(n) * c * h * w)), dim3(kThreads), 0, s,
-                       du_ws, up_w, g_logits, n * c, h, w, dlogits);
+                       du_ws, up_w, g_logits, grad_scale, n * c, h, w, dlogits);
   } else {
-    // logits-only gradient: dlogits = g_logits (through the same kernel with du = 0 rows skipped)
+    // logits-only gradient: dlogits = grad_scale * g_logits
     if (g_logits == nullptr) return DRNMI_EINVAL;
-    return static_cast<int>(hipMemcpyAsync(dlogits, g_logits, static_cast<size_t>(n) * c * h * w * 4,
-                                           hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(up8_bwd_kernel, dim3(grid_of(static_cast<int64_t>(n) * c * h * w)), dim3(kThreads), 0, s,
+                       nullptr, up_w, g_logits, grad_scale, n * c, h, w, dlogits);
   }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_up8_bilinear_lsm_bwd_f32(const float* g_logprobs, const float* logprobs, const float* g_logits,
+                                              float grad_scale, int32_t n, int32_t c, int32_t h, int32_t w,
+                                              float* du_ws, float* dlogits, void* stream) {
+  if (dlogits == nullptr || n <= 0 || c <= 0 || h <= 0 || w <= 0) return DRNMI_EINVAL;
+  if (g_logprobs != nullptr && (logprobs == nullptr || du_ws == nullptr)) return DRNMI_EINVAL;
+  if (g_logprobs == nullptr && g_logits == nullptr) return DRNMI_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t hw = static_cast<int64_t>(64) * h * w;
+  if (g_logprobs != nullptr) {
+    hipLaunchKernelGGL(lsm_bwd_kernel, dim3(grid_of(n * hw)), dim3(kThreads), 0, s, g_logprobs, logprobs, n, c, hw,
+                       grad_scale, du_ws);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return static_cast<int>(e);
+  }
+  hipLaunchKernelGGL(up8_bilinear_bwd_kernel, dim3(grid_of(static_cast<int64_t>(n) * c * h * w)), dim3(kThreads), 0, s,
+                     g_logprobs != nullptr ? du_ws : nullptr, g_logits, grad_scale, n * c, h, w, dlogits);
   return static_cast<int>(hipGetLastError());
 }
 

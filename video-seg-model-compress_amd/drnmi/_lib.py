@@ -71,6 +71,7 @@ SIGNATURES = {
     "drnmi_nchw_to_nhwc": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_nhwc_to_nchw": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_up8_logsoftmax_argmax": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
+    "drnmi_up8_bilinear_logsoftmax_argmax": (ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_mask_apply_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP]),
     "drnmi_mask_apply_bits_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP]),
     "drnmi_confusion_matrix": (ctypes.c_int, [_VP, _I32, _VP, _I32, _I64, _I32, _VP, _VP]),
@@ -85,6 +86,7 @@ SIGNATURES = {
     "drnmi_conv_wgrad_f32": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
     "drnmi_zero_insert_f32": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     "drnmi_up8_lsm_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _F32, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
+    "drnmi_up8_bilinear_lsm_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _F32, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
     "drnmi_ce_workspace_bytes": (ctypes.c_int64, []),
     "drnmi_ce_loss_f32": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I64, _I64, _VP, _VP, _VP, _VP]),
     "drnmi_ce_loss_bwd_f32": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I64, _I64, _VP, _VP, _VP, _VP]),

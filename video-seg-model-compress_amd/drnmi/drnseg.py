@@ -9,9 +9,13 @@ Reference API (kept): semantic_seg.py:126-164 / lmodels/drnseg.py:268-305
                        log.txt:18-170, and a DataParallel/DDP "module." prefix)
 
 Differences by design:
-  * forward runs the fused HIP plan (drnmi.engine) on a ROCm device.  It never falls
-    back to ATen; on CPU it raises.  In train mode it runs the fine-tune path
+  * forward runs the fused HIP plan (drnmi.engine) on a ROCm device, as the registered
+    custom op torch.ops.drnmi.forward (drnmi.torch_ops; also .predict / .segment).  It never
+    falls back to ATen; on CPU it raises.  In train mode it runs the fine-tune path
     (drnmi.train: batch-stat BN, autograd through the HIP backward kernels, fp32).
+  * use_torch_up=True keeps the reference's nn.UpsamplingBilinear2d(scale_factor=8) head
+    (lmodels/drnseg.py:285-287: bilinear, align_corners=True, output 8h x 8w) on its own
+    fused HIP kernel (drnmi_up8_bilinear_logsoftmax_argmax).
   * precision: "fp32" (default; the reference's arithmetic, parity mode, exact-fp32
     MFMA), "bf16" (perf mode, fp32 accumulation) or "int8" (W8A8 for the cin >= 64 convs,
     config C5; needs calibrate_int8() first — the reference has no quantisation, so this
@@ -31,7 +35,7 @@ import os
 import torch
 import torch.nn as nn
 
-from . import _lib, drn
+from . import _lib, drn, torch_ops
 from .engine import PackedNet, Plan, lower_drnseg
 from .weights import bilinear_up_kernel
 
@@ -52,10 +56,6 @@ class DRNSeg(nn.Module):
     def __init__(self, model_name, classes, pretrained_model=None, pretrained=True,
                  use_torch_up=False):
         super().__init__()
-        if use_torch_up:
-            raise NotImplementedError(
-                "use_torch_up=True (nn.UpsamplingBilinear2d) is not on the north-star path; "
-                "the fused kernel implements the ConvTranspose2d 'up' (lmodels/drnseg.py:288-293)")
         factory = getattr(drn, model_name, None)
         if factory is None:
             raise KeyError(f"unknown model {model_name!r}; known: {drn.ARCHS}")
@@ -68,11 +68,15 @@ class DRNSeg(nn.Module):
         n = self.seg.kernel_size[0] * self.seg.kernel_size[1] * self.seg.out_channels
         self.seg.weight.data.normal_(0, math.sqrt(2.0 / n))
         self.seg.bias.data.zero_()
-        up = nn.ConvTranspose2d(classes, classes, 16, stride=8, padding=4, output_padding=0,
-                                groups=classes, bias=False)
-        fill_up_weights(up)
-        up.weight.requires_grad = False
-        self.up = up
+        if use_torch_up:
+            self.up = nn.UpsamplingBilinear2d(scale_factor=8)
+        else:
+            up = nn.ConvTranspose2d(classes, classes, 16, stride=8, padding=4, output_padding=0,
+                                    groups=classes, bias=False)
+            fill_up_weights(up)
+            up.weight.requires_grad = False
+            self.up = up
+        self.use_torch_up = bool(use_torch_up)
         self.model_name = model_name
         self.classes = classes
         self.precision = "fp32"
@@ -82,6 +86,9 @@ class DRNSeg(nn.Module):
         self._packed = {}
         self._plans = {}
         self._pack_key = None
+        self._key_tensors = None     # cached parameter/buffer list of the repack key
+        self.timing_hook = None      # optional per-launch callback (bench.py's HIP events)
+        self._handle = torch_ops.register_model(self)   # torch.ops.drnmi.* state handle
 
     # ----------------------------------------------------------------- reference API
     def optim_parameters(self, memo=None):
@@ -99,46 +106,81 @@ class DRNSeg(nn.Module):
                 raise NotImplementedError("the fine-tune path runs in fp32 (the reference's arithmetic)")
             from .train import train_forward
             return train_forward(self, x)
-        plan, stream = self._prepare(x.shape[0], x.shape[2], x.shape[3], x.device)
         if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] != 3:
             raise ValueError("DRNSeg.forward expects fp32 [B,3,H,W]")
-        x = x.contiguous()
-        plan.ingest_nchw(x, stream)
-        plan.run_backbone(stream)
-        oh, ow = plan.out_hw
-        logprobs = torch.empty(x.shape[0], self.classes, oh, ow, dtype=torch.float32, device=x.device)
-        plan.head(self._up_plane(x.device), stream, logprobs, None)
-        logits = plan.bufs["logits"].clone()
-        return logprobs, logits
+        self._check_device(x)
+        return torch.ops.drnmi.forward(x, self._handle)
 
     # ----------------------------------------------------------------- fused paths
     def predict(self, x: torch.Tensor) -> torch.Tensor:
         """torch.max(model(x)[0], 1)[1] (semantic_seg.py:444-445) as one fused pass: int64 labels."""
-        plan, stream = self._prepare(x.shape[0], x.shape[2], x.shape[3], x.device)
-        plan.ingest_nchw(x.contiguous(), stream)
-        plan.run_backbone(stream)
-        oh, ow = plan.out_hw
-        labels = torch.empty(x.shape[0], oh, ow, dtype=torch.int64, device=x.device)
-        plan.head(self._up_plane(x.device), stream, None, labels)
-        return labels
+        if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError("DRNSeg.predict expects fp32 [B,3,H,W]")
+        self._check_device(x)
+        return torch.ops.drnmi.predict(x, self._handle)
 
     def segment(self, frames_u8: torch.Tensor, mean=INFO_MEAN, std=INFO_STD, bgr: bool = False,
                 labels: torch.Tensor | None = None) -> torch.Tensor:
         """Video path: uint8 HWC frames [B,H,W,3] on the GPU -> uint8 label maps [B,8h,8w].
 
         Fuses ToTensorVideoImage + Normalize (data_transforms.py:256-281, :109-125) into the
-        ingest kernel and model(img)[0] + torch.max(final,1) into the head kernel."""
+        ingest kernel and model(img)[0] + torch.max(final,1) into the head kernel.  Runs as
+        torch.ops.drnmi.segment (graph-capturable); `labels=` writes into a caller buffer."""
         if frames_u8.dtype != torch.uint8 or frames_u8.dim() != 4 or frames_u8.shape[3] != 3:
             raise ValueError("segment expects uint8 [B,H,W,3] frames")
+        self._check_device(frames_u8)
+        if labels is not None:
+            return self._segment_impl(frames_u8, mean, std, bgr, labels)
+        return torch.ops.drnmi.segment(frames_u8, self._handle, [float(v) for v in mean],
+                                       [float(v) for v in std], bool(bgr))
+
+    # bodies of the torch.ops.drnmi ops (drnmi/torch_ops.py)
+    def _forward_impl(self, x: torch.Tensor):
+        plan, stream = self._prepare(x.shape[0], x.shape[2], x.shape[3], x.device)
+        x = x.contiguous()
+        plan.ingest_nchw(x, stream)
+        plan.run_backbone(stream, self.timing_hook)
+        oh, ow = plan.out_hw
+        logprobs = torch.empty(x.shape[0], self.classes, oh, ow, dtype=torch.float32, device=x.device)
+        self._head(plan, stream, logprobs, None)
+        logits = plan.bufs["logits"].clone()
+        return logprobs, logits
+
+    def _predict_impl(self, x: torch.Tensor) -> torch.Tensor:
+        plan, stream = self._prepare(x.shape[0], x.shape[2], x.shape[3], x.device)
+        plan.ingest_nchw(x.contiguous(), stream)
+        plan.run_backbone(stream, self.timing_hook)
+        oh, ow = plan.out_hw
+        labels = torch.empty(x.shape[0], oh, ow, dtype=torch.int64, device=x.device)
+        self._head(plan, stream, None, labels)
+        return labels
+
+    def _segment_impl(self, frames_u8, mean, std, bgr, labels):
         plan, stream = self._prepare(frames_u8.shape[0], frames_u8.shape[1], frames_u8.shape[2],
                                      frames_u8.device)
         plan.ingest_u8(frames_u8.contiguous(), mean, std, bgr, stream)
-        plan.run_backbone(stream)
+        plan.run_backbone(stream, self.timing_hook)
         oh, ow = plan.out_hw
         if labels is None:
             labels = torch.empty(frames_u8.shape[0], oh, ow, dtype=torch.uint8, device=frames_u8.device)
-        plan.head(self._up_plane(frames_u8.device), stream, None, labels)
+        elif labels.shape != (frames_u8.shape[0], oh, ow) or labels.dtype not in (torch.uint8, torch.int64) \
+                or not labels.is_contiguous() or labels.device != frames_u8.device:
+            raise ValueError(f"labels must be a contiguous uint8/int64 [{frames_u8.shape[0]}, {oh}, {ow}] tensor "
+                             f"on {frames_u8.device}")
+        self._head(plan, stream, None, labels)
         return labels
+
+    def _head(self, plan, stream, logprobs, labels):
+        if self.use_torch_up:
+            plan.head_bilinear(stream, logprobs, labels)
+        else:
+            plan.head(self._up_plane(plan.packed.device), stream, logprobs, labels)
+
+    @staticmethod
+    def _check_device(t: torch.Tensor):
+        if t.device.type != "cuda":
+            raise RuntimeError("drnmi.DRNSeg runs on the HIP engine only: move the model and input "
+                               "to a ROCm device (no CPU fallback by design)")
 
     # ----------------------------------------------------------------- configuration
     def set_precision(self, precision: str) -> "DRNSeg":
@@ -195,6 +237,7 @@ class DRNSeg(nn.Module):
         return plan
 
     def load_state_dict(self, state_dict, strict=True, assign=False):
+        self._key_tensors = None
         fixed = {}
         for k, v in state_dict.items():
             if k.startswith("module."):
@@ -208,11 +251,19 @@ class DRNSeg(nn.Module):
     def _up_plane(self, device):
         return self.up.weight[0, 0].detach().to(device, torch.float32).contiguous()
 
+    def _apply(self, fn, *args, **kwargs):
+        self._key_tensors = None          # .to() / .cuda() / .float() may swap tensors
+        return super()._apply(fn, *args, **kwargs)
+
     def _state_key(self):
-        key = [self.precision]
-        for t in list(self.parameters()) + list(self.buffers()):
-            key.append((t.data_ptr(), t._version, str(t.device)))
-        return tuple(key)
+        """Repack key: every parameter/buffer's storage and version counter (an in-place update
+        -- optimizer step, apply_masks, load_state_dict -- bumps the version).  The tensor list
+        is cached (walking the module tree cost ~0.6 ms per call); _apply / load_state_dict
+        reset it."""
+        ts = self._key_tensors
+        if ts is None:
+            ts = self._key_tensors = list(self.parameters()) + list(self.buffers())
+        return (self.precision, tuple((t.data_ptr(), t._version) for t in ts))
 
     def _prepare(self, n, h, w, device, keep_all=False):
         if device.type != "cuda":

@@ -17,6 +17,7 @@ tensors' version counters), so Pruner.apply_masks or a load_state_dict is picked
 from __future__ import annotations
 
 import ctypes
+import dataclasses
 from dataclasses import dataclass, field
 
 import torch
@@ -165,11 +166,16 @@ def _fold_bn(bn: nn.BatchNorm2d):
 
 
 class PackedNet:
-    """Device-resident packed weights for one precision."""
+    """Device-resident packed weights for one precision.
+
+    Owns its own copy of the graph's ConvNodes: the packed tensors (wpk, scale, shift, unit
+    masks, int8 fields) of one precision never overwrite another precision's, so a Plan of
+    any PackedNet stays valid while other precisions are packed."""
 
     def __init__(self, graph: Graph, precision: str, device, block_sparse: bool = True,
                  act_scales: dict | None = None):
-        self.graph = graph
+        self.graph = Graph(nodes=[dataclasses.replace(nd) for nd in graph.nodes],
+                           stage_outputs=dict(graph.stage_outputs), channels=dict(graph.channels))
         self.block_sparse = block_sparse
         self.precision = precision
         # int8 nets run their small-channel layers in bf16: "base" is that precision
@@ -532,6 +538,17 @@ class Plan:
             logprobs.data_ptr() if logprobs is not None else None,
             labels.data_ptr() if labels is not None else None,
             lab_dtype, n, c, lh, lw, ctypes.c_void_p(stream)), "up8_logsoftmax_argmax")
+
+    def head_bilinear(self, stream: int, logprobs: torch.Tensor | None, labels: torch.Tensor | None):
+        """use_torch_up head: UpsamplingBilinear2d(8) + LogSoftmax + argmax (lmodels/drnseg.py:285-287)."""
+        lib = _lib.load()
+        logits = self.bufs["logits"]
+        n, c, lh, lw = logits.shape
+        lab_dtype = _lib.DRNMI_I64 if labels is not None and labels.dtype == torch.int64 else _lib.DRNMI_U8
+        _lib.check(lib.drnmi_up8_bilinear_logsoftmax_argmax(
+            logits.data_ptr(), logprobs.data_ptr() if logprobs is not None else None,
+            labels.data_ptr() if labels is not None else None, lab_dtype, n, c, lh, lw, ctypes.c_void_p(stream)),
+            "up8_bilinear_logsoftmax_argmax")
 
     def stage_nchw(self, value: str) -> torch.Tensor:
         """fp32 NCHW copy of an intermediate activation (parity taps; keep_all plans).  int8

@@ -24,8 +24,15 @@ def fast_hist(pred: torch.Tensor, label: torch.Tensor, n: int, hist: torch.Tenso
         raise TypeError("pred/label must be uint8 or int64")
     if not (pred.is_cuda and label.is_cuda):
         raise RuntimeError("fast_hist runs on the HIP kernel: tensors must be on a ROCm device")
+    if pred.device != label.device:
+        raise RuntimeError("pred and label are on different devices")
+    if not 0 < n <= 32:
+        raise ValueError("n must be in 1..32 (drnmi_confusion_matrix)")
     if hist is None:
         hist = torch.zeros(n, n, dtype=torch.int64, device=pred.device)
+    elif (hist.dtype != torch.int64 or tuple(hist.shape) != (n, n) or not hist.is_contiguous()
+          or hist.device != pred.device):
+        raise ValueError(f"hist must be a contiguous int64 ({n}, {n}) tensor on {pred.device}")
     pred, label = pred.contiguous(), label.contiguous()
     lib = _lib.load()
     _lib.check(lib.drnmi_confusion_matrix(pred.data_ptr(), _CODES[pred.dtype], label.data_ptr(),

@@ -122,6 +122,11 @@ class DistributedDataParallel(nn.Module):
                 torch.autograd.graph.increment_version(t)   # eval plans repack on version change
 
     def forward(self, *args, **kwargs):
+        # a backward that raised part-way never ran _finalize: start every step from a clean
+        # reducer so no bucket stays 'launched' and the ranks cannot silently diverge
+        self._queued = False
+        if self._reducer is not None:
+            self._reducer.reset()
         if self.broadcast_buffers and self.module.training and self.world > 1:
             with torch.no_grad():
                 for b in self.module.buffers():
@@ -140,7 +145,10 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._queued = False
-        self._reducer.finalize()
+        try:
+            self._reducer.finalize()
+        finally:
+            self._reducer.reset()
 
     # the reference calls these on the wrapped model
     def optim_parameters(self, memo=None):

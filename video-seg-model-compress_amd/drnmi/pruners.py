@@ -53,6 +53,7 @@ class Pruner:
         self.mask_dict = collections.OrderedDict()
         self.layer_configs = self.parse_config_file(config_fp)
         self._bits_cache = {}
+        self._binary_cache = {}
 
     # -- subclasses implement
     def parse_config_file(self, config_fp):  # pragma: no cover - abstract
@@ -69,6 +70,8 @@ class Pruner:
         if not self.mask_dict:
             return
         params = _resolve_tensors(model, list(self.mask_dict))
+        if use_bits and not all(self._is_binary(layer) for layer in params):
+            use_bits = False      # a non-0/1 mask: w *= mask with the fp32 mask kernel (Pruner.py:20)
         ws, ms, ns = [], [], []
         for layer, w in params.items():
             m = self.mask_dict[layer]
@@ -98,13 +101,26 @@ class Pruner:
         for w in ws:        # in-place write through the C-ABI: bump the version counters
             torch.autograd.graph.increment_version(w)   # (DRNSeg repacks on change)
 
+    def _is_binary(self, layer) -> bool:
+        """True when mask_dict[layer] holds only 0 and 1 (what the 1-bit formats can represent)."""
+        m = self.mask_dict[layer]
+        key = (m.data_ptr(), m._version)
+        hit = self._binary_cache.get(layer)
+        if hit is None or hit[0] != key:
+            hit = (key, bool(((m == 0) | (m == 1)).all().item()))
+            self._binary_cache[layer] = hit
+        return hit[1]
+
     def _mask_bits(self, layer, device):
-        """Bit-packed copy of mask_dict[layer] (bit i of word i/32), cached per mask tensor."""
+        """Bit-packed copy of mask_dict[layer] (bit i of word i/32), cached per mask tensor.
+        Raises ValueError for a mask that is not 0/1 valued (it would be silently binarised)."""
         m = self.mask_dict[layer]
         key = (m.data_ptr(), m._version, str(device))
         hit = self._bits_cache.get(layer)
         if hit is not None and hit[0] == key:
             return hit[1]
+        if not self._is_binary(layer):
+            raise ValueError(f"{layer}: mask is not 0/1 valued; the 1-bit mask path cannot hold it")
         words = _pack_bits((m.detach().reshape(-1) != 0).cpu().numpy())
         bits = torch.from_numpy(words.view(np.int32).copy()).to(device)
         self._bits_cache[layer] = (key, bits)
@@ -138,6 +154,7 @@ class Pruner:
                 raise ValueError(f"{path}: mask format {int(z['format'][0])} != {MASK_FORMAT_VERSION}")
             self.mask_dict = collections.OrderedDict()
             self._bits_cache = {}
+            self._binary_cache = {}
             for i, layer in enumerate(z["layers"].tolist()):
                 words, shape = z[f"bits{i}"], tuple(int(s) for s in z[f"shape{i}"])
                 n = int(np.prod(shape))

@@ -221,10 +221,16 @@ class TrainRunner:
             per_node.append((y, mean, invstd) if save else None)
         lh, lw = shapes["logits"]
         logprobs = torch.empty(n, logits.shape[1], 8 * lh, 8 * lw, dtype=torch.float32, device=dev)
-        up = self.model._up_plane(dev)
-        _lib.check(lib.drnmi_up8_logsoftmax_argmax(logits.data_ptr(), up.data_ptr(), logprobs.data_ptr(), None,
-                                                   _lib.DRNMI_U8, n, logits.shape[1], lh, lw,
-                                                   ctypes.c_void_p(stream)), "up8_logsoftmax")
+        if self.model.use_torch_up:      # UpsamplingBilinear2d(8) head (lmodels/drnseg.py:285-287)
+            up = None
+            _lib.check(lib.drnmi_up8_bilinear_logsoftmax_argmax(logits.data_ptr(), logprobs.data_ptr(), None,
+                                                                _lib.DRNMI_U8, n, logits.shape[1], lh, lw,
+                                                                ctypes.c_void_p(stream)), "up8_bilinear_logsoftmax")
+        else:
+            up = self.model._up_plane(dev)
+            _lib.check(lib.drnmi_up8_logsoftmax_argmax(logits.data_ptr(), up.data_ptr(), logprobs.data_ptr(), None,
+                                                       _lib.DRNMI_U8, n, logits.shape[1], lh, lw,
+                                                       ctypes.c_void_p(stream)), "up8_logsoftmax")
         saved = None
         if save:
             saved = {"vals": vals, "shapes": shapes, "nodes": per_node, "n": n, "up": up}
@@ -244,9 +250,14 @@ class TrainRunner:
         du = torch.empty_like(logprobs) if g_lp is not None else None
         glp = g_lp.contiguous() if g_lp is not None else None
         glg = g_logits.contiguous() if g_logits is not None else None
-        _lib.check(lib.drnmi_up8_lsm_bwd_f32(_vp(glp), _vp(logprobs) if glp is not None else None, _vp(glg),
-                                             _vp(saved["up"]), float(self.grad_scale), n, ncls, lh, lw, _vp(du),
-                                             _vp(dlog), sp), "up8_lsm_bwd")
+        if saved["up"] is None:          # use_torch_up: transpose of the bilinear x8
+            _lib.check(lib.drnmi_up8_bilinear_lsm_bwd_f32(_vp(glp), _vp(logprobs) if glp is not None else None,
+                                                          _vp(glg), float(self.grad_scale), n, ncls, lh, lw, _vp(du),
+                                                          _vp(dlog), sp), "up8_bilinear_lsm_bwd")
+        else:
+            _lib.check(lib.drnmi_up8_lsm_bwd_f32(_vp(glp), _vp(logprobs) if glp is not None else None, _vp(glg),
+                                                 _vp(saved["up"]), float(self.grad_scale), n, ncls, lh, lw, _vp(du),
+                                                 _vp(dlog), sp), "up8_lsm_bwd")
         del du
         grads = {}          # value -> NHWC fp32 gradient buffer
         for idx in range(len(self.nodes) - 1, -1, -1):
