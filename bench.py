@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--arch", default="drn_d_22")
     ap.add_argument("--height", type=int, default=1024)
     ap.add_argument("--width", type=int, default=2048)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "int8"],
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "fp32x", "int8"],
                     help="int8: W8A8 for the cin >= 64 convs (config C5), scales calibrated on 2 "
                          "synthetic frames before the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline sample budget")
@@ -181,7 +181,7 @@ def main():
     from drnmi import _lib
     from drnmi.dist import max_over_ranks
     from drnmi.drnseg import INFO_MEAN, INFO_STD, build
-    from drnmi.roofline import MFMA_PEAK, network_roofline, node_work
+    from drnmi.roofline import kernel_peak, network_roofline, node_work
 
     if args.prune:
         model, n_pruned = pruned_model(args, dev)
@@ -285,7 +285,7 @@ def main():
         avg_d = sum(durs) / len(durs)
         avg_f = sum(flops) / len(flops)
         ach = avg_f / avg_d / 1e12
-        peak = MFMA_PEAK["int8" if dominant.startswith("conv_i8") else plan.packed.base] / 1e12
+        peak = kernel_peak(dominant, plan.packed.base) / 1e12
         out["roofline"] = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 2), "peak": peak,
                            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
                            "traffic_unit": "bytes/launch", "traffic_source": traffic_src,

@@ -25,7 +25,13 @@
 extern "C" {
 #endif
 
-enum drnmi_dtype { DRNMI_F32 = 0, DRNMI_BF16 = 1, DRNMI_U8 = 2, DRNMI_I64 = 3, DRNMI_I8 = 4 };
+enum drnmi_dtype { DRNMI_F32 = 0, DRNMI_BF16 = 1, DRNMI_U8 = 2, DRNMI_I64 = 3, DRNMI_I8 = 4, DRNMI_F32X3 = 5 };
+/* DRNMI_F32X3 (conv dtype only, the "fp32x" precision mode): x, res and y are fp32 NHWC as in
+ * DRNMI_F32, wgt is three bf16 planes [3][cout_pad][k_pad] with w = w1 + w2 + w3 (an exact split
+ * of the fp32 weight), and the conv runs fp32-accurate arithmetic on the bf16 MFMA pipe: each
+ * fp32 activation is split the same way in registers and the six products above 2^-24 are
+ * accumulated in fp32 (csrc/conv_x6.hip).  Requires cin >= 32 (power of two), ks 1 or 3,
+ * out_dtype DRNMI_F32. */
 
 enum drnmi_status {
   DRNMI_OK = 0,

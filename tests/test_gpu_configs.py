@@ -34,10 +34,11 @@ def _masks_match_golden(golden, tag, mask_dict):
         assert sha == str(golden[f"{tag}/sha/{layer}"]), layer
 
 
-def test_c1_d22_512x1024_fp32_vs_oracle():
+@pytest.mark.parametrize("precision", ["fp32", "fp32x"])
+def test_c1_d22_512x1024_fp32_vs_oracle(precision):
     from drnmi.drnseg import build
     from drnmi.weights import synth_frames
-    m = build("drn_d_22", 19, seed=5, device=DEV, precision="fp32")
+    m = build("drn_d_22", 19, seed=5, device=DEV, precision=precision)
     frames = synth_frames(31, 1, 512, 1024)
     x = O.preprocess_u8(frames)
     lp, logits = m(x.to(DEV))
@@ -53,7 +54,7 @@ def test_c1_d22_512x1024_fp32_vs_oracle():
     lab = torch.max(lp, 1)[1].cpu().numpy()
     ref_lab = torch.max(ref_lp, 1)[1].numpy()
     diff = lab != ref_lab
-    print(f"C1 D-22 1x3x512x1024 fp32: logits max-abs {err:.2e}, log-probs {lp_err:.2e}, "
+    print(f"C1 D-22 1x3x512x1024 {precision}: logits max-abs {err:.2e}, log-probs {lp_err:.2e}, "
           f"labels differ {int(diff.sum())} px ({int((margin <= 1e-4).sum())} px with margin <= 1e-4)")
     assert err <= 1e-3 and lp_err <= 1e-3
     assert not np.any(diff & (margin > 1e-4))

@@ -131,3 +131,37 @@ def test_bf16_segment_matches_bf16_forward_labels(golden_forward):
     agree_ref = (lab_seg == ref).float().mean().item()
     print(f"bf16 segment vs predict agreement {agree:.4f}, vs reference {agree_ref:.4f}")
     assert agree >= 0.98 and agree_ref >= 0.98
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fp32x_forward_matches_reference(case, golden_forward):
+    """fp32x (fp32-accurate split-bf16 MFMA for every cin >= 32 conv): the fp32 gates."""
+    m = model(case, golden_forward).set_precision("fp32x")
+    x = torch.from_numpy(golden_forward[case + "/input"]).to(DEV)
+    lp, logits = m(x)
+    m.set_precision("fp32")
+    torch.cuda.synchronize()
+    err = np.abs(logits.cpu().numpy() - golden_forward[case + "/logits"]).max()
+    labels = torch.max(lp, 1)[1].cpu().numpy()
+    diff = int((labels != golden_forward[case + "/labels"]).sum())
+    print(f"{case} fp32x: logit max-abs {err:.2e}, labels differ {diff} px")
+    assert err <= 1e-3 and diff == 0
+
+
+def test_fp32x_stages_match_oracle(golden_forward):
+    case = "d54_1x64x128"
+    m = model(case, golden_forward).set_precision("fp32x")
+    x = torch.from_numpy(golden_forward[case + "/input"])
+    plan = m.plan(x.shape[0], x.shape[2], x.shape[3], keep_all=True)
+    from drnmi import _lib
+    plan.ingest_nchw(x.to(DEV), _lib.stream_ptr())
+    plan.run_backbone(_lib.stream_ptr())
+    assert sum(nd.x6 for nd in plan.packed.graph.nodes) >= 40
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    _, _, stages = O.drnseg_forward(sd, "drn_d_54", x)
+    for name, val in m._graph.stage_outputs.items():
+        got = plan.stage_nchw(val).cpu()
+        ref = stages[name]
+        err = (got - ref).abs().max().item()
+        assert err <= 1e-4 * max(1.0, ref.abs().max().item()), f"{name}: {err}"
+    m.set_precision("fp32")

@@ -5,12 +5,14 @@ Tolerances (written here, per precision):
   bf16 perf mode  : reference computed on bf16-rounded operands; |y - ref| <= 1.5e-2 * max|ref|
                     (bf16 output rounding 2^-9 plus fp32 accumulation-order differences)
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
 
-from drnmi import ops
+from drnmi import _lib, ops
 from oracle import drn_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -333,3 +335,66 @@ def test_confusion_matrix_matches_fast_hist(dt):
     np.testing.assert_array_equal(h.cpu().numpy(), 2 * ref)
     np.testing.assert_allclose(metrics.per_class_iu(h), O.per_class_iu(2 * ref))
     assert metrics.miou(h) == round(float(np.nanmean(O.per_class_iu(ref))) * 100, 2)
+
+
+X6_CASES = [
+    # (n, h, w, cin, cout, ks, stride, pad, dil, res)
+    (1, 20, 36, 512, 512, 3, 1, 4, 4, True),     # layer6-shaped, dilation 4, 256-channel tile
+    (2, 11, 13, 256, 256, 3, 1, 2, 2, False),    # ragged pixel tile, dilation 2
+    (1, 16, 16, 128, 128, 3, 1, 1, 1, True),     # 128-channel tile
+    (1, 17, 15, 32, 64, 3, 2, 1, 1, False),      # cin 32, stride 2, 64-channel tile
+    (1, 16, 16, 64, 128, 1, 2, 0, 1, False),     # 1x1 stride-2 downsample
+]
+
+
+@pytest.mark.parametrize("case", X6_CASES)
+def test_conv_x6_fp32_accuracy(case):
+    """DRNMI_F32X3 (split-bf16, 6 products) vs an fp64 conv: as close as the exact-f32 kernel."""
+    import torch.nn.functional as F
+    from drnmi import ops
+    from drnmi.engine import split3_bf16
+    n, h, w, cin, cout, ks, s, pad, dil, res = case
+    g = torch.Generator().manual_seed(cin + cout + ks)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, ks, ks, generator=g) / (cin * ks * ks) ** 0.5
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g)
+    y64 = F.conv2d(x.double(), wt.double(), stride=s, padding=pad, dilation=dil) * sc.double().view(1, -1, 1, 1) \
+        + sh.double().view(1, -1, 1, 1)
+    r = None
+    if res:
+        r = torch.randn(y64.shape, generator=g)
+        y64 = y64 + r.double()
+    y64 = torch.relu(y64)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    rd = r.permute(0, 2, 3, 1).contiguous().to(DEV) if res else None
+    f32 = ops.conv2d_bn_act(xd, wt.to(DEV), sc.to(DEV), sh.to(DEV), rd, stride=s, padding=pad, dilation=dil,
+                            relu=True)
+    wpk, k = ops.pack_conv_weight(wt.to(DEV), cin, torch.float32)
+    planes = split3_bf16(wpk)
+    scp = torch.ones(wpk.shape[0], device=DEV)
+    shp = torch.zeros(wpk.shape[0], device=DEV)
+    scp[:cout], shp[:cout] = sc.to(DEV), sh.to(DEV)
+    ho = (h + 2 * pad - dil * (ks - 1) - 1) // s + 1
+    wo = (w + 2 * pad - dil * (ks - 1) - 1) // s + 1
+    y = torch.empty(n, ho, wo, cout, device=DEV)
+    a = _lib.ConvArgs()
+    a.x, a.wgt, a.scale, a.shift = xd.data_ptr(), planes.data_ptr(), scp.data_ptr(), shp.data_ptr()
+    a.res = rd.data_ptr() if res else None
+    a.y = y.data_ptr()
+    a.y_sn, a.y_sp, a.y_sc = ho * wo * cout, cout, 1
+    a.n, a.h, a.w, a.cin = n, h, w, cin
+    a.ho, a.wo, a.cout, a.cout_pad = ho, wo, cout, wpk.shape[0]
+    a.ks, a.stride, a.pad, a.dil = ks, s, pad, dil
+    a.k, a.k_pad = k, wpk.shape[1]
+    a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_F32X3, _lib.DRNMI_F32, -1, _lib.ALGO_IGEMM
+    name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
+    assert name.startswith("conv_x6_kernel")
+    _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "x6")
+    torch.cuda.synchronize()
+    ref = y64.permute(0, 2, 3, 1).numpy()
+    e_x6 = np.abs(y.cpu().double().numpy() - ref).max()
+    e_f32 = np.abs(f32.cpu().double().numpy() - ref).max()
+    scale = np.abs(ref).max()
+    print(f"{name} {case}: max-abs vs fp64 {e_x6:.2e} (exact-f32 kernel {e_f32:.2e}, |y| {scale:.1f})")
+    assert e_x6 <= max(4 * e_f32, 1e-6 * scale)

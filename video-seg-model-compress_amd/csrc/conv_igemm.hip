@@ -335,6 +335,8 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
     return DRNMI_EINVAL;
   if (p.dtype == DRNMI_I8) {
     if (p.out_dtype != DRNMI_I8 && p.out_dtype != DRNMI_BF16 && p.out_dtype != DRNMI_F32) return DRNMI_EINVAL;
+  } else if (p.dtype == DRNMI_F32X3) {
+    if (p.out_dtype != DRNMI_F32) return DRNMI_EINVAL;
   } else if ((p.dtype != DRNMI_BF16 && p.dtype != DRNMI_F32) ||
              (p.out_dtype != DRNMI_BF16 && p.out_dtype != DRNMI_F32)) {
     return DRNMI_EINVAL;
@@ -344,6 +346,7 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
       p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
     return DRNMI_EINVAL;
   if (p.dtype == DRNMI_I8) return i8_conv_dispatch(p, reinterpret_cast<hipStream_t>(stream));   // int8: one kernel family
+  if (p.dtype == DRNMI_F32X3) return x6_conv_dispatch(p, reinterpret_cast<hipStream_t>(stream));
   if (p.tile >= 4 || (p.tile < 0 && (big_conv_supported(p) || halo_conv_supported(p))))
     return big_conv_dispatch(p, p.tile < 0 ? -1 : p.tile - 4, reinterpret_cast<hipStream_t>(stream));
   const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;
@@ -366,6 +369,7 @@ extern "C" const char* drnmi_conv_kernel_name(const drnmi_conv_args* a) {
   const drnmi_conv_args& p = *a;
   if (p.algo == DRNMI_ALGO_PATCH) return patch_conv_name(p);
   if (p.dtype == DRNMI_I8) return i8_conv_name(p);
+  if (p.dtype == DRNMI_F32X3) return x6_conv_name(p);
   if (p.tile >= 4 || (p.tile < 0 && (big_conv_supported(p) || halo_conv_supported(p))))
     return big_conv_name(p, p.tile < 0 ? -1 : p.tile - 4);
   const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;

@@ -1,0 +1,327 @@
+// fp32-accurate NHWC implicit-GEMM convolution on the bf16 MFMA pipe ("fp32x" precision mode).
+//
+// The north star's parity gate (logits within 1e-3 of the reference PyTorch-CPU fp32 forward,
+// argmax maps bit-exact) needs fp32-class arithmetic; bf16 misses it (98.4 %
+// argmax agreement) and the f32-input MFMA runs at 1/16 of the bf16 rate (157 TF).  Here every
+// fp32 operand is split exactly into three bf16 terms, x = x1 + x2 + x3 (x1 = bf16(x),
+// x2 = bf16(x - x1), x3 = bf16(x - x1 - x2): 24 significant bits, the fp32 significand), and
+// the product is formed from the six terms above 2^-24:
+//     x*w ~ x1 w1 + (x1 w2 + x2 w1) + (x1 w3 + x2 w2 + x3 w1)
+// with fp32 accumulation in v_mfma_f32_16x16x32_bf16 — six bf16 MFMAs per fp32 product, 417 TF
+// of fp32-accurate peak (2.65x the f32 MFMA).  The dropped terms are < 2^-24 relative: the
+// result is as close to exact as an fp32 FMA chain (measured on the DRN-D goldens: see DESIGN.md).
+//
+// Serves every conv with cin >= 32 and ks 1/3 in fp32x mode (layer3..8 3x3 convs at dilation
+// 1/2/4, the 1x1 downsamples, seg 1x1 + bias; lmodels/drn.py:27-29, :49-65, :86-106,
+// :181-186, :201-211, lmodels/drnseg.py:278-284).
+//
+//   * Weights are pre-split on the host side of the plan: [3][cout_pad][k_pad] bf16 planes.
+//   * Activations stay fp32 NHWC in HBM (the fp32 mode's layout); each pixel row of the B tile
+//     lands in LDS as fp32 (LDS-DMA, per-lane im2col source addresses, zero page for padding)
+//     and is split into its three bf16 fragments in registers right after the fragment read —
+//     one split per B fragment feeds FM x 6 MFMAs, so the VALU work hides under the MFMAs.
+//   * K step = 32 input channels of one tap; tile = BCO output channels x 256 pixels; each wave
+//     owns WCO channels x 64 pixels (FM x 4 fragments); LDS rows XOR-swizzled on the DMA source
+//     and on the fragment read; NST-stage ring with counted vmcnt + raw s_barrier; tiles dealt
+//     XCD-major.
+//   * Epilogue in fp32: v = acc * scale + shift (+ residual), ReLU, fp32 NHWC (or the strided
+//     fp32 NCHW seg logits).
+#include "common.h"
+#include "kernels.h"
+
+namespace drnmi {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void g_void_t;
+
+__device__ uint4 g_x6_zero[64];   // zero-initialised: the source of padded taps / rows
+
+constexpr int kBPX = 256;   // pixels per tile
+constexpr int kBK = 32;     // input channels per K step
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+__device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }    // bf16 A rows
+__device__ __forceinline__ int swz128(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }   // fp32 B rows
+
+// Exact three-way split of 8 fp32 values into bf16 fragments (round-to-nearest-even each
+// step; x - x1 and (x - x1) - x2 are exact in fp32 by Sterbenz).
+__device__ __forceinline__ void split3(const float4& lo4, const float4& hi4, bf16x8& b1, bf16x8& b2, bf16x8& b3) {
+  const float x[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const __bf16 h = static_cast<__bf16>(x[i]);
+    const float r1 = x[i] - static_cast<float>(h);
+    const __bf16 m = static_cast<__bf16>(r1);
+    const float r2 = r1 - static_cast<float>(m);
+    b1[i] = h;
+    b2[i] = m;
+    b3[i] = static_cast<__bf16>(r2);
+  }
+}
+
+template <int WCO, int WC>
+struct X6Cfg {
+  static constexpr int BCO = WCO * WC;
+  static constexpr int FM = WCO / 16;
+  static constexpr int FN = 4;
+  static constexpr int NW = 4 * WC;
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int A_PLANE = BCO * 64;          // one bf16 plane: BCO rows x 32 K x 2 B
+  static constexpr int A_BYTES = 3 * A_PLANE;
+  static constexpr int B_BYTES = kBPX * 128;        // 256 pixel rows x 32 ch x 4 B
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_PW = A_BYTES / 1024 / NW;  // 1-KB DMA pieces per wave per step
+  static constexpr int B_PW = B_BYTES / 1024 / NW;
+  static constexpr int GLDS = A_PW + B_PW;
+  static constexpr int NST = (2 * STAGE <= 160 * 1024 && 3 * STAGE > 160 * 1024) ? 2 : 3;
+  static constexpr int LDS = NST * STAGE;
+  static_assert(A_PW * NW * 1024 == A_BYTES && B_PW * NW * 1024 == B_BYTES, "DMA split");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+template <int KS, int WCO, int WC>
+__global__ void __launch_bounds__(256 * WC, 1)
+conv_x6_kernel(const drnmi_conv_args p) {
+  using C = X6Cfg<WCO, WC>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wc = wave >> 2;          // channel column of the tile
+  const int wp = wave & 3;           // 64-pixel slice of the tile
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  const int M = p.n * p.ho * p.wo;
+  const int hw_o = p.ho * p.wo;
+  const int nco = (p.cout + C::BCO - 1) / C::BCO;
+  const int npx = (M + kBPX - 1) / kBPX;
+  const int tile = xcd_remap(blockIdx.x, npx * nco);
+  const int px0 = (tile / nco) * kBPX;
+  const int co0 = (tile % nco) * C::BCO;
+
+  const int cin = p.cin;
+  const int lc = 31 - __builtin_clz(cin);
+  const int H = p.h, W = p.w, dil = p.dil;
+  const float* __restrict__ x = reinterpret_cast<const float*>(p.x);
+  const uint16_t* __restrict__ wt = reinterpret_cast<const uint16_t*>(p.wgt);
+  const int64_t plane_stride = static_cast<int64_t>(p.cout_pad) * p.k_pad;
+  const int nk = p.k_pad / kBK;
+  const char* zero_src = reinterpret_cast<const char*>(g_x6_zero) + lane * 16;
+
+  // --- A pieces: 16 rows of 64 B each; linear row R = plane * BCO + r
+  int64_t a_off[C::A_PW];
+#pragma unroll
+  for (int i = 0; i < C::A_PW; ++i) {
+    const int R = (wave * C::A_PW + i) * 16 + (lane >> 2);
+    const int pl = R / C::BCO, r = R - pl * C::BCO;
+    a_off[i] = pl * plane_stride + static_cast<int64_t>(co0 + r) * p.k_pad + swz64(r, lane & 3) * 8;
+  }
+  // --- B pieces: 8 pixel rows of 128 B; (ih0, iw0) of tap (0,0) and the element offset of the
+  // row's chunk at that tap (only dereferenced when the tap is inside the image)
+  int b_ih[C::B_PW], b_iw[C::B_PW], b_off[C::B_PW];
+#pragma unroll
+  for (int j = 0; j < C::B_PW; ++j) {
+    const int r = (wave * C::B_PW + j) * 8 + (lane >> 3);
+    const int m = px0 + r;
+    b_ih[j] = -(1 << 28);
+    b_iw[j] = -(1 << 28);
+    b_off[j] = 0;
+    if (m < M) {
+      const int n = m / hw_o;
+      const int q = m - n * hw_o;
+      const int oh = q / p.wo;
+      const int ow = q - oh * p.wo;
+      b_ih[j] = oh * p.stride - p.pad;
+      b_iw[j] = ow * p.stride - p.pad;
+      b_off[j] = ((n * H + b_ih[j]) * W + b_iw[j]) * cin + swz128(r, lane & 7) * 4;
+    }
+  }
+
+  auto issue = [&](int kt, int stage) {
+    const int cb = kt / (KS * KS);
+    const int tap = kt - cb * (KS * KS);
+    const int k0 = (tap << lc) + cb * kBK;
+    const int dh = (tap / KS) * dil;
+    const int dw = (tap - (tap / KS) * KS) * dil;
+    const int toff = (dh * W + dw) * cin + cb * kBK;
+    char* sa = smem + stage * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::A_PW; ++i) glds16(wt + a_off[i] + k0, sa + (wave * C::A_PW + i) * 1024);
+#pragma unroll
+    for (int j = 0; j < C::B_PW; ++j) {
+      const bool ok = static_cast<unsigned>(b_ih[j] + dh) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(b_iw[j] + dw) < static_cast<unsigned>(W);
+      const void* src = ok ? static_cast<const void*>(x + (b_off[j] + toff)) : static_cast<const void*>(zero_src);
+      glds16(src, sa + C::A_BYTES + (wave * C::B_PW + j) * 1024);
+    }
+  };
+
+  f32x4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int t = 0; t < C::NST - 1 && t < nk; ++t) issue(t, t);
+
+  for (int t = 0; t < nk; ++t) {
+    const int newer = ((nk - 1) < (t + C::NST - 2) ? (nk - 1) : (t + C::NST - 2)) - t;
+    if (C::NST >= 3 && newer >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::GLDS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // the stage read at step t-1 is free for every wave: refill it with step t + NST - 1
+    if (t + C::NST - 1 < nk) issue(t + C::NST - 1, (t + C::NST - 1) % C::NST);
+
+    const char* sa = smem + (t % C::NST) * C::STAGE;
+    const char* sb = sa + C::A_BYTES;
+    bf16x8 b1[C::FN], b2[C::FN], b3[C::FN];
+#pragma unroll
+    for (int fn = 0; fn < C::FN; ++fn) {
+      const int r = wp * 64 + fn * 16 + fr;
+      const float4 lo4 = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq) * 16);
+      const float4 hi4 = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq + 1) * 16);
+      split3(lo4, hi4, b1[fn], b2[fn], b3[fn]);
+    }
+#pragma unroll
+    for (int fm = 0; fm < C::FM; ++fm) {
+      const int r = wc * WCO + fm * 16 + fr;
+      const char* ar = sa + r * 64 + swz64(r, fq) * 16;
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(ar);
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(ar + C::A_PLANE);
+      const bf16x8 a3 = *reinterpret_cast<const bf16x8*>(ar + 2 * C::A_PLANE);
+      // smallest terms first; independent accumulators between dependent MFMAs
+#pragma unroll
+      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, b1[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b2[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b3[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b1[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[fn], acc[fm][fn], 0, 0, 0);
+    }
+  }
+
+  // --- epilogue: lane owns channels co..co+3 of pixel m, fp32
+  const float* __restrict__ res = reinterpret_cast<const float*>(p.res);
+  const bool nhwc = p.y_sc == 1;
+#pragma unroll
+  for (int fn = 0; fn < C::FN; ++fn) {
+    const int m = px0 + wp * 64 + fn * 16 + fr;
+    if (m >= M) continue;
+    const int n = m / hw_o;
+    const int q = m - n * hw_o;
+    const int64_t ybase = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp;
+#pragma unroll
+    for (int fm = 0; fm < C::FM; ++fm) {
+      const int co = co0 + wc * WCO + fm * 16 + fq * 4;
+      if (co >= p.cout) continue;
+      const bool full = co + 3 < p.cout;
+      const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);   // padded to cout_pad
+      float v[4] = {acc[fm][fn][0], acc[fm][fn][1], acc[fm][fn][2], acc[fm][fn][3]};
+      if (p.scale != nullptr) {
+        const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);
+        v[0] = v[0] * sc.x + sh.x;
+        v[1] = v[1] * sc.y + sh.y;
+        v[2] = v[2] * sc.z + sh.z;
+        v[3] = v[3] * sc.w + sh.w;
+      } else {
+        v[0] += sh.x;
+        v[1] += sh.y;
+        v[2] += sh.z;
+        v[3] += sh.w;
+      }
+      if (res != nullptr) {
+        const float* rp = res + static_cast<int64_t>(m) * p.cout + co;
+        if (full) {
+          const float4 rv = *reinterpret_cast<const float4*>(rp);
+          v[0] += rv.x;
+          v[1] += rv.y;
+          v[2] += rv.z;
+          v[3] += rv.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (co + j < p.cout) v[j] += rp[j];
+        }
+      }
+      if (p.relu) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+      }
+      float* y = reinterpret_cast<float*>(p.y);
+      if (nhwc && full) {
+        *reinterpret_cast<float4*>(y + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (co + j < p.cout) y[ybase + static_cast<int64_t>(co + j) * p.y_sc] = v[j];
+      }
+    }
+  }
+}
+
+template <int KS, int WCO, int WC>
+hipError_t launch_x6(const drnmi_conv_args& p, hipStream_t s) {
+  using C = X6Cfg<WCO, WC>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x6_kernel<KS, WCO, WC>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const int64_t blocks = ((M + kBPX - 1) / kBPX) * ((p.cout + C::BCO - 1) / C::BCO);
+  hipLaunchKernelGGL((conv_x6_kernel<KS, WCO, WC>), dim3(static_cast<unsigned>(blocks)), dim3(C::THREADS), C::LDS,
+                     s, p);
+  return hipGetLastError();
+}
+
+// 0: 256-channel tile (8 waves), 1: 128 (4 waves), 2: 64 (4 waves)
+int x6_variant(const drnmi_conv_args& p) { return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 1 : 2; }
+constexpr int kX6Bco[3] = {256, 128, 64};
+
+}  // namespace
+
+bool x6_conv_supported(const drnmi_conv_args& p) {
+  return p.dtype == DRNMI_F32X3 && p.out_dtype == DRNMI_F32 && p.cin >= kBK && (p.cin & (p.cin - 1)) == 0 &&
+         (p.ks == 1 || p.ks == 3) && p.k == p.ks * p.ks * p.cin && p.k_pad == p.k &&
+         static_cast<int64_t>(p.n) * p.h * p.w * p.cin < (int64_t(1) << 31) && p.h < 16384 && p.w < 16384 &&
+         (p.y_sc != 1 || p.y_sp == p.cout);
+}
+
+int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
+  if (!x6_conv_supported(p)) return DRNMI_ENOTSUP;
+  const int v = x6_variant(p);
+  // every weight row a tile's DMA reads must exist in each plane
+  if ((p.cout + kX6Bco[v] - 1) / kX6Bco[v] * kX6Bco[v] > p.cout_pad) return DRNMI_EINVAL;
+  hipError_t e;
+  if (p.ks == 3) e = v == 0 ? launch_x6<3, 128, 2>(p, s) : v == 1 ? launch_x6<3, 128, 1>(p, s) : launch_x6<3, 64, 1>(p, s);
+  else e = v == 0 ? launch_x6<1, 128, 2>(p, s) : v == 1 ? launch_x6<1, 128, 1>(p, s) : launch_x6<1, 64, 1>(p, s);
+  return static_cast<int>(e);
+}
+
+const char* x6_conv_name(const drnmi_conv_args& p) {
+  if (!x6_conv_supported(p)) return nullptr;
+  static const char* n3[3] = {"conv_x6_kernel<3, 128, 2>", "conv_x6_kernel<3, 128, 1>", "conv_x6_kernel<3, 64, 1>"};
+  static const char* n1[3] = {"conv_x6_kernel<1, 128, 2>", "conv_x6_kernel<1, 128, 1>", "conv_x6_kernel<1, 64, 1>"};
+  return p.ks == 3 ? n3[x6_variant(p)] : n1[x6_variant(p)];
+}
+
+}  // namespace drnmi

@@ -19,4 +19,8 @@ const char* i8_conv_name(const drnmi_conv_args& p);
 bool halo_conv_supported(const drnmi_conv_args& p);
 int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
 const char* halo_conv_name(const drnmi_conv_args& p);
+// fp32-accurate 6-product split-bf16 implicit GEMM (conv_x6.hip): dtype DRNMI_F32X3, cin >= 32.
+bool x6_conv_supported(const drnmi_conv_args& p);
+int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
+const char* x6_conv_name(const drnmi_conv_args& p);
 }  // namespace drnmi

@@ -10,7 +10,7 @@ import os
 
 from .build import LIB_PATH
 
-DRNMI_F32, DRNMI_BF16, DRNMI_U8, DRNMI_I64, DRNMI_I8 = 0, 1, 2, 3, 4
+DRNMI_F32, DRNMI_BF16, DRNMI_U8, DRNMI_I64, DRNMI_I8, DRNMI_F32X3 = 0, 1, 2, 3, 4, 5
 ALGO_IGEMM, ALGO_PATCH = 0, 1
 
 _STATUS = {-1: "DRNMI_EINVAL (bad shape/stride/dtype)", -2: "DRNMI_ENOTSUP (no kernel for this config)"}

@@ -17,7 +17,9 @@ Differences by design:
     (lmodels/drnseg.py:285-287: bilinear, align_corners=True, output 8h x 8w) on its own
     fused HIP kernel (drnmi_up8_bilinear_logsoftmax_argmax).
   * precision: "fp32" (default; the reference's arithmetic, parity mode, exact-fp32
-    MFMA), "bf16" (perf mode, fp32 accumulation) or "int8" (W8A8 for the cin >= 64 convs,
+    MFMA), "fp32x" (fp32-accurate arithmetic on the bf16 MFMA pipe: exact 3-way bf16 splits,
+    6 products, for every conv with cin >= 32; parity gates as fp32, ~3x faster), "bf16"
+    (perf mode, fp32 accumulation) or "int8" (W8A8 for the cin >= 64 convs,
     config C5; needs calibrate_int8() first — the reference has no quantisation, so this
     mode is ours) via set_precision().
   * segment(frames_u8) is the fused seg_video path (seg_video_old_no_plot.py:157-169:
@@ -184,8 +186,8 @@ class DRNSeg(nn.Module):
 
     # ----------------------------------------------------------------- configuration
     def set_precision(self, precision: str) -> "DRNSeg":
-        if precision not in ("fp32", "bf16", "int8"):
-            raise ValueError("precision must be 'fp32', 'bf16' or 'int8'")
+        if precision not in ("fp32", "fp32x", "bf16", "int8"):
+            raise ValueError("precision must be 'fp32', 'fp32x', 'bf16' or 'int8'")
         self.precision = precision
         return self
 

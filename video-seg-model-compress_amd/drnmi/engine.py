@@ -30,7 +30,12 @@ BN_EPS_DEFAULT = 1e-5
 K_ALIGN = 32
 COUT_ALIGN = 128
 
-DTYPES = {"fp32": (torch.float32, _lib.DRNMI_F32), "bf16": (torch.bfloat16, _lib.DRNMI_BF16)}
+DTYPES = {"fp32": (torch.float32, _lib.DRNMI_F32), "bf16": (torch.bfloat16, _lib.DRNMI_BF16),
+          "fp32x": (torch.float32, _lib.DRNMI_F32)}
+# fp32x: fp32 activations everywhere (the fp32 mode's buffers); the convs with cin >= X6_MIN_CIN
+# and ks 1/3 run fp32-accurate split-bf16 arithmetic (csrc/conv_x6.hip, dtype DRNMI_F32X3), the
+# full-resolution small-channel stem / layer1 / layer2 stay on the exact f32 MFMA kernels.
+X6_MIN_CIN = 32
 TORCH_OF_CODE = {_lib.DRNMI_F32: torch.float32, _lib.DRNMI_BF16: torch.bfloat16, _lib.DRNMI_I8: torch.int8}
 # W8A8 (config C5): convs whose input channel stride is >= this run on the int8 MFMA kernel
 # (conv_i8_kernel: K steps of 64/128 int8 channels); the full-resolution small-channel layers
@@ -82,6 +87,7 @@ class ConvNode:
     r_val: str | None = None
     res_scale: float = 0.0
     out_scale: float = 0.0       # 1 / scale of an int8 output (0: bf16 / fp32 output)
+    x6: bool = False             # fp32x: wpk holds three bf16 planes, launched as DRNMI_F32X3
 
 
 @dataclass
@@ -258,8 +264,15 @@ class PackedNet:
                     shift[:cout] = conv.bias.detach().to(self.device, torch.float32)
                 nd.scale, nd.shift = scale.contiguous(), shift.contiguous()
                 nd.i8, nd.x_val, nd.r_val, nd.res_scale, nd.out_scale = False, nd.src, nd.res, 0.0, 0.0
+                nd.x6 = False
                 if ni in self.i8_nodes:
                     self._pack_int8(nd, full, scale, cout)
+                    continue
+                if self.precision == "fp32x" and cs >= X6_MIN_CIN and kh in (1, 3):
+                    nd.x6 = True
+                    nd.wpk = split3_bf16(full)
+                    nd.scale_folded = False
+                    nd.unit_mask, nd.zero_unit_frac = None, 0.0
                     continue
                 # bf16 LDS-DMA kernels: fold the BN scale into the weights so the kernel starts its
                 # accumulators from shift + residual (include/drnmi.h: scale may be NULL)
@@ -301,6 +314,18 @@ class PackedNet:
             nd.res_scale = float(self.act_scales[nd.res])
         if self.vcode.get(nd.dst) == _lib.DRNMI_I8:
             nd.out_scale = 1.0 / float(self.act_scales[nd.dst])
+
+
+def split3_bf16(w: torch.Tensor) -> torch.Tensor:
+    """fp32 [R, K] -> bf16 [3, R, K] planes with w = w1 + w2 + w3 (round-to-nearest-even at each
+    step; the residuals are exact in fp32), the weight side of the fp32x arithmetic
+    (include/drnmi.h DRNMI_F32X3)."""
+    w = w.float()
+    w1 = w.to(torch.bfloat16)
+    r1 = w - w1.float()
+    w2 = r1.to(torch.bfloat16)
+    w3 = (r1 - w2.float()).to(torch.bfloat16)
+    return torch.stack([w1, w2, w3]).contiguous()
 
 
 # Below this fraction of all-zero 16 x 32 units the dense kernel is used: skipping costs scalar
@@ -442,7 +467,7 @@ class Plan:
         a.ks, a.stride, a.pad, a.dil = c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0]
         a.k, a.k_pad = nd.k, nd.k_pad
         a.relu = 1 if nd.relu else 0
-        a.dtype = pk.value_code(nd.x_val)
+        a.dtype = _lib.DRNMI_F32X3 if nd.x6 else pk.value_code(nd.x_val)
         a.tile = -1
         a.algo = _lib.ALGO_PATCH if _uses_patch(nd, nd.cin_stride, pk.base) else _lib.ALGO_IGEMM
         a.res_scale, a.out_scale = nd.res_scale, nd.out_scale

@@ -11,13 +11,24 @@ f32-input MFMA 157.3 TFLOP/s.
 from __future__ import annotations
 
 HBM_PEAK_BPS = 8.0e12
-MFMA_PEAK = {"bf16": 2.5e15, "fp32": 157.3e12, "int8": 5.0e15}   # int8: dense i8 MFMA = 2x bf16
+# int8: dense i8 MFMA = 2x bf16; fp32x: fp32-accurate split-bf16 arithmetic, 6 bf16 MFMAs per fp32
+# product (csrc/conv_x6.hip) = 2.5 PF / 6
+MFMA_PEAK = {"bf16": 2.5e15, "fp32": 157.3e12, "int8": 5.0e15, "fp32x": 2.5e15 / 6}
+
+
+def kernel_peak(kernel_name: str, base: str) -> float:
+    """MFMA peak of the arithmetic a kernel (named as rocprofv3 names it) runs."""
+    if kernel_name.startswith("conv_i8"):
+        return MFMA_PEAK["int8"]
+    if kernel_name.startswith("conv_x6"):
+        return MFMA_PEAK["fp32x"]
+    return MFMA_PEAK["fp32" if base == "fp32x" else base]
 
 
 def node_work(plan):
     """[(name, flops, bytes)] for every conv node, plus the head (up+argmax)."""
     pk = plan.packed
-    base = 2 if pk.base == "bf16" else 4
+    base = 2 if pk.base == "bf16" else 4        # fp32 / fp32x: fp32 activations
     out = []
     for nd in pk.graph.nodes:
         esz = 1 if nd.i8 else base          # int8 launches: int8 activations and weights
@@ -47,8 +58,9 @@ def node_work(plan):
 def node_peaks(plan):
     """MFMA peak per row of node_work (int8 launches at the i8 rate)."""
     pk = plan.packed
-    base = MFMA_PEAK[pk.base]
-    return [MFMA_PEAK["int8"] if nd.i8 else base for nd in pk.graph.nodes] + [base]
+    base = MFMA_PEAK["fp32" if pk.base == "fp32x" else pk.base]
+    return [MFMA_PEAK["int8"] if nd.i8 else MFMA_PEAK["fp32x"] if nd.x6 else base
+            for nd in pk.graph.nodes] + [base]
 
 
 def network_roofline(plan):
