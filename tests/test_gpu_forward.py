@@ -69,15 +69,18 @@ def test_fp32_stages_match_oracle(case, golden_forward):
         assert err <= 1e-4 * max(1.0, ref.abs().max().item()), f"{name}: {err}"
 
 
-def test_predict_and_segment_agree(golden_forward):
+@pytest.mark.parametrize("precision", ["fp32", "fp32x"])
+def test_predict_and_segment_agree(golden_forward, precision):
     case = "d22_1x300x300"
-    m = model(case, golden_forward).set_precision("fp32")
+    m = model(case, golden_forward).set_precision(precision)
     frames = torch.from_numpy(golden_forward[case + "/frames"]).to(DEV)
     x = torch.from_numpy(golden_forward[case + "/input"]).to(DEV)
     lab_pred = m.predict(x)
     lab_seg = m.segment(frames)
+    m.set_precision("fp32")
     assert lab_seg.dtype == torch.uint8 and lab_seg.shape == (1, 304, 304)
     assert torch.equal(lab_pred.cpu(), lab_seg.cpu().long())
+    assert torch.equal(lab_pred.cpu(), torch.from_numpy(golden_forward[case + "/labels"]).long())
 
 
 @pytest.mark.parametrize("case", ["d22_2x128x256", "d38_1x64x128", "d54_1x64x128"])

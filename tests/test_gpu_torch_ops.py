@@ -50,7 +50,7 @@ def test_up8_and_mask_ops_match_capi():
     assert all(torch.equal(a, b) for a, b in zip(w, expect))
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16", "fp32", "fp32x"])
 def test_segment_op_and_graph_capture(precision):
     from drnmi.drnseg import build
     from drnmi.weights import synth_frames

@@ -41,15 +41,35 @@ struct PatchCfg {
   static_assert(TC % 16 == 0, "tile columns in 16-pixel fragments");
 };
 
-template <int CIN, int COUT, int KS, int S, int TR, int TC, bool SRC_U8>
+// Exact three-way split of 8 fp32 values into bf16 fragments (fp32x mode; as conv_x6.hip).
+__device__ __forceinline__ void split3(const float4& lo4, const float4& hi4, bf16x8& b1, bf16x8& b2, bf16x8& b3) {
+  const float x[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const __bf16 h = static_cast<__bf16>(x[i]);
+    const float r1 = x[i] - static_cast<float>(h);
+    const __bf16 m = static_cast<__bf16>(r1);
+    b1[i] = h;
+    b2[i] = m;
+    b3[i] = static_cast<__bf16>(r1 - static_cast<float>(m));
+  }
+}
+
+// X6 (fp32x mode, dtype DRNMI_F32X3): fp32 input patch in LDS, weights as three bf16 planes in
+// registers, every B fragment split exactly into three bf16 terms and the six products above
+// 2^-24 accumulated in fp32 (csrc/conv_x6.hip has the derivation); fp32 NHWC output.
+template <int CIN, int COUT, int KS, int S, int TR, int TC, bool SRC_U8, bool X6 = false>
 __global__ void __launch_bounds__(kThreads)
 patch_conv_kernel(const drnmi_conv_args p) {
   using C = PatchCfg<CIN, COUT, KS, S, TR, TC, SRC_U8>;
-  __shared__ __attribute__((aligned(16))) bf16_t patch[C::LDS_ELEMS];
+  using PT = typename std::conditional<X6, float, bf16_t>::type;
+  __shared__ __attribute__((aligned(16))) PT patch[C::LDS_ELEMS];
   // Persistent: each workgroup walks tiles blockIdx.x, +gridDim.x, ...  The next tile's
   // input is loaded into registers while the current one computes (the 4x64-pixel tiles are
   // too short-lived to pay a workgroup dispatch each).
-  constexpr int VPP = SRC_U8 ? 1 : CIN / 8;                 // staged units per pixel
+  constexpr int EPU = X6 ? 4 : 8;                           // elements per 16-B unit
+  constexpr int NPL = X6 ? 3 : 1;                           // weight planes
+  constexpr int VPP = SRC_U8 ? 1 : CIN / EPU;               // staged units per pixel
   constexpr int NUNITS = C::PR * C::PC * VPP;
   constexpr int NPT = (NUNITS + kThreads - 1) / kThreads;    // per thread
   using Unit = typename std::conditional<SRC_U8, uint32_t, uint4>::type;
@@ -63,13 +83,16 @@ patch_conv_kernel(const drnmi_conv_args p) {
 
   // ---- weights -> registers: A fragment (mf, ks) = W[mf*16 + lane&15][ks*32 + 8*(lane>>4) ..+7]
   const bf16_t* __restrict__ wt = reinterpret_cast<const bf16_t*>(p.wgt);
-  bf16x8 wa[C::MF][C::NK];
+  const int64_t plane = static_cast<int64_t>(p.cout_pad) * p.k_pad;
+  bf16x8 wa[NPL][C::MF][C::NK];
 #pragma unroll
-  for (int mf = 0; mf < C::MF; ++mf)
+  for (int pl = 0; pl < NPL; ++pl)
 #pragma unroll
-    for (int ks = 0; ks < C::NK; ++ks)
-      wa[mf][ks] = *reinterpret_cast<const bf16x8*>(
-          wt + static_cast<int64_t>(mf * 16 + (lane & 15)) * p.k_pad + ks * 32 + 8 * (lane >> 4));
+    for (int mf = 0; mf < C::MF; ++mf)
+#pragma unroll
+      for (int ks = 0; ks < C::NK; ++ks)
+        wa[pl][mf][ks] = *reinterpret_cast<const bf16x8*>(
+            wt + pl * plane + static_cast<int64_t>(mf * 16 + (lane & 15)) * p.k_pad + ks * 32 + 8 * (lane >> 4));
 
   // ---- input patch of a tile -> registers (zero outside the image = the conv's padding)
   Unit stage[NPT];
@@ -98,8 +121,8 @@ patch_conv_kernel(const drnmi_conv_args p) {
       } else {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (ok)
-          v = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.x) +
-                                              ((static_cast<int64_t>(n) * p.h + ih) * p.w + iw) * CIN + v8 * 8);
+          v = *reinterpret_cast<const uint4*>(reinterpret_cast<const PT*>(p.x) +
+                                              ((static_cast<int64_t>(n) * p.h + ih) * p.w + iw) * CIN + v8 * EPU);
         stage[u] = v;
       }
     }
@@ -111,20 +134,27 @@ patch_conv_kernel(const drnmi_conv_args p) {
       if (i >= NUNITS) break;
       if constexpr (SRC_U8) {
         // reference normalisation, same fp32 op order (data_transforms.py:109-125, :256-281)
-        uint2 v = make_uint2(0, 0);
+        float v0 = 0.f, v1 = 0.f, v2 = 0.f;
         if (stage[u] != 0xffffffffu) {
           float c0 = static_cast<float>(stage[u] & 0xff), c1 = static_cast<float>((stage[u] >> 8) & 0xff),
                 c2 = static_cast<float>((stage[u] >> 16) & 0xff);
           if (p.bgr) { const float t = c0; c0 = c2; c2 = t; }
-          const float v0 = (c0 / 255.0f - p.mean[0]) / p.std[0];
-          const float v1 = (c1 / 255.0f - p.mean[1]) / p.std[1];
-          const float v2 = (c2 / 255.0f - p.mean[2]) / p.std[2];
-          v.x = static_cast<uint32_t>(f32_to_bf16(v0)) | (static_cast<uint32_t>(f32_to_bf16(v1)) << 16);
-          v.y = static_cast<uint32_t>(f32_to_bf16(v2));
+          v0 = (c0 / 255.0f - p.mean[0]) / p.std[0];
+          v1 = (c1 / 255.0f - p.mean[1]) / p.std[1];
+          v2 = (c2 / 255.0f - p.mean[2]) / p.std[2];
         }
-        *reinterpret_cast<uint2*>(patch + i * 4) = v;
+        if constexpr (X6) {
+          *reinterpret_cast<float4*>(patch + i * 4) = make_float4(v0, v1, v2, 0.f);
+        } else {
+          uint2 v = make_uint2(0, 0);
+          if (stage[u] != 0xffffffffu) {
+            v.x = static_cast<uint32_t>(f32_to_bf16(v0)) | (static_cast<uint32_t>(f32_to_bf16(v1)) << 16);
+            v.y = static_cast<uint32_t>(f32_to_bf16(v2));
+          }
+          *reinterpret_cast<uint2*>(patch + i * 4) = v;
+        }
       } else {
-        *reinterpret_cast<uint4*>(patch + i * 8) = stage[u];
+        *reinterpret_cast<uint4*>(patch + i * EPU) = stage[u];
       }
     }
   };
@@ -137,7 +167,6 @@ patch_conv_kernel(const drnmi_conv_args p) {
     pcol[q] = (idx % TC) * S;
   }
   const int kq = lane >> 4;
-  bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(p.y);
 
   int b = blockIdx.x;
   if (b < ntiles) load_tile(b);
@@ -157,30 +186,51 @@ patch_conv_kernel(const drnmi_conv_args p) {
     for (int ks = 0; ks < C::NK; ++ks) {
 #pragma unroll
       for (int q = 0; q < C::PFW; ++q) {
-        bf16x8 bv;
+        // the lane's 8 K elements of this pixel fragment: 16 B (bf16) or 32 B (fp32) of the patch
+        const PT* src = nullptr;
         if constexpr (SRC_U8) {
           // k = kh*32 + kw*4 + c: step ks = kernel row kh, fragment = taps kw = 2kq, 2kq+1
-          const bf16_t* src = patch + ((prow[q] + ks) * C::PC + pcol[q] + 2 * kq) * 4;
-          const uint2 lo = *reinterpret_cast<const uint2*>(src);
-          const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
-          const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          bv = __builtin_bit_cast(bf16x8, u);
+          src = patch + ((prow[q] + ks) * C::PC + pcol[q] + 2 * kq) * 4;
         } else {
           const int k0 = ks * 32 + 8 * kq;
           const int tap = k0 / CIN;
           const int ci = k0 % CIN;
           if (tap < KS * KS) {
             const int kh = tap / KS, kw = tap % KS;
-            const uint4 u = *reinterpret_cast<const uint4*>(
-                patch + ((prow[q] + kh) * C::PC + pcol[q] + kw) * CIN + ci);
-            bv = __builtin_bit_cast(bf16x8, u);
-          } else {
-            bv = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+            src = patch + ((prow[q] + kh) * C::PC + pcol[q] + kw) * CIN + ci;
           }
         }
+        if constexpr (X6) {
+          float4 lo = make_float4(0.f, 0.f, 0.f, 0.f), hi = lo;
+          if (src != nullptr) {
+            lo = *reinterpret_cast<const float4*>(src);
+            hi = *reinterpret_cast<const float4*>(src + 4);
+          }
+          bf16x8 b1, b2, b3;
+          split3(lo, hi, b1, b2, b3);
 #pragma unroll
-        for (int mf = 0; mf < C::MF; ++mf)
-          acc[mf][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[mf][ks], bv, acc[mf][q], 0, 0, 0);
+          for (int mf = 0; mf < C::MF; ++mf) {
+            f32x4 a = acc[mf][q];
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[2][mf][ks], b1, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][mf][ks], b2, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][mf][ks], b3, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[1][mf][ks], b1, a, 0, 0, 0);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][mf][ks], b2, a, 0, 0, 0);
+            acc[mf][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][mf][ks], b1, a, 0, 0, 0);
+          }
+        } else {
+          bf16x8 bv = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+          if constexpr (SRC_U8) {
+            const uint2 lo = *reinterpret_cast<const uint2*>(src);
+            const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
+            bv = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+          } else if (src != nullptr) {
+            bv = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(src));
+          }
+#pragma unroll
+          for (int mf = 0; mf < C::MF; ++mf)
+            acc[mf][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[0][mf][ks], bv, acc[mf][q], 0, 0, 0);
+        }
       }
     }
 
@@ -204,10 +254,14 @@ patch_conv_kernel(const drnmi_conv_args p) {
           v[j] = acc[mf][q][j] * (p.scale != nullptr ? p.scale[co + j] : 1.f) + p.shift[co + j];
           if (p.relu) v[j] = fmaxf(v[j], 0.f);
         }
-        uint2 o;
-        o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
-        o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
-        *reinterpret_cast<uint2*>(y + base + co) = o;
+        if constexpr (X6) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.y) + base + co) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          uint2 o;
+          o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+          o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.y) + base + co) = o;
+        }
       }
     }
   }
@@ -550,10 +604,10 @@ stem_dma_kernel(const drnmi_conv_args p) {
 
 int g_num_cus = 0;
 
-template <int CIN, int COUT, int KS, int S, int TR, int TC, bool SRC_U8>
+template <int CIN, int COUT, int KS, int S, int TR, int TC, bool SRC_U8, bool X6 = false>
 hipError_t launch_patch(const drnmi_conv_args& p, hipStream_t s) {
   static int per_cu = 0;
-  auto kern = patch_conv_kernel<CIN, COUT, KS, S, TR, TC, SRC_U8>;
+  auto kern = patch_conv_kernel<CIN, COUT, KS, S, TR, TC, SRC_U8, X6>;
   if (per_cu == 0) {
     int dev = 0, cus = 0, blocks = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -632,7 +686,29 @@ static bool stem_dma_ok(const drnmi_conv_args& p) {
          static_cast<int64_t>(p.n) * p.ho * p.wo * 16 * 2 < (int64_t(1) << 31) && p.pad == 3 && p.w >= 8;
 }
 
+// fp32x (DRNMI_F32X3 in, fp32 NHWC out): the full-resolution small-channel layers
+static int patch_x6_dispatch(const drnmi_conv_args& p, hipStream_t s) {
+  if (p.out_dtype != DRNMI_F32 || p.dil != 1 || p.res != nullptr || p.y_sc != 1 || p.y_sp != p.cout)
+    return DRNMI_ENOTSUP;
+  hipError_t e;
+  if (p.src_u8) {
+    if (p.cin != 4 || p.cout != 16 || p.ks != 7 || p.stride != 1 || p.k != 224 || p.k_pad != 224)
+      return DRNMI_ENOTSUP;
+    e = launch_patch<4, 16, 7, 1, 4, 64, true, true>(p, s);
+  } else if (p.cin == 8 && p.cout == 16 && p.ks == 7 && p.stride == 1) {
+    e = launch_patch<8, 16, 7, 1, 4, 64, false, true>(p, s);
+  } else if (p.cin == 16 && p.cout == 16 && p.ks == 3 && p.stride == 1) {
+    e = launch_patch<16, 16, 3, 1, 4, 64, false, true>(p, s);
+  } else if (p.cin == 16 && p.cout == 32 && p.ks == 3 && p.stride == 2) {
+    e = launch_patch<16, 32, 3, 2, 4, 32, false, true>(p, s);
+  } else {
+    return DRNMI_ENOTSUP;
+  }
+  return static_cast<int>(e);
+}
+
 int patch_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
+  if (p.dtype == DRNMI_F32X3) return patch_x6_dispatch(p, s);
   if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.dil != 1 || p.res != nullptr) return DRNMI_ENOTSUP;
   if (p.y_sc != 1 || p.y_sp != p.cout) return DRNMI_ENOTSUP;            // packed NHWC output
   hipError_t e;
@@ -659,6 +735,13 @@ int patch_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
 }
 
 const char* patch_conv_name(const drnmi_conv_args& p) {
+  if (p.dtype == DRNMI_F32X3) {
+    if (p.src_u8) return "patch_conv_kernel<4, 16, 7, 1, 4, 64, true, true>";
+    if (p.cin == 8 && p.cout == 16 && p.ks == 7) return "patch_conv_kernel<8, 16, 7, 1, 4, 64, false, true>";
+    if (p.cin == 16 && p.cout == 16 && p.ks == 3) return "patch_conv_kernel<16, 16, 3, 1, 4, 64, false, true>";
+    if (p.cin == 16 && p.cout == 32 && p.ks == 3) return "patch_conv_kernel<16, 32, 3, 2, 4, 32, false, true>";
+    return nullptr;
+  }
   if (p.src_u8) return stem_dma_ok(p) ? "stem_dma_kernel" : "patch_conv_kernel<4, 16, 7, 1, 4, 64, true>";
   if (p.cin == 8 && p.cout == 16 && p.ks == 7) return "patch_conv_kernel<8, 16, 7, 1, 4, 64, false>";
   if (p.cin == 16 && p.cout == 16 && p.ks == 3 && p.stride == 1)

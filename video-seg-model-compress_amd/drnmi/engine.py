@@ -45,6 +45,8 @@ INT8_MIN_CIN = 64
 # (cin_stride, cout, ks, stride, dil) served by the LDS-patch kernel (bf16 only; include/drnmi.h)
 # (32 -> 64 stride 2 runs faster on the K-32 LDS-DMA implicit GEMM: 67 vs 108 us per 4 frames)
 PATCH_SHAPES = {(8, 16, 7, 1, 1), (16, 16, 3, 1, 1), (16, 32, 3, 2, 1)}
+# fp32x: the same full-resolution layers on the split-bf16 patch kernel (fp32 in / out)
+X6_PATCH_SHAPES = PATCH_SHAPES
 STEM_U8_K = 224     # fused u8 stem: k = kh*32 + kw*4 + c
 
 
@@ -268,7 +270,8 @@ class PackedNet:
                 if ni in self.i8_nodes:
                     self._pack_int8(nd, full, scale, cout)
                     continue
-                if self.precision == "fp32x" and cs >= X6_MIN_CIN and kh in (1, 3):
+                if self.precision == "fp32x" and ((cs >= X6_MIN_CIN and kh in (1, 3)) or
+                                                  _uses_patch(nd, cs, "fp32x")):
                     nd.x6 = True
                     nd.wpk = split3_bf16(full)
                     nd.scale_folded = False
@@ -286,12 +289,13 @@ class PackedNet:
             self.stem_u8_w = None
             stem = self.graph.nodes[0]
             w = stem.conv.weight.detach().to(self.device, torch.float32)
-            if self.base == "bf16" and tuple(w.shape[1:]) == (3, 7, 7):
+            if self.base in ("bf16", "fp32x") and tuple(w.shape[1:]) == (3, 7, 7) and \
+                    _uses_patch(stem, self.cstride["input"], self.base):
                 wp = torch.zeros(w.shape[0], 7, 8, 4, device=self.device, dtype=torch.float32)
                 wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
                 full = torch.zeros(stem.cout_pad, STEM_U8_K, device=self.device, dtype=torch.float32)
                 full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
-                self.stem_u8_w = full.to(self.tdtype).contiguous()
+                self.stem_u8_w = split3_bf16(full) if self.base == "fp32x" else full.to(self.tdtype).contiguous()
 
 
     def _pack_int8(self, nd: ConvNode, full: torch.Tensor, bn_scale: torch.Tensor, cout: int):
@@ -354,7 +358,9 @@ def _uses_patch(nd: ConvNode, cin_stride: int, precision: str) -> bool:
         return False
     c = nd.conv
     shape = (cin_stride, c.out_channels, c.kernel_size[0], c.stride[0], c.dilation[0])
-    return precision == "bf16" and shape in PATCH_SHAPES and nd.res is None and not nd.out_fp32_nchw
+    if nd.res is not None or nd.out_fp32_nchw:
+        return False
+    return (precision == "bf16" and shape in PATCH_SHAPES) or (precision == "fp32x" and shape in X6_PATCH_SHAPES)
 
 
 def _fused_init_route(nd: ConvNode, cin_stride: int) -> bool:
