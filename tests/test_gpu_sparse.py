@@ -1,7 +1,9 @@
 """Block-sparse MFMA path (north_star: "MFMA used only on the dense-within-block sub-tiles of the
-block-sparse weights"): pruned 16 x 32 weight units skip their MFMAs.  Parity gate: the sparse
-launch is BIT-IDENTICAL to the dense kernel on the same (masked) weights — a skipped unit only
-ever contributed exact zeros — and the masked model matches the oracle like any dense one."""
+block-sparse weights"): K steps whose weight slice is all zero for a whole output-channel tile
+(pruned blocks covering the tile's rows) are dropped -- no weight DMA, no pixel gather, no MFMA.
+Parity gate: the sparse launch is BIT-IDENTICAL to the dense kernel on the same (masked) weights
+-- a dropped step only ever contributed exact zeros -- and the masked model matches the oracle
+like any dense one."""
 import json
 import os
 
@@ -34,19 +36,22 @@ def pruned_model(arch, seed, cfg):
     return m.to(DEV).eval()
 
 
-def conv_layers(m, min_cin=16):
+def conv_layers(m, min_cin=16, bh=16, bw=1):
     return [k for k, v in m.state_dict().items() if k.startswith("layer.") and k.endswith(".weight")
-            and v.dim() == 4 and v.shape[1] >= min_cin and v.shape[0] % 16 == 0]
+            and v.dim() == 4 and v.shape[1] >= min_cin and v.shape[0] % bh == 0 and v.shape[1] % bw == 0]
 
 
 def block_cfg(m, bh, bw, sp):
-    return {"pruner_type": "block", "configs": [{"layer_set": conv_layers(m), "sparsity": sp, "block_height": bh,
+    return {"pruner_type": "block", "configs": [{"layer_set": conv_layers(m, bh=bh, bw=bw), "sparsity": sp,
+                                                 "block_height": bh,
                                                  "block_width": bw, "sub_rows": -1, "sub_cols": -1,
                                                  "collapse_tensor": False}]}
 
 
 @pytest.mark.parametrize("arch,bh,bw,shape", [("drn_d_38", 16, 16, (2, 3, 128, 256)),
-                                              ("drn_d_22", 16, 32, (1, 3, 256, 256))])
+                                              ("drn_d_22", 16, 32, (1, 3, 256, 256)),
+                                              ("drn_d_38", 256, 64, (2, 3, 128, 256)),
+                                              ("drn_d_22", 128, 64, (1, 3, 200, 264))])
 def test_sparse_bit_identical_to_dense(arch, bh, bw, shape, monkeypatch):
     from drnmi.drnseg import DRNSeg
     probe = DRNSeg(arch, 19, pretrained=False)

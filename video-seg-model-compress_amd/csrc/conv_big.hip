@@ -101,6 +101,24 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
+// index of the n-th set bit of m (n < popcount(m)): binary search on popcounts
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int n) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t low = m & ((uint64_t(1) << w) - 1);
+    const int c = __popcll(low);
+    if (n >= c) {
+      n -= c;
+      m >>= w;
+      pos += w;
+    } else {
+      m = low;
+    }
+  }
+  return pos;
+}
+
 __device__ __forceinline__ int xcd_remap2(int bid, int nwg) {
   const int q = nwg / 8, r = nwg % 8;
   const int xcd = bid % 8;
@@ -464,31 +482,46 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   int px0 = (tile / nco) * kBPX;
   int co0 = (tile % nco) * C::BCO;
   setup(px0, co0);
-  auto live_bits = [&](int kt) -> uint32_t {
-    const int ku0 = step_params(kt).k0 >> 5;
-    const int wpr = (p.k_pad + 1023) >> 10;                 // mask words per row-block
-    uint32_t bits = 0;
-#pragma unroll
-    for (int fm = 0; fm < C::FM; ++fm) {
-      const int rb = (co0 + wc * WCO + fm * 16) >> 4;
-      const uint32_t word = __builtin_amdgcn_readfirstlane(p.unit_mask[rb * wpr + (ku0 >> 5)]);
-      bits |= ((word >> (ku0 & 31)) & ((1u << C::SUB) - 1)) << (fm * C::SUB);
-    }
-    return bits;
+  // SPARSE: K-step compaction.  A K step whose weight slice (all BCO rows of this tile x BK
+  // packed columns) is zero -- a pruned block covering the tile's rows, BlockPruner.py:139-241 --
+  // is dropped entirely: no weight DMA, no pixel-row gather, no MFMA.  Lane q holds the K-step
+  // id of live position q (lst0) and q + 64 (lst1), built once per tile from two ballots; a
+  // position's step is then a readlane (positions are wave-uniform).  nk <= 128 (dispatch).
+  int nlive = nk;
+  int lst0 = lane, lst1 = lane + 64;
+  if constexpr (SPARSE) {
+    const int wpr = (p.k_pad + 1023) >> 10;
+    auto step_live = [&](int kt) -> bool {
+      if (kt >= nk) return false;
+      const int u0 = step_params(kt).k0 >> 5;
+      bool any = false;
+      for (int rb = co0 >> 4; rb < (co0 + C::BCO) >> 4; ++rb)
+        any |= ((p.unit_mask[rb * wpr + (u0 >> 5)] >> (u0 & 31)) & ((1u << C::SUB) - 1)) != 0;
+      return any;
+    };
+    const uint64_t b0 = __ballot(step_live(lane)), b1 = __ballot(step_live(lane + 64));
+    const int c0 = __popcll(b0), c1 = __popcll(b1);
+    nlive = __builtin_amdgcn_readfirstlane(c0 + c1);   // wave-uniform trip count (scalar loop)
+    // position q -> K step: the q-th live step of b0, then of b1
+    const int q1 = 64 + lane - c0;                       // b1 index of position 64 + lane
+    lst0 = lane < c0 ? nth_set_bit(b0, lane) : (lane - c0 < c1 ? 64 + nth_set_bit(b1, lane - c0) : 0);
+    lst1 = q1 < c1 ? 64 + nth_set_bit(b1, q1) : 0;
+  }
+  auto kt_at = [&](int pos) -> int {
+    if constexpr (!SPARSE) return pos;
+    return pos < 64 ? __builtin_amdgcn_readlane(lst0, pos) : __builtin_amdgcn_readlane(lst1, pos - 64);
   };
-  uint32_t live_next = 0xffffffffu;
   constexpr bool DEFER = NWP < 4;
   if constexpr (K::ESZ == 2) init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
   else zero_tile(acc);
-  for (int t = 0; t < NST - 1 && t < nk; ++t) issue(t, t);
+  for (int t = 0; t < NST - 1 && t < nlive; ++t) issue(kt_at(t), t);
 
   while (true) {
-    if constexpr (SPARSE) live_next = live_bits(0);
-
-    for (int t = 0; t < nk; ++t) {
+    // t runs over the (live) K-step positions; kt_at(t) is the K step itself
+    for (int t = 0; t < nlive; ++t) {
       const int cur = t % NST;
-      // retire step t: the steps issued after it (min(nk-1, t+NST-2) - t) may stay in flight
-      const int newer = ((nk - 1) < (t + NST - 2) ? (nk - 1) : (t + NST - 2)) - t;
+      // retire step t: the steps issued after it (min(nlive-1, t+NST-2) - t) may stay in flight
+      const int newer = ((nlive - 1) < (t + NST - 2) ? (nlive - 1) : (t + NST - 2)) - t;
       if (NST >= 4 && newer >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * C::GLDS) : "memory");
       else if (NST >= 3 && newer >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::GLDS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -498,24 +531,13 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       const char* sa = smem + cur * C::STAGE;
       const char* sb = sa + C::A_BYTES;
       constexpr int NG = C::SUB * C::GR;
-      // block sparsity: bit (fm * SUB + sub) = unit (row-block of fragment fm, K unit of substep
-      // sub) has a nonzero weight; wave-uniform (scalar loads, scalar branches).  The bits of step
-      // t+1 are loaded while step t computes.
-      uint32_t live = 0xffffffffu;
-      if constexpr (SPARSE) {
-        live = live_next;
-        if (t + 1 < nk) live_next = live_bits(t + 1);
-      }
       constexpr int PPG = (C::GLDS + C::GR - 1) / C::GR;   // DMA pieces per group (first substep)
-      const bool nxt = (DRNMI_ABLATE & 1) ? false : (DRNMI_PIN ? true : t + NST - 1 < nk);
-      const StepP sp = step_params(DRNMI_PIN ? (t + NST - 1 < nk ? t + NST - 1 : nk - 1) : t + NST - 1);
+      const bool nxt = (DRNMI_ABLATE & 1) ? false : (DRNMI_PIN ? true : t + NST - 1 < nlive);
+      const StepP sp = step_params(kt_at(t + NST - 1 < nlive ? t + NST - 1 : nlive - 1));
       const int nst = (t + NST - 1) % NST;
       constexpr int PFD = DRNMI_PFD;
       constexpr int NAF = PFD + 1;               // A-fragment ring depth
       typename K::frag af[NAF][C::FPG], bfr[2][C::FN];
-      auto unit_live = [&](int q, int h) {
-        return !SPARSE || ((live >> ((((q % C::GR) * C::FPG + h) * C::SUB) + q / C::GR)) & 1u) != 0;
-      };
       auto load_a = [&](typename K::frag (&dst)[C::FPG], int q) {
         const int c = (q / C::GR) * 4 + fq;
 #pragma unroll
@@ -561,7 +583,6 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         } else {
 #pragma unroll
         for (int h = 0; h < C::FPG; ++h) {
-          if (!unit_live(q, h)) continue;        // all-zero 16 x 32 weight unit: no MFMA
 #pragma unroll
           for (int fn = 0; fn < C::FN; ++fn)
             acc[(q % C::GR) * C::FPG + h][fn] = K::mma(
@@ -1067,7 +1088,7 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   }
   const int base = variant % 6;
   const bool persist = variant >= 6;
-  if (p.unit_mask != nullptr && !persist && sparse_name(p.ks, base) != nullptr) {
+  if (p.unit_mask != nullptr && !persist && sparse_name(p.ks, base) != nullptr && p.k_pad / v.bk <= 128) {
     e = p.ks == 3 ? launch_sparse<3>(p, base, s) : launch_sparse<1>(p, base, s);
     return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
   }
@@ -1080,7 +1101,9 @@ const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_name(p);
   if (variant < 0) variant = auto_variant(p);
   if (variant >= kNumVariants) return nullptr;
-  if (p.unit_mask != nullptr && variant < 6 && sparse_name(p.ks, variant) != nullptr) return sparse_name(p.ks, variant);
+  if (p.unit_mask != nullptr && variant < 6 && sparse_name(p.ks, variant) != nullptr &&
+      p.k_pad / kVariants[variant].bk <= 128)
+    return sparse_name(p.ks, variant);
   return p.ks == 3 ? kVariants[variant].name3 : kVariants[variant].name1;
 }
 
