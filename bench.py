@@ -203,10 +203,12 @@ def main():
         return lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
 
     names = [launched_name(i) for i in range(len(plan.args))]
-    # useful work of block-sparse launches: dense FLOPs x (1 - fraction of skipped zero units)
+    # useful work of a pruned layer: dense FLOPs x the density of its weights, on
+    # dense and sparse kernels alike (the dense kernel multiplies the zeros too)
     nodes = plan.packed.graph.nodes
-    works = [(w[0], w[1] * (1.0 - nodes[i].zero_unit_frac if nodes[i].unit_mask is not None else 1.0), w[2])
-             if i < len(nodes) else w for i, w in enumerate(works)]
+    density = [float((nd.conv.weight != 0).sum()) / nd.conv.weight.numel() for nd in nodes]
+    dense_flops = {i: w[1] for i, w in enumerate(works)}
+    works = [(w[0], w[1] * density[i], w[2]) if i < len(nodes) else w for i, w in enumerate(works)]
     events = []
     pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * len(names) * args.steps)]
 
@@ -244,9 +246,10 @@ def main():
         if before:
             pend[i] = ev
         else:
-            g_ = per.setdefault(names[i], {"d": [], "f": [], "b": []})
+            g_ = per.setdefault(names[i], {"d": [], "f": [], "b": [], "fd": []})
             g_["d"].append(pend.pop(i).elapsed_time(ev) * 1e-3)
             g_["f"].append(works[i][1])
+            g_["fd"].append(dense_flops[i])
             g_["b"].append(works[i][2])
     dominant = max(per, key=lambda k: sum(per[k]["d"])) if per else None
     durs = per[dominant]["d"] if dominant else []
@@ -274,12 +277,14 @@ def main():
                    "global_batch": B * world, "parallelism": f"dp{world} (frames sharded, no data-path collective)"},
     }
     if args.prune:
-        sparse = [nd for nd in plan.packed.graph.nodes if nd.unit_mask is not None]
+        sparse = [i for i, nm in enumerate(names) if nm.startswith("conv_big_kernel") and nm.endswith("true>")]
         out["config"]["workload"] = out["config"]["workload"].replace("dense inference", f"{args.prune} pruned inference")
         out["config"]["block_sparse"] = {"pruned_layers": n_pruned, "sparse_launches": len(sparse),
-                                         "mean_zero_unit_frac": round(sum(nd.zero_unit_frac for nd in sparse)
-                                                                      / max(len(sparse), 1), 4),
-                                         "kernels": "unit-skipping" if args.block_sparse else "dense"}
+                                         "mean_weight_density_of_sparse_launches":
+                                             round(sum(density[i] for i in sparse) / max(len(sparse), 1), 4),
+                                         "kernels": "K-step compaction" if args.block_sparse else "dense",
+                                         "flops": "useful (dense x weight density); dense-equivalent in "
+                                                  "roofline.dense_equivalent_achieved"}
     traffic, traffic_src = pmc_traffic(args, dominant) if durs else (None, None)
     if durs:
         avg_d = sum(durs) / len(durs)
@@ -289,6 +294,7 @@ def main():
         out["roofline"] = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 2), "peak": peak,
                            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
                            "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                           "dense_equivalent_achieved": round(sum(per[dominant]["fd"]) / len(durs) / avg_d / 1e12, 2),
                            "launches": len(durs), "avg_launch_us": round(avg_d * 1e6, 2),
                            "avg_launch_gflop": round(avg_f / 1e9, 3),
                            "share_of_step": round(sum(durs) / el, 3)}
