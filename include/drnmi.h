@@ -171,6 +171,26 @@ int drnmi_up8_bilinear_logsoftmax_argmax(const float* logits, float* logprobs, v
                                          int32_t label_dtype, int32_t n, int32_t c, int32_t h, int32_t w,
                                          void* stream);
 
+/* Bilinear resize with Pillow's arithmetic (Image.resize(size, BILINEAR): separable, horizontal
+ * pass first, the filter support widened by the downscale factor; coefficient tables computed on
+ * the device exactly as Pillow's precompute_coeffs).  Bit-identical to Pillow 12.
+ *   drnmi_resize_bilinear_u8: uint8 HWC3 frames [n][h][w][3] -> [n][oh][ow][3]; 8-bit fixed point
+ *     with 22 fractional bits and a uint8 intermediate (Pillow's 8bpc path).  Replaces
+ *     T.Resize((300, 300)) on each decoded frame (seg_video_old_no_plot.py:126-127).
+ *   drnmi_resize_bilinear_f32: fp32 planes [planes][h][w] -> [planes][oh][ow]; fp32 x double
+ *     summed in double, fp32 intermediate (Pillow's 'F' mode).  accumulate != 0: dst += result in
+ *     fp32.  Replaces resize_4d_tensor + the scale sum of test_ms (semantic_seg.py:471-504, :540).
+ *   ws: device workspace of drnmi_resize_workspace_bytes(n or planes, h, w, oh, ow, 3 or 4) bytes.
+ *   drnmi_argmax_nchw_f32: labels[n][p] = first index of the max over c of x[n][c][p] (numpy
+ *     argmax(axis=1), semantic_seg.py:543), uint8 or int64 labels. */
+int64_t drnmi_resize_workspace_bytes(int32_t n, int32_t h, int32_t w, int32_t oh, int32_t ow, int32_t elem_bytes);
+int drnmi_resize_bilinear_u8(const uint8_t* src, int32_t n, int32_t h, int32_t w, uint8_t* dst, int32_t oh, int32_t ow,
+                             void* ws, int64_t ws_bytes, void* stream);
+int drnmi_resize_bilinear_f32(const float* src, int32_t planes, int32_t h, int32_t w, float* dst, int32_t oh,
+                              int32_t ow, int32_t accumulate, void* ws, int64_t ws_bytes, void* stream);
+int drnmi_argmax_nchw_f32(const float* x, int32_t n, int32_t c, int64_t hw, void* labels, int32_t label_dtype,
+                          void* stream);
+
 /* Multi-tensor in-place mask apply: w[t][i] *= m[t][i] for every tensor t.
  * Replaces Pruner.apply_masks (pruners/Pruner.py:17-20, same body BlockPruner.py:27-30,
  * SRMBRepMasker.py:20-23): one launch for all masked layers instead of one ATen mul_ per

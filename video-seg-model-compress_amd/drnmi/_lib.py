@@ -72,6 +72,10 @@ SIGNATURES = {
     "drnmi_nhwc_to_nchw": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_up8_logsoftmax_argmax": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_up8_bilinear_logsoftmax_argmax": (ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
+    "drnmi_resize_workspace_bytes": (ctypes.c_int64, [_I32, _I32, _I32, _I32, _I32, _I32]),
+    "drnmi_resize_bilinear_u8": (ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _I32, _I32, _VP, _I64, _VP]),
+    "drnmi_resize_bilinear_f32": (ctypes.c_int, [_VP, _I32, _I32, _I32, _VP, _I32, _I32, _I32, _VP, _I64, _VP]),
+    "drnmi_argmax_nchw_f32": (ctypes.c_int, [_VP, _I32, _I32, _I64, _VP, _I32, _VP]),
     "drnmi_mask_apply_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP]),
     "drnmi_mask_apply_bits_f32": (ctypes.c_int, [_I32, _VP, _VP, _VP, _VP]),
     "drnmi_confusion_matrix": (ctypes.c_int, [_VP, _I32, _VP, _I32, _I64, _I32, _VP, _VP]),

@@ -122,15 +122,21 @@ class DRNSeg(nn.Module):
         return torch.ops.drnmi.predict(x, self._handle)
 
     def segment(self, frames_u8: torch.Tensor, mean=INFO_MEAN, std=INFO_STD, bgr: bool = False,
-                labels: torch.Tensor | None = None) -> torch.Tensor:
+                labels: torch.Tensor | None = None, size=None) -> torch.Tensor:
         """Video path: uint8 HWC frames [B,H,W,3] on the GPU -> uint8 label maps [B,8h,8w].
 
         Fuses ToTensorVideoImage + Normalize (data_transforms.py:256-281, :109-125) into the
         ingest kernel and model(img)[0] + torch.max(final,1) into the head kernel.  Runs as
-        torch.ops.drnmi.segment (graph-capturable); `labels=` writes into a caller buffer."""
+        torch.ops.drnmi.segment (graph-capturable); `labels=` writes into a caller buffer.
+        size=(oh, ow): first resize the frames on the GPU exactly as seg_video's
+        T.Resize((300, 300)) does on each PIL frame (seg_video_old_no_plot.py:126-127;
+        Pillow BILINEAR arithmetic, drnmi_resize_bilinear_u8)."""
         if frames_u8.dtype != torch.uint8 or frames_u8.dim() != 4 or frames_u8.shape[3] != 3:
             raise ValueError("segment expects uint8 [B,H,W,3] frames")
         self._check_device(frames_u8)
+        if size is not None and tuple(size) != tuple(frames_u8.shape[1:3]):
+            from .ops import resize_bilinear_u8
+            frames_u8 = resize_bilinear_u8(frames_u8, size)
         if labels is not None:
             return self._segment_impl(frames_u8, mean, std, bgr, labels)
         return torch.ops.drnmi.segment(frames_u8, self._handle, [float(v) for v in mean],

@@ -153,3 +153,62 @@ def stem_u8(frames_u8: torch.Tensor, weight: torch.Tensor, scale, shift, mean, s
     lib = _lib.load()
     _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr(dev))), "stem_u8")
     return y
+
+
+def resize_bilinear_u8(frames_u8: torch.Tensor, size) -> torch.Tensor:
+    """uint8 HWC3 frames [N,H,W,3] -> [N,oh,ow,3] with Pillow's Image.resize(BILINEAR) arithmetic,
+    bit-identical (T.Resize((300, 300)) of seg_video_old_no_plot.py:126-127).  size = (oh, ow)."""
+    n, h, w, c = frames_u8.shape
+    if frames_u8.dtype != torch.uint8 or c != 3:
+        raise ValueError("resize_bilinear_u8 expects uint8 [N,H,W,3] frames")
+    oh, ow = int(size[0]), int(size[1])
+    lib = _lib.load()
+    nbytes = lib.drnmi_resize_workspace_bytes(n, h, w, oh, ow, 3)
+    if nbytes < 0:
+        raise ValueError("resize_bilinear_u8: bad sizes")
+    dev = frames_u8.device
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    out = torch.empty(n, oh, ow, 3, dtype=torch.uint8, device=dev)
+    _lib.check(lib.drnmi_resize_bilinear_u8(frames_u8.contiguous().data_ptr(), n, h, w, out.data_ptr(), oh, ow,
+                                            ws.data_ptr(), nbytes, ctypes.c_void_p(_lib.stream_ptr(dev))),
+               "resize_bilinear_u8")
+    return out
+
+
+def resize_bilinear_f32(planes: torch.Tensor, size, out: torch.Tensor | None = None,
+                        accumulate: bool = False) -> torch.Tensor:
+    """fp32 [..., H, W] planes -> [..., oh, ow] with Pillow's 'F'-mode Image.resize(BILINEAR)
+    arithmetic (resize_4d_tensor, semantic_seg.py:471-504); accumulate: out += resized."""
+    *lead, h, w = planes.shape
+    if planes.dtype != torch.float32:
+        raise ValueError("resize_bilinear_f32 expects fp32 planes")
+    oh, ow = int(size[0]), int(size[1])
+    npl = 1
+    for d in lead:
+        npl *= d
+    dev = planes.device
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs out=")
+        out = torch.empty(*lead, oh, ow, dtype=torch.float32, device=dev)
+    elif tuple(out.shape) != (*lead, oh, ow) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous fp32 tensor of the resized shape")
+    lib = _lib.load()
+    nbytes = lib.drnmi_resize_workspace_bytes(npl, h, w, oh, ow, 4)
+    if nbytes < 0:
+        raise ValueError("resize_bilinear_f32: bad sizes")
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    _lib.check(lib.drnmi_resize_bilinear_f32(planes.contiguous().data_ptr(), npl, h, w, out.data_ptr(), oh, ow,
+                                             1 if accumulate else 0, ws.data_ptr(), nbytes,
+                                             ctypes.c_void_p(_lib.stream_ptr(dev))), "resize_bilinear_f32")
+    return out
+
+
+def argmax_nchw(x: torch.Tensor, label_dtype=torch.int64) -> torch.Tensor:
+    """numpy x.argmax(axis=1) over fp32 NCHW (first maximum wins) -> [N,H,W] labels."""
+    n, c, h, w = x.shape
+    lab = torch.empty(n, h, w, dtype=label_dtype, device=x.device)
+    code = _lib.DRNMI_U8 if label_dtype == torch.uint8 else _lib.DRNMI_I64
+    _lib.check(_lib.load().drnmi_argmax_nchw_f32(x.contiguous().data_ptr(), n, c, h * w, lab.data_ptr(), code,
+                                                 ctypes.c_void_p(_lib.stream_ptr(x.device))), "argmax_nchw")
+    return lab

@@ -54,6 +54,7 @@ class Pruner:
         self.layer_configs = self.parse_config_file(config_fp)
         self._bits_cache = {}
         self._binary_cache = {}
+        self._factors = {}           # layer -> compact mask factors (SRMBRepMasker period tiles)
 
     # -- subclasses implement
     def parse_config_file(self, config_fp):  # pragma: no cover - abstract
@@ -63,6 +64,7 @@ class Pruner:
         t = torch.from_numpy(np.ascontiguousarray(mask))
         self.mask_dict[layer] = t.cuda() if self.on_gpu else t
         self._bits_cache.pop(layer, None)
+        self._factors.pop(layer, None)
 
     # -- the hot step
     def apply_masks(self, model, use_bits: bool = True):
@@ -129,39 +131,103 @@ class Pruner:
     # -- compact on-disk masks (the reference never persists masks,
     #    semantic_seg.py:1085-1092, so an SRMB run cannot be resumed with the same masks)
     def save_masks(self, path):
-        """Write mask_dict as 1 bit per weight (the apply kernel's word layout) to an .npz.
-
+        """Write mask_dict to an .npz in the most compact exact form per layer:
+          * SRMBRepMasker masks still equal to their generated factors: the factors -- OB and the
+            period tile P as bits plus the block sizes (kind 1), or the non-repetitive block
+            pattern OCP (kind 2); the whole mask is their kron (SRMBRepMasker.py:337-383).  All
+            factor bits of all layers share one word array, so a D-22 SRMB mask set is ~2 KB;
+          * any other mask: 1 bit per weight in the apply kernel's word layout (kind 0).
         Masks must be 0/1 valued (every reference pruner stores 0./1. floats); anything else
         raises ValueError rather than being silently binarised."""
+        layers = list(self.mask_dict)
         arrays = {"format": np.array([MASK_FORMAT_VERSION], dtype=np.int64),
-                  "layers": np.array(list(self.mask_dict), dtype=np.str_)}
+                  "layers": np.array(layers, dtype=np.str_)}
+        shapes = np.ones((len(layers), 4), dtype=np.int64)
+        ndims = np.zeros(len(layers), dtype=np.int64)
+        dtypes = []
+        meta = np.zeros((len(layers), 12), dtype=np.int64)   # kind, ib(2), cb(2), A(2), B(2), offA, offB, 0
+        fwords, off = [], 0
         for i, (layer, m) in enumerate(self.mask_dict.items()):
             a = m.detach().cpu().numpy()
             nz = a != 0
             if not np.array_equal(a[nz], np.ones(int(nz.sum()), dtype=a.dtype)):
                 raise ValueError(f"{layer}: mask is not 0/1 valued; the bit format cannot hold it")
+            if a.ndim > 4:
+                raise ValueError(f"{layer}: masks of more than 4 dimensions are not supported")
+            ndims[i] = a.ndim
+            shapes[i, :a.ndim] = a.shape
+            dtypes.append(str(a.dtype))
+            fac = self._factors.get(layer)
+            if fac is not None and np.array_equal(SRMBRepMasker.expand_factors(fac) != 0, nz):
+                grids = [fac["ob"], fac["p"]] if fac["rep"] else [fac["ocp"]]
+                meta[i, 0] = 1 if fac["rep"] else 2
+                meta[i, 1:3] = fac["ib"]
+                if fac["rep"]:
+                    meta[i, 3:5] = fac["cb"]
+                for j, g in enumerate(grids):
+                    g = np.asarray(g)
+                    w = _pack_bits(g.reshape(-1) != 0)
+                    meta[i, 5 + 2 * j:7 + 2 * j] = g.shape
+                    meta[i, 9 + j] = off
+                    fwords.append(w)
+                    off += w.size
+                continue
             arrays[f"bits{i}"] = _pack_bits(nz.reshape(-1))
-            arrays[f"shape{i}"] = np.array(a.shape, dtype=np.int64)
-            arrays[f"dtype{i}"] = np.array([str(a.dtype)], dtype=np.str_)
+        arrays.update(shapes=shapes, ndims=ndims, dtypes=np.array(dtypes, dtype=np.str_), meta=meta,
+                      fwords=np.concatenate(fwords) if fwords else np.zeros(0, dtype=np.uint32))
         with open(path, "wb") as f:
             np.savez_compressed(f, **arrays)
 
     def load_masks(self, path):
-        """Restore mask_dict from save_masks() output; seeds the bit cache so the next
-        apply_masks uploads no fp32 mask at all."""
+        """Restore mask_dict from save_masks() output (format 1: bits only, or 2); seeds the bit
+        cache so the next apply_masks uploads no fp32 mask at all."""
         with np.load(path, allow_pickle=False) as z:
-            if int(z["format"][0]) != MASK_FORMAT_VERSION:
-                raise ValueError(f"{path}: mask format {int(z['format'][0])} != {MASK_FORMAT_VERSION}")
+            version = int(z["format"][0])
+            if version not in (1, MASK_FORMAT_VERSION):
+                raise ValueError(f"{path}: mask format {version} is not 1..{MASK_FORMAT_VERSION}")
             self.mask_dict = collections.OrderedDict()
             self._bits_cache = {}
             self._binary_cache = {}
+            self._factors = {}
+            fwords = z["fwords"] if version >= 2 else None
             for i, layer in enumerate(z["layers"].tolist()):
-                words, shape = z[f"bits{i}"], tuple(int(s) for s in z[f"shape{i}"])
+                if version >= 2:
+                    shape = tuple(int(v) for v in z["shapes"][i, :int(z["ndims"][i])])
+                    dt = str(z["dtypes"][i])
+                    meta = [int(v) for v in z["meta"][i]]
+                else:
+                    shape = tuple(int(v) for v in z[f"shape{i}"])
+                    dt = str(z[f"dtype{i}"][0])
+                    meta = [0] * 12
                 n = int(np.prod(shape))
-                if words.dtype != np.uint32 or words.size != (n + 31) // 32:
-                    raise ValueError(f"{path}: {layer}: {words.size} words for {n} weights")
-                mask = _unpack_bits(words, n).reshape(shape).astype(str(z[f"dtype{i}"][0]))
-                self._store(layer, mask)
+                kind = meta[0]
+                if kind in (1, 2):
+                    def grid(j):
+                        shp = (meta[5 + 2 * j], meta[6 + 2 * j])
+                        cnt = shp[0] * shp[1]
+                        w = fwords[meta[9 + j]:meta[9 + j] + (cnt + 31) // 32]
+                        if w.size != (cnt + 31) // 32:
+                            raise ValueError(f"{path}: {layer}: truncated factor words")
+                        return _unpack_bits(w, cnt).reshape(shp).astype(np.float64)
+                    fac = {"shape": shape, "dtype": dt, "ib": (meta[1], meta[2]), "rep": kind == 1}
+                    if kind == 1:
+                        fac.update(ob=grid(0), p=grid(1), cb=(meta[3], meta[4]))
+                    else:
+                        fac.update(ocp=grid(0).astype(dt))
+                    mask = SRMBRepMasker.expand_factors(fac)
+                    if mask.size != n:
+                        raise ValueError(f"{path}: {layer}: factors expand to {mask.size} weights, not {n}")
+                    self._store(layer, mask.astype(dt))
+                    self._factors[layer] = fac
+                    words = _pack_bits(mask.reshape(-1) != 0)
+                elif kind == 0:
+                    words = z[f"bits{i}"]
+                    if words.dtype != np.uint32 or words.size != (n + 31) // 32:
+                        raise ValueError(f"{path}: {layer}: {words.size} words for {n} weights")
+                    mask = _unpack_bits(words, n).reshape(shape).astype(dt)
+                    self._store(layer, mask)
+                else:
+                    raise ValueError(f"{path}: {layer}: unknown mask kind {kind}")
                 if self.on_gpu:
                     m = self.mask_dict[layer]
                     self._bits_cache[layer] = ((m.data_ptr(), m._version, str(m.device)),
@@ -175,7 +241,7 @@ class Pruner:
             print(layer, "sparsity = {}".format(sp * 100))
 
 
-MASK_FORMAT_VERSION = 1
+MASK_FORMAT_VERSION = 2   # 1: bits only; 2: + SRMB factor (period-tile) layers
 
 
 def _pack_bits(flat: np.ndarray) -> np.ndarray:
@@ -570,7 +636,9 @@ class SRMBRepMasker(Pruner):
     def generate_masks(self, model, is_static=True, verbose=False):
         sd = model.state_dict()
         for layer, c in self.layer_configs.items():
-            self._store(layer, SRMBRepMasker.construct_mask(sd[layer].detach().cpu().numpy(), c))
+            fac = SRMBRepMasker.mask_factors(sd[layer].detach().cpu().numpy(), c)
+            self._store(layer, SRMBRepMasker.expand_factors(fac))
+            self._factors[layer] = fac          # compact (period-tile) form for save_masks
             if verbose:
                 print("Generated mask for layer {}".format(layer))
 
@@ -712,6 +780,14 @@ class SRMBRepMasker(Pruner):
     @staticmethod
     def construct_mask(tensor, config):
         """mask = kron(kron(OB, kron(CB, P)), IB) (SRMBRepMasker.py:337-383)."""
+        return SRMBRepMasker.expand_factors(SRMBRepMasker.mask_factors(tensor, config))
+
+    @staticmethod
+    def mask_factors(tensor, config):
+        """The mask's Kronecker factors, drawing the RNG exactly as SRMBRepMasker.py:337-383 does:
+        repetitive masks are kron(kron(OB, kron(1(obh/cbh x obw/cbw), P)), 1(ibh x ibw*k)) -- an OB
+        pattern over a period tile P, so OB and P (bits) and the block sizes ARE the mask; the
+        non-repetitive form keeps its (rows/ibh x cols/ibw) block pattern OCP."""
         tensor = np.asarray(tensor)
         rows, cols = tensor.shape[0], tensor.shape[1]
         ks = tensor.size // (rows * cols)
@@ -725,13 +801,14 @@ class SRMBRepMasker(Pruner):
         ibh, ibw = config.ibh, config.ibw
         gen = SRMBRepMasker.generate_sparsity_pattern
         ob = gen(rows // obh, cols // obw, config.osp, config.opat, config.cross_prob, config.is_symmetric)
-        cb = np.ones((obh // cbh, obw // cbw), dtype=tensor.dtype)
-        ib = np.ones((ibh, ibw * ks), dtype=tensor.dtype)
+        fac = {"shape": tuple(tensor.shape), "dtype": str(tensor.dtype), "ib": (ibh, ibw * ks),
+               "rep": bool(config.is_repetitive)}
         if config.is_repetitive:
             p = gen(cbh // ibh, cbw // ibw, config.isp, config.ipat, config.cross_prob, config.is_symmetric)
-            m = np.kron(np.kron(ob, np.kron(cb, p)), ib)
-            return m.reshape(tensor.shape).astype(tensor.dtype)
+            fac.update(ob=ob, cb=(obh // cbh, obw // cbw), p=p)
+            return fac
         ocp = np.zeros((rows // ibh, cols // ibw), dtype=tensor.dtype)
+        cb = np.ones((obh // cbh, obw // cbw), dtype=tensor.dtype)
         snr, snc = obh // ibh, obw // ibw
         for rb in range(rows // obh):
             for cb_ in range(cols // obw):
@@ -739,7 +816,19 @@ class SRMBRepMasker(Pruner):
                     p = gen(cbh // ibh, cbw // ibw, config.isp, config.ipat, config.cross_prob,
                             config.is_symmetric)
                     ocp[rb * snr:(rb + 1) * snr, cb_ * snc:(cb_ + 1) * snc] += np.kron(cb, p)
-        return np.kron(ocp, ib).reshape(tensor.shape)
+        fac.update(ocp=ocp)
+        return fac
+
+    @staticmethod
+    def expand_factors(fac):
+        """The full weight-shaped mask from mask_factors() (the reference's kron, same dtypes)."""
+        dt = np.dtype(fac["dtype"])
+        ib = np.ones(fac["ib"], dtype=dt)
+        if fac["rep"]:
+            cb = np.ones(fac["cb"], dtype=dt)
+            m = np.kron(np.kron(fac["ob"], np.kron(cb, fac["p"])), ib)
+            return m.reshape(fac["shape"]).astype(dt)
+        return np.kron(fac["ocp"].astype(dt), ib).reshape(fac["shape"])
 
 
 __all__ = ["Pruner", "BlockPruner", "BlockPrunerConfig", "BlockMatrix", "RmbPruner", "RmbPrunerConfig",
