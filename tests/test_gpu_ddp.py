@@ -104,3 +104,41 @@ def test_ddp_two_ranks_average_gradients():
         assert e <= 1e-6, (k, e)
     assert np.array_equal(p0, p1)                         # parameters stay in lock-step
     print(f"DDP world 2: {nb} buckets, worst grad rel err vs mean of local grads {worst:.2e}")
+
+
+def _nccl_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "video-seg-model-compress_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    try:
+        from drnmi.parallel import DistributedDataParallel
+        m = _fresh_model().cuda(rank)
+        ddp = DistributedDataParallel(m, device_ids=[rank], bucket_cap_mb=8)
+        x, t = _inputs(rank)
+        loss = _loss(ddp(x.cuda(rank)), t.cuda(rank))
+        loss.backward()
+        grads = torch.cat([p.grad.detach().reshape(-1) for p in m.parameters() if p.grad is not None])
+        torch.cuda.synchronize()
+        q.put((rank, grads.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL DDP needs >= 2 GPUs (one per rank)")
+def test_ddp_nccl_two_gpus():
+    """The same DDP drop-in over the "nccl" (= RCCL over xGMI) backend, one process per GPU:
+    both ranks end with bitwise-identical averaged gradients."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_nccl_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=300) for _ in procs], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.array_equal(out[0][1], out[1][1])
