@@ -83,6 +83,14 @@ typedef struct drnmi_conv_args {
   /* scale must be non-NULL for int8.  Ignored for other dtypes.                             */
   float res_scale;
   float out_scale;            /* 1 / (scale of the int8 output activation)                */
+  /* Fused second input (bf16 LDS-DMA kernels, x2 != NULL): y = act(conv(x, w) + conv1x1_s(x2, w2)
+   * * scale + shift) as ONE implicit GEMM over the concatenated K [ks*ks*cin | cin2]; wgt rows hold
+   * [w | w2] (k = ks*ks*cin + cin2).  This folds a BasicBlock / Bottleneck 1x1 downsample
+   * (lmodels/drn.py:181-186, its BN scale folded into w2, shifts summed) into the block's last
+   * conv, so the residual branch is never written to HBM.  x2: NHWC [n][h2][w2][cin2], sampled at
+   * (oh*stride2, ow*stride2); cin2 % 64 == 0, res must be NULL.  x2 = NULL: unused.           */
+  const void* x2;
+  int32_t cin2, h2, w2, stride2;
 } drnmi_conv_args;
 
 /* Algorithms behind drnmi_conv2d_bn_act:

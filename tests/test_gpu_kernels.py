@@ -398,3 +398,76 @@ def test_conv_x6_fp32_accuracy(case):
     scale = np.abs(ref).max()
     print(f"{name} {case}: max-abs vs fp64 {e_x6:.2e} (exact-f32 kernel {e_f32:.2e}, |y| {scale:.1f})")
     assert e_x6 <= max(4 * e_f32, 1e-6 * scale)
+
+
+@pytest.mark.parametrize("case", [
+    # (n, h, w, cin, cout, ks, dil, cin2, stride2, h2, w2)
+    (2, 16, 24, 256, 256, 3, 2, 128, 1, 16, 24),     # layer5.0: conv2 + 1x1 downsample 128 -> 256
+    (1, 12, 20, 512, 512, 3, 4, 256, 1, 12, 20),     # layer6.0: dilation 4, 256 -> 512
+    (1, 9, 13, 256, 1024, 1, 1, 512, 2, 18, 26),     # Bottleneck conv3 + stride-2 downsample
+])
+def test_conv_fused_downsample(case):
+    """drnmi_conv_args.x2: y = relu(conv(x, w) + conv1x1_s(x2, w2) + shift) as one launch (the
+    downsample folded into the block's last conv) vs torch fp32 on the same bf16 operands."""
+    n, h, w, cin, cout, ks, dil, cin2, s2, h2, w2 = case
+    g = torch.Generator().manual_seed(cin + cin2)
+    x = (torch.randn(n, h, w, cin, generator=g)).to(torch.bfloat16)
+    x2 = (torch.randn(n, h2, w2, cin2, generator=g)).to(torch.bfloat16)
+    wt = (torch.randn(cout, cin, ks, ks, generator=g) / (cin * ks * ks) ** 0.5).to(torch.bfloat16)
+    wd = (torch.randn(cout, cin2, 1, 1, generator=g) / cin2 ** 0.5).to(torch.bfloat16)
+    sh = torch.randn(cout, generator=g)
+    pad = dil if ks == 3 else 0
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wt.float(), padding=pad, dilation=dil) \
+        + F.conv2d(x2.float().permute(0, 3, 1, 2), wd.float(), stride=s2) + sh.view(1, -1, 1, 1)
+    ref = torch.relu(ref).permute(0, 2, 3, 1)
+    k1 = ks * ks * cin
+    wpk = torch.zeros(cout, k1 + cin2, dtype=torch.bfloat16)
+    wpk[:, :k1] = wt.permute(0, 2, 3, 1).reshape(cout, k1)
+    wpk[:, k1:] = wd.reshape(cout, cin2)
+    ho, wo = h, w
+    y = torch.empty(n, ho, wo, cout, dtype=torch.bfloat16, device=DEV)
+    xd, x2d, wpd, shd = x.to(DEV), x2.to(DEV), wpk.to(DEV), sh.to(DEV)
+    a = _lib.ConvArgs()
+    a.x, a.wgt, a.scale, a.shift, a.res, a.y = xd.data_ptr(), wpd.data_ptr(), None, shd.data_ptr(), None, y.data_ptr()
+    a.y_sn, a.y_sp, a.y_sc = ho * wo * cout, cout, 1
+    a.n, a.h, a.w, a.cin, a.ho, a.wo, a.cout, a.cout_pad = n, h, w, cin, ho, wo, cout, cout
+    a.ks, a.stride, a.pad, a.dil = ks, 1, pad, dil
+    a.k = a.k_pad = k1 + cin2
+    a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_BF16, _lib.DRNMI_BF16, -1, _lib.ALGO_IGEMM
+    a.x2, a.cin2, a.h2, a.w2, a.stride2 = x2d.data_ptr(), cin2, h2, w2, s2
+    name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
+    assert name.startswith("conv_big_kernel"), name
+    _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds")
+    torch.cuda.synchronize()
+    err = (y.float().cpu() - ref).abs().max().item()
+    print(f"{name} {case}: max-abs {err:.3e} (|y| {ref.abs().max().item():.2f})")
+    assert err <= 0.02 * max(1.0, ref.abs().max().item())
+    # no kernel without x2 support may take it silently
+    a.tile = 0
+    assert _lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())) < 0
+
+
+def test_bf16_fused_downsample_network_matches_unfused(golden_forward):
+    """The bf16 network with the downsamples folded (default) vs the separate launches: the fused
+    form skips one bf16 rounding of the residual, so the two agree to bf16 noise."""
+    from drnmi import engine
+    from drnmi.drnseg import build
+    case = "d22_2x128x256"
+    m = build("drn_d_22", 19, seed=int(golden_forward[case + "/meta"][0]), device=DEV, precision="bf16")
+    frames = torch.from_numpy(golden_forward[case + "/frames"]).to(DEV)
+    pk_plan = m.plan(2, 128, 256)
+    assert len(pk_plan.skip) == 2
+    fused = m.segment(frames).long()
+    engine.FUSE_DOWNSAMPLE = False
+    try:
+        m2 = build("drn_d_22", 19, seed=int(golden_forward[case + "/meta"][0]), device=DEV, precision="bf16")
+        assert not m2.plan(2, 128, 256).skip
+        unfused = m2.segment(frames).long()
+    finally:
+        engine.FUSE_DOWNSAMPLE = True
+    ref = torch.from_numpy(golden_forward[case + "/labels"]).long().to(DEV)
+    agree = (fused == unfused).float().mean().item()
+    a_f = (fused == ref).float().mean().item()
+    a_u = (unfused == ref).float().mean().item()
+    print(f"fused vs unfused labels {agree:.4f}; vs reference fused {a_f:.4f} unfused {a_u:.4f}")
+    assert agree >= 0.99 and a_f >= 0.98

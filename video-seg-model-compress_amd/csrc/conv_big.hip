@@ -396,6 +396,11 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   const T* __restrict__ x = reinterpret_cast<const T*>(p.x);
   const T* __restrict__ wt = reinterpret_cast<const T*>(p.wgt);
   const int nk = p.k_pad / BK;
+  // fused second input (x2 != NULL: the block's 1x1 downsample folded into this conv, the
+  // concatenated-K GEMM [W | W_ds] x [im2col(x) ; x2 sampled at stride2]): the last
+  // cin2 / BK K steps read x2 instead of a tap of x
+  const T* __restrict__ x2 = reinterpret_cast<const T*>(p.x2);
+  const int nk1 = x2 != nullptr ? (KS * KS * cin) / BK : nk;
   const int fr = lane & 15;       // fragment row (channel or pixel within a 16-block)
   const int fq = lane >> 4;       // 16-B k chunk within a 64-B substep
 
@@ -412,6 +417,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   // image; big_conv_supported / i8_conv_supported bound n*h*w*cin < 2^31 and h, w < 16384)
   uint32_t b_hw[C::B_INSTR];
   int b_off[C::B_INSTR];
+  int b2_off[C::B_INSTR];         // x2 element offset of the row's chunk (x2 steps)
   const char* zero_src = reinterpret_cast<const char*>(g_zero_page) + lane * 16;
 
   auto setup = [&](int px0, int co0) {
@@ -428,6 +434,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       const int m = px0 + r;
       b_hw[i] = 0xC000C000u;
       b_off[i] = 0;
+      b2_off[i] = -1;
       if (m < M) {
         const int n = m / hw_o;
         const int q = m - n * hw_o;
@@ -437,15 +444,24 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         const int iw0 = ow * p.stride - p.pad;
         b_hw[i] = (static_cast<uint32_t>(ih0) << 16) | (static_cast<uint32_t>(iw0) & 0xffffu);
         b_off[i] = ((n * H + ih0) * W + iw0) * cin + swzb<C::ROWB>(r, lslot) * CE;
+        if (x2 != nullptr)
+          b2_off[i] = ((n * p.h2 + oh * p.stride2) * p.w2 + ow * p.stride2) * p.cin2 + swzb<C::ROWB>(r, lslot) * CE;
       }
     }
   };
 
   // K step kt = (channel block cb, tap): taps innermost, so the KS*KS steps that re-read one
   // channel slice of the same pixel neighbourhood run back to back (L2 hits, not MALL).
-  struct StepP { int k0, dh, dw; int64_t toff; };
+  struct StepP { int k0, dh, dw; int64_t toff; bool second; };
   auto step_params = [&](int kt) {
     StepP sp;
+    sp.second = kt >= nk1;
+    if (sp.second) {                               // x2 step: channels (kt - nk1) * BK of x2
+      sp.k0 = KS * KS * cin + (kt - nk1) * BK;
+      sp.dh = sp.dw = 0;
+      sp.toff = (kt - nk1) * BK;
+      return sp;
+    }
     const int cb = kt / (KS * KS);
     const int tap = kt - cb * (KS * KS);
     sp.k0 = (tap << lc) + cb * BK;                 // packed weight column: tap * cin + channel
@@ -466,6 +482,8 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       const bool ok = static_cast<unsigned>(ih0 + sp.dh) < static_cast<unsigned>(H) &&
                       static_cast<unsigned>(iw0 + sp.dw) < static_cast<unsigned>(W);
       const void* src = ok ? static_cast<const void*>(x + (b_off[j] + sp.toff)) : static_cast<const void*>(zero_src);
+      if (sp.second)
+        src = b2_off[j] >= 0 ? static_cast<const void*>(x2 + (b2_off[j] + sp.toff)) : static_cast<const void*>(zero_src);
       glds16(src, sa + C::A_BYTES + (wave * C::B_INSTR + j) * 1024);
     }
   };
@@ -1063,10 +1081,20 @@ const char* i8_conv_name(const drnmi_conv_args& p) {
   return p.ks == 3 ? kI8Variants[v].name3 : kI8Variants[v].name1;
 }
 
+// second input (fused 1x1 downsample): bf16 NHWC x2 [n][h2][w2][cin2], cin2 a multiple of 64 with
+// n*h2*w2*cin2 < 2^31, sampled at (oh*stride2, ow*stride2) inside x2; no residual with it
+static bool x2_ok(const drnmi_conv_args& p) {
+  if (p.x2 == nullptr) return p.k == p.ks * p.ks * p.cin;
+  return p.cin2 >= 64 && p.cin2 % 64 == 0 && p.cin >= 64 && p.res == nullptr && p.unit_mask == nullptr &&
+         p.stride2 >= 1 && (p.ho - 1) * p.stride2 < p.h2 && (p.wo - 1) * p.stride2 < p.w2 &&
+         static_cast<int64_t>(p.n) * p.h2 * p.w2 * p.cin2 < (int64_t(1) << 31) &&
+         p.k == p.ks * p.ks * p.cin + p.cin2;
+}
+
 bool big_conv_supported(const drnmi_conv_args& p) {
   return static_cast<int64_t>(p.n) * p.h * p.w * p.cin < (int64_t(1) << 31) && p.h < 16384 && p.w < 16384 &&
          p.dtype == DRNMI_BF16 && p.cin >= kMinCin && (p.cin & (p.cin - 1)) == 0 && p.cout_pad % 128 == 0 &&
-         (p.ks == 1 || p.ks == 3) && p.k == p.ks * p.ks * p.cin && p.k_pad == p.k &&
+         (p.ks == 1 || p.ks == 3) && x2_ok(p) && p.k_pad == p.k &&
          (p.out_dtype == DRNMI_F32 || (p.y_sc == 1 && p.y_sp == p.cout));
 }
 
@@ -1082,7 +1110,7 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   if ((p.cout + v.bco - 1) / v.bco * v.bco > p.cout_pad) return DRNMI_EINVAL;
   hipError_t e;
   if (variant == kPingPong) {
-    if (p.cout % 256 != 0) return DRNMI_ENOTSUP;
+    if (p.cout % 256 != 0 || p.x2 != nullptr) return DRNMI_ENOTSUP;
     e = p.ks == 3 ? launch_pp<3>(p, s) : launch_pp<1>(p, s);
     return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
   }

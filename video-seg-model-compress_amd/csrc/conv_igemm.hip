@@ -318,6 +318,7 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (a == nullptr) return DRNMI_EINVAL;
   const drnmi_conv_args& p = *a;
   if (p.algo == DRNMI_ALGO_PATCH) {
+    if (p.x2 != nullptr) return DRNMI_ENOTSUP;     // fused second input: LDS-DMA kernels only
     if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.shift == nullptr ||
         p.n <= 0 || p.h <= 0 || p.w <= 0 || p.cout > p.cout_pad)
       return DRNMI_EINVAL;
@@ -329,7 +330,8 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (p.algo != DRNMI_ALGO_IGEMM || p.src_u8) return DRNMI_EINVAL;
   const bool pow2 = p.cin >= 8 && (p.cin & (p.cin - 1)) == 0;
   if (!pow2 || p.n <= 0 || p.h <= 0 || p.w <= 0 || p.ho <= 0 || p.wo <= 0) return DRNMI_EINVAL;
-  if (p.cout <= 0 || p.cout > p.cout_pad || p.k != p.ks * p.ks * p.cin) return DRNMI_EINVAL;
+  if (p.cout <= 0 || p.cout > p.cout_pad || p.k != p.ks * p.ks * p.cin + (p.x2 != nullptr ? p.cin2 : 0))
+    return DRNMI_EINVAL;
   if (p.k_pad < p.k || p.k_pad % kBK != 0 || p.stride <= 0 || p.dil <= 0 || p.pad < 0) return DRNMI_EINVAL;
   if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.shift == nullptr)
     return DRNMI_EINVAL;
@@ -349,6 +351,7 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (p.dtype == DRNMI_F32X3) return x6_conv_dispatch(p, reinterpret_cast<hipStream_t>(stream));
   if (p.tile >= 4 || (p.tile < 0 && (big_conv_supported(p) || halo_conv_supported(p))))
     return big_conv_dispatch(p, p.tile < 0 ? -1 : p.tile - 4, reinterpret_cast<hipStream_t>(stream));
+  if (p.x2 != nullptr) return DRNMI_ENOTSUP;          // fused second input: LDS-DMA kernels only
   const int tile = p.tile < 0 ? auto_tile(p.cout) : p.tile;
   if (tile >= 4 || p.cout_pad % kTiles[tile].bn != 0) return DRNMI_EINVAL;
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;

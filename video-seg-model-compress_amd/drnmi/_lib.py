@@ -41,6 +41,8 @@ class ConvArgs(ctypes.Structure):
         ("unit_mask", ctypes.c_void_p),
         ("res_scale", ctypes.c_float),
         ("out_scale", ctypes.c_float),
+        ("x2", ctypes.c_void_p),
+        ("cin2", ctypes.c_int32), ("h2", ctypes.c_int32), ("w2", ctypes.c_int32), ("stride2", ctypes.c_int32),
     ]
 
 

@@ -90,6 +90,10 @@ class ConvNode:
     res_scale: float = 0.0
     out_scale: float = 0.0       # 1 / scale of an int8 output (0: bf16 / fp32 output)
     x6: bool = False             # fp32x: wpk holds three bf16 planes, launched as DRNMI_F32X3
+    # fused 1x1 downsample (bf16): this node's launch also computes the residual branch
+    # (include/drnmi.h drnmi_conv_args.x2); ds_of names the folded-away downsample node
+    fused: dict | None = None    # {"wpk", "shift", "k", "x2_val", "stride2", "ds": node index}
+    fused_into: int = -1         # downsample node: index of the conv that computes it
 
 
 @dataclass
@@ -285,6 +289,7 @@ class PackedNet:
                 nd.unit_mask, nd.zero_unit_frac = None, 0.0
                 if nd.scale_folded and self.block_sparse:
                     nd.unit_mask, nd.zero_unit_frac = _unit_mask(nd.wpk, self.code)
+            self._fuse_downsamples()
             # fused-ingest stem weights (bf16 patch kernel reads uint8 frames directly)
             self.stem_u8_w = None
             stem = self.graph.nodes[0]
@@ -297,6 +302,43 @@ class PackedNet:
                 full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
                 self.stem_u8_w = split3_bf16(full) if self.base == "fp32x" else full.to(self.tdtype).contiguous()
 
+
+    def _fuse_downsamples(self):
+        """bf16: fold each BasicBlock / Bottleneck 1x1 downsample (lmodels/drn.py:181-186) into the
+        block's last conv as extra K columns -- [W2 | W_ds] over [im2col(t) ; x sampled at the
+        downsample stride], both BN scales already folded into the weights, shifts summed -- so
+        the residual branch is one GEMM segment instead of a launch that writes it to HBM and a
+        residual read.  Only where the last conv already runs on conv_big (the LDS-DMA kernel
+        that takes x2); plans with keep_all (parity taps, calibration) keep the separate launch."""
+        g = self.graph
+        for nd in g.nodes:
+            nd.fused, nd.fused_into = None, -1
+        if self.base != "bf16" or not FUSE_DOWNSAMPLE:
+            return
+        producer = {nd.dst: i for i, nd in enumerate(g.nodes)}
+        reads = {}
+        for nd in g.nodes:
+            for v in (nd.src, nd.res):
+                if v:
+                    reads[v] = reads.get(v, 0) + 1
+        for i, nd in enumerate(g.nodes):
+            j = producer.get(nd.res) if nd.res else None
+            if j is None or nd.i8 or nd.x6 or not nd.scale_folded or nd.unit_mask is not None:
+                continue
+            ds = g.nodes[j]
+            if (not ds.name.endswith("downsample.0") or ds.relu or ds.i8 or not ds.scale_folded
+                    or ds.conv.kernel_size[0] != 1 or ds.conv.padding[0] != 0 or reads.get(nd.res) != 1):
+                continue
+            cin2 = self.cstride[ds.src]
+            if cin2 % 64 != 0 or ds.cout_pad != nd.cout_pad or nd.k_pad != nd.k:
+                continue
+            if not _route_name(nd, nd.cin_stride).startswith("conv_big") or \
+                    not _route_name(nd, nd.cin_stride, cin2).startswith("conv_big"):
+                continue
+            nd.fused = {"wpk": torch.cat([nd.wpk, ds.wpk[:, :cin2]], dim=1).contiguous(),
+                        "shift": (nd.shift + ds.shift).contiguous(), "k": nd.k + cin2,
+                        "x2_val": ds.src, "stride2": ds.conv.stride[0], "ds": j}
+            ds.fused_into = i
 
     def _pack_int8(self, nd: ConvNode, full: torch.Tensor, bn_scale: torch.Tensor, cout: int):
         """Per-output-channel symmetric int8 weights (oracle/int8_oracle.py quantize_weight_rows):
@@ -363,6 +405,31 @@ def _uses_patch(nd: ConvNode, cin_stride: int, precision: str) -> bool:
     return (precision == "bf16" and shape in PATCH_SHAPES) or (precision == "fp32x" and shape in X6_PATCH_SHAPES)
 
 
+# bf16: fold 1x1 downsamples into the block's last conv (PackedNet._fuse_downsamples)
+FUSE_DOWNSAMPLE = True
+
+
+def _route_name(nd: ConvNode, cin_stride: int, cin2: int = 0) -> str:
+    """Kernel the bf16 launch of `nd` (optionally with a fused cin2-channel second input) goes to,
+    probed on a 16x16 map through drnmi_conv_kernel_name (routing does not depend on size)."""
+    c = nd.conv
+    a = _lib.ConvArgs()
+    a.n, a.h, a.w, a.cin = 1, 16, 16, cin_stride
+    a.ks, a.stride, a.pad, a.dil = c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0]
+    a.ho = _conv_out(16, a.ks, a.stride, a.pad, a.dil)
+    a.wo = a.ho
+    a.cout, a.cout_pad = c.out_channels, nd.cout_pad
+    a.k = a.ks * a.ks * cin_stride + cin2
+    a.k_pad = a.k
+    a.dtype, a.out_dtype, a.y_sp, a.y_sc = _lib.DRNMI_BF16, _lib.DRNMI_BF16, c.out_channels, 1
+    a.scale = None
+    a.tile, a.algo = -1, _lib.ALGO_IGEMM
+    if cin2:
+        a.x2, a.cin2, a.h2, a.w2, a.stride2 = 1, cin2, 16 * c.stride[0], 16 * c.stride[0], 1
+    name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
+    return name.decode() if name is not None else ""
+
+
 def _fused_init_route(nd: ConvNode, cin_stride: int) -> bool:
     """True when the bf16 launch of `nd` goes to conv_big / conv_pp / conv_halo (the kernels
     that take scale = NULL and seed the accumulators with shift + residual).  Routing does not
@@ -408,15 +475,25 @@ class Plan:
         self.out_hw = (8 * lh, 8 * lw)
 
         # Liveness-based buffer reuse (exact-size, per-dtype pool).  Launches read nd.x_val /
-        # nd.r_val (an int8 copy "q:<v>" of a bf16 value in int8 nets).
+        # nd.r_val (an int8 copy "q:<v>" of a bf16 value in int8 nets), and a fused conv its
+        # downsample's input instead of the residual (PackedNet._fuse_downsamples).
+        self.fuse = not keep_all
         for nd in g.nodes:
             if not nd.x_val:
                 nd.x_val, nd.r_val = nd.src, nd.res
-        last_use = {}
+        self.skip = {i for i, nd in enumerate(g.nodes) if self.fuse and nd.fused_into >= 0}
+        reads_of = {}
         for i, nd in enumerate(g.nodes):
-            last_use[nd.x_val] = i
-            if nd.r_val:
-                last_use[nd.r_val] = i
+            if i in self.skip:
+                reads_of[i] = set()
+            elif self.fuse and nd.fused:
+                reads_of[i] = {nd.x_val, nd.fused["x2_val"]}
+            else:
+                reads_of[i] = {nd.x_val, nd.r_val} - {None}
+        last_use = {}
+        for i in range(len(g.nodes)):
+            for v in reads_of[i]:
+                last_use[v] = i
         self.bufs = {}
         pool = {}
         self.bufs["input"] = torch.empty(n * h * w * 8, dtype=packed.tdtype, device=dev)
@@ -427,6 +504,8 @@ class Plan:
             self.bufs[v] = lst.pop() if lst else torch.empty(numel, dtype=td, device=dev)
 
         for i, nd in enumerate(g.nodes):
+            if i in self.skip:
+                continue                          # computed inside the block's last conv
             oh, ow = self.shapes[nd.dst]
             if nd.out_fp32_nchw:
                 self.bufs[nd.dst] = torch.empty(n, nd.conv.out_channels, oh, ow, dtype=torch.float32, device=dev)
@@ -435,12 +514,12 @@ class Plan:
             for v in packed.quant_after.get(i, []):
                 alloc("q:" + v, n * oh * ow * packed.cstride[v])
             if not keep_all:
-                for v in {nd.x_val, nd.r_val} - {None, "input"}:
+                for v in reads_of[i] - {"input"}:
                     if last_use.get(v) == i and v in self.bufs and v != nd.dst:
                         t = self.bufs[v]
                         pool.setdefault((t.numel(), t.dtype), []).append(t)
         self.keep_all = keep_all
-        self.args = [self._conv_args(nd) for nd in g.nodes]
+        self.args = [None if i in self.skip else self._conv_args(nd) for i, nd in enumerate(g.nodes)]
         self.stem_u8 = self._stem_u8_args()
         self.src = "nchw"
 
@@ -454,7 +533,8 @@ class Plan:
         a.wgt = nd.wpk.data_ptr()
         a.scale = None if nd.scale_folded else nd.scale.data_ptr()
         a.shift = nd.shift.data_ptr()
-        a.res = self.bufs[nd.r_val].data_ptr() if nd.r_val else None
+        fused = nd.fused if self.fuse else None
+        a.res = self.bufs[nd.r_val].data_ptr() if (nd.r_val and not fused) else None
         a.y = self.bufs[nd.dst].data_ptr()
         cout = c.out_channels
         if nd.out_fp32_nchw:
@@ -478,6 +558,14 @@ class Plan:
         a.algo = _lib.ALGO_PATCH if _uses_patch(nd, nd.cin_stride, pk.base) else _lib.ALGO_IGEMM
         a.res_scale, a.out_scale = nd.res_scale, nd.out_scale
         a.unit_mask = nd.unit_mask.data_ptr() if nd.unit_mask is not None else None
+        if fused:
+            f = fused
+            a.wgt, a.shift, a.res = f["wpk"].data_ptr(), f["shift"].data_ptr(), None
+            a.k = a.k_pad = f["k"]
+            a.x2 = self.bufs[f["x2_val"]].data_ptr()
+            a.cin2 = pk.cstride[f["x2_val"]]
+            a.h2, a.w2 = self.shapes[f["x2_val"]]
+            a.stride2 = f["stride2"]
         return a
 
     def _stem_u8_args(self) -> _lib.ConvArgs | None:
@@ -494,11 +582,14 @@ class Plan:
         return a
 
     def refresh_weight_ptrs(self):
-        for a, nd in zip(self.args, self.packed.graph.nodes):
-            a.wgt = nd.wpk.data_ptr()
-            a.scale = None if nd.scale_folded else nd.scale.data_ptr()
-            a.shift = nd.shift.data_ptr()
-            a.unit_mask = nd.unit_mask.data_ptr() if nd.unit_mask is not None else None
+        nodes = self.packed.graph.nodes
+        skip = {i for i, nd in enumerate(nodes) if self.fuse and nd.fused_into >= 0}
+        if skip != self.skip:
+            raise RuntimeError("repack changed the downsample fusion of a live plan")
+        for i, nd in enumerate(nodes):
+            if i in self.skip:
+                continue
+            self.args[i] = self._conv_args(nd)
         if self.stem_u8 is not None:
             nd = self.packed.graph.nodes[0]
             self.stem_u8.wgt = self.packed.stem_u8_w.data_ptr()
@@ -509,6 +600,8 @@ class Plan:
     def run_backbone(self, stream: int, timing_hook=None):
         lib = _lib.load()
         for i, (a, nd) in enumerate(zip(self.args, self.packed.graph.nodes)):
+            if a is None:
+                continue                          # downsample folded into the block's last conv
             if i == 0 and self.src == "u8":
                 a = self.stem_u8
             if timing_hook is not None:
