@@ -200,6 +200,8 @@ def main():
 
     def launched_name(i):
         a = plan.stem_u8 if (i == 0 and plan.stem_u8 is not None) else plan.args[i]
+        if a is None:
+            return ""                        # downsample folded into its block's last conv
         return lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
 
     names = [launched_name(i) for i in range(len(plan.args))]
@@ -207,6 +209,18 @@ def main():
     # dense and sparse kernels alike (the dense kernel multiplies the zeros too)
     nodes = plan.packed.graph.nodes
     density = [float((nd.conv.weight != 0).sum()) / nd.conv.weight.numel() for nd in nodes]
+    # a folded-away downsample's FLOPs run inside its block's last conv: attribute them there
+    # (its input read too; the residual is never written or read)
+    works = list(works)
+    for i in sorted(getattr(plan, "skip", ())):
+        j = nodes[i].fused_into
+        n_, fj, bj = works[j]
+        fi, bi = works[i][1], works[i][2]
+        oh, ow = plan.shapes[nodes[j].dst]
+        res_b = plan.n * oh * ow * nodes[j].conv.out_channels * 2      # the bf16 residual tensor
+        # conv2 bytes lose the residual read; the downsample's input + weights (not its output) join
+        works[j] = (n_, fj + fi, bj - res_b + (bi - res_b))
+        works[i] = (works[i][0], 0.0, 0.0)
     dense_flops = {i: w[1] for i, w in enumerate(works)}
     works = [(w[0], w[1] * density[i], w[2]) if i < len(nodes) else w for i, w in enumerate(works)]
     events = []
