@@ -371,7 +371,7 @@ struct BigCfg {
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-template <typename T, int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE>
+template <typename T, int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE, bool X2 = false>
 __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   using K = KT<T>;
   using C = BigCfg<WCO, WC, NST, BK, NWP, K::ESZ>;
@@ -400,7 +400,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   // concatenated-K GEMM [W | W_ds] x [im2col(x) ; x2 sampled at stride2]): the last
   // cin2 / BK K steps read x2 instead of a tap of x
   const T* __restrict__ x2 = reinterpret_cast<const T*>(p.x2);
-  const int nk1 = x2 != nullptr ? (KS * KS * cin) / BK : nk;
+  const int nk1 = X2 ? (KS * KS * cin) / BK : nk;
   const int fr = lane & 15;       // fragment row (channel or pixel within a 16-block)
   const int fq = lane >> 4;       // 16-B k chunk within a 64-B substep
 
@@ -417,7 +417,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   // image; big_conv_supported / i8_conv_supported bound n*h*w*cin < 2^31 and h, w < 16384)
   uint32_t b_hw[C::B_INSTR];
   int b_off[C::B_INSTR];
-  int b2_off[C::B_INSTR];         // x2 element offset of the row's chunk (x2 steps)
+  int b2_off[X2 ? C::B_INSTR : 1];   // x2 element offset of the row's chunk (x2 steps)
   const char* zero_src = reinterpret_cast<const char*>(g_zero_page) + lane * 16;
 
   auto setup = [&](int px0, int co0) {
@@ -434,7 +434,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       const int m = px0 + r;
       b_hw[i] = 0xC000C000u;
       b_off[i] = 0;
-      b2_off[i] = -1;
+      if constexpr (X2) b2_off[i] = -1;
       if (m < M) {
         const int n = m / hw_o;
         const int q = m - n * hw_o;
@@ -444,7 +444,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         const int iw0 = ow * p.stride - p.pad;
         b_hw[i] = (static_cast<uint32_t>(ih0) << 16) | (static_cast<uint32_t>(iw0) & 0xffffu);
         b_off[i] = ((n * H + ih0) * W + iw0) * cin + swzb<C::ROWB>(r, lslot) * CE;
-        if (x2 != nullptr)
+        if constexpr (X2)
           b2_off[i] = ((n * p.h2 + oh * p.stride2) * p.w2 + ow * p.stride2) * p.cin2 + swzb<C::ROWB>(r, lslot) * CE;
       }
     }
@@ -455,7 +455,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   struct StepP { int k0, dh, dw; int64_t toff; bool second; };
   auto step_params = [&](int kt) {
     StepP sp;
-    sp.second = kt >= nk1;
+    sp.second = X2 && kt >= nk1;
     if (sp.second) {                               // x2 step: channels (kt - nk1) * BK of x2
       sp.k0 = KS * KS * cin + (kt - nk1) * BK;
       sp.dh = sp.dw = 0;
@@ -482,8 +482,9 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       const bool ok = static_cast<unsigned>(ih0 + sp.dh) < static_cast<unsigned>(H) &&
                       static_cast<unsigned>(iw0 + sp.dw) < static_cast<unsigned>(W);
       const void* src = ok ? static_cast<const void*>(x + (b_off[j] + sp.toff)) : static_cast<const void*>(zero_src);
-      if (sp.second)
-        src = b2_off[j] >= 0 ? static_cast<const void*>(x2 + (b2_off[j] + sp.toff)) : static_cast<const void*>(zero_src);
+      if constexpr (X2)
+        if (sp.second)
+          src = b2_off[j] >= 0 ? static_cast<const void*>(x2 + (b2_off[j] + sp.toff)) : static_cast<const void*>(zero_src);
       glds16(src, sa + C::A_BYTES + (wave * C::B_INSTR + j) * 1024);
     }
   };
@@ -644,10 +645,10 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   }
 }
 
-template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE>
+template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE, bool X2 = false>
 __global__ void __launch_bounds__(64 * NWP * WC, 1)
 conv_big_kernel(const drnmi_conv_args p) {
-  conv_big_body<uint16_t, KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE>(p);
+  conv_big_body<uint16_t, KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE, X2>(p);
 }
 
 // W8A8 (config C5): the same LDS-DMA pipeline over int8 elements, BK int8 channels per K step
@@ -871,13 +872,13 @@ hipError_t launch_pp(const drnmi_conv_args& p, hipStream_t s) {
 
 int g_num_cus = 0;
 
-template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP = 4, bool SPARSE = false>
+template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP = 4, bool SPARSE = false, bool X2 = false>
 hipError_t launch_big(const drnmi_conv_args& p, hipStream_t s) {
   using C = BigCfg<WCO, WC, NST, BK, NWP>;
   static bool attr_set = false;
   if (!attr_set) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&conv_big_kernel<KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE>),
+        reinterpret_cast<const void*>(&conv_big_kernel<KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE, X2>),
         hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -896,7 +897,7 @@ hipError_t launch_big(const drnmi_conv_args& p, hipStream_t s) {
     const int64_t cap = g_num_cus * (per_cu > 0 ? per_cu : 1);
     blocks = blocks < cap ? blocks : cap;
   }
-  hipLaunchKernelGGL((conv_big_kernel<KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE>), dim3(static_cast<unsigned>(blocks)),
+  hipLaunchKernelGGL((conv_big_kernel<KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE, X2>), dim3(static_cast<unsigned>(blocks)),
                      dim3(C::THREADS), C::LDS, s, p);
   return hipGetLastError();
 }
@@ -909,18 +910,18 @@ struct Variant {
 
 // tile ids 4 + v in drnmi_conv_args.tile
 constexpr Variant kVariants[] = {
-    {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, false, 4, false>", "conv_big_kernel<1, 128, 1, 3, 64, false, 4, false>"},
-    {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, false, 4, false>", "conv_big_kernel<1, 128, 2, 2, 64, false, 4, false>"},
-    {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, false, 4, false>", "conv_big_kernel<1, 64, 1, 4, 32, false, 4, false>"},
-    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, false, 4, false>", "conv_big_kernel<1, 32, 1, 3, 64, false, 4, false>"},
-    {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, false, 4, false>", "conv_big_kernel<1, 128, 2, 4, 32, false, 4, false>"},
-    {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, false, 4, false>", "conv_big_kernel<1, 128, 1, 4, 32, false, 4, false>"},
-    {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, true, 4, false>", "conv_big_kernel<1, 128, 1, 3, 64, true, 4, false>"},
-    {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, true, 4, false>", "conv_big_kernel<1, 128, 2, 2, 64, true, 4, false>"},
-    {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, true, 4, false>", "conv_big_kernel<1, 64, 1, 4, 32, true, 4, false>"},
-    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, true, 4, false>", "conv_big_kernel<1, 32, 1, 3, 64, true, 4, false>"},
-    {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, true, 4, false>", "conv_big_kernel<1, 128, 2, 4, 32, true, 4, false>"},
-    {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, true, 4, false>", "conv_big_kernel<1, 128, 1, 4, 32, true, 4, false>"},
+    {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, false, 4, false, false>", "conv_big_kernel<1, 128, 1, 3, 64, false, 4, false, false>"},
+    {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, false, 4, false, false>", "conv_big_kernel<1, 128, 2, 2, 64, false, 4, false, false>"},
+    {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, false, 4, false, false>", "conv_big_kernel<1, 64, 1, 4, 32, false, 4, false, false>"},
+    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, false, 4, false, false>", "conv_big_kernel<1, 32, 1, 3, 64, false, 4, false, false>"},
+    {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, false, 4, false, false>", "conv_big_kernel<1, 128, 2, 4, 32, false, 4, false, false>"},
+    {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, false, 4, false, false>", "conv_big_kernel<1, 128, 1, 4, 32, false, 4, false, false>"},
+    {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, true, 4, false, false>", "conv_big_kernel<1, 128, 1, 3, 64, true, 4, false, false>"},
+    {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, true, 4, false, false>", "conv_big_kernel<1, 128, 2, 2, 64, true, 4, false, false>"},
+    {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, true, 4, false, false>", "conv_big_kernel<1, 64, 1, 4, 32, true, 4, false, false>"},
+    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, true, 4, false, false>", "conv_big_kernel<1, 32, 1, 3, 64, true, 4, false, false>"},
+    {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, true, 4, false, false>", "conv_big_kernel<1, 128, 2, 4, 32, true, 4, false, false>"},
+    {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, true, 4, false, false>", "conv_big_kernel<1, 128, 1, 4, 32, true, 4, false, false>"},
     {256, 64, "conv_pp_kernel<3>", "conv_pp_kernel<1>"},
 };
 constexpr int kPingPong = 12;
@@ -1006,14 +1007,14 @@ hipError_t launch_sparse(const drnmi_conv_args& p, int base, hipStream_t s) {
 }
 
 const char* sparse_name(int ks, int base) {
-  static const char* n3[6] = {"conv_big_kernel<3, 128, 1, 3, 64, false, 4, true>",
-                              "conv_big_kernel<3, 128, 2, 2, 64, false, 4, true>", nullptr, nullptr,
-                              "conv_big_kernel<3, 128, 2, 4, 32, false, 4, true>",
-                              "conv_big_kernel<3, 128, 1, 4, 32, false, 4, true>"};
-  static const char* n1[6] = {"conv_big_kernel<1, 128, 1, 3, 64, false, 4, true>",
-                              "conv_big_kernel<1, 128, 2, 2, 64, false, 4, true>", nullptr, nullptr,
-                              "conv_big_kernel<1, 128, 2, 4, 32, false, 4, true>",
-                              "conv_big_kernel<1, 128, 1, 4, 32, false, 4, true>"};
+  static const char* n3[6] = {"conv_big_kernel<3, 128, 1, 3, 64, false, 4, true, false>",
+                              "conv_big_kernel<3, 128, 2, 2, 64, false, 4, true, false>", nullptr, nullptr,
+                              "conv_big_kernel<3, 128, 2, 4, 32, false, 4, true, false>",
+                              "conv_big_kernel<3, 128, 1, 4, 32, false, 4, true, false>"};
+  static const char* n1[6] = {"conv_big_kernel<1, 128, 1, 3, 64, false, 4, true, false>",
+                              "conv_big_kernel<1, 128, 2, 2, 64, false, 4, true, false>", nullptr, nullptr,
+                              "conv_big_kernel<1, 128, 2, 4, 32, false, 4, true, false>",
+                              "conv_big_kernel<1, 128, 1, 4, 32, false, 4, true, false>"};
   return ks == 3 ? n3[base] : n1[base];
 }
 
@@ -1116,6 +1117,14 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   }
   const int base = variant % 6;
   const bool persist = variant >= 6;
+  if (p.x2 != nullptr) {                  // fused second input: its own instantiation (bases 0 / 1)
+    if (persist || (base != 0 && base != 1)) return DRNMI_ENOTSUP;
+    if (p.ks == 3) e = base == 1 ? launch_big<3, 128, 2, 2, 64, false, 4, false, true>(p, s)
+                                 : launch_big<3, 128, 1, 3, 64, false, 4, false, true>(p, s);
+    else e = base == 1 ? launch_big<1, 128, 2, 2, 64, false, 4, false, true>(p, s)
+                       : launch_big<1, 128, 1, 3, 64, false, 4, false, true>(p, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
   if (p.unit_mask != nullptr && !persist && sparse_name(p.ks, base) != nullptr && p.k_pad / v.bk <= 128) {
     e = p.ks == 3 ? launch_sparse<3>(p, base, s) : launch_sparse<1>(p, base, s);
     return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
@@ -1129,6 +1138,14 @@ const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_name(p);
   if (variant < 0) variant = auto_variant(p);
   if (variant >= kNumVariants) return nullptr;
+  if (p.x2 != nullptr) {
+    if (variant != 0 && variant != 1) return nullptr;
+    static const char* n[2][2] = {{"conv_big_kernel<1, 128, 1, 3, 64, false, 4, false, true>",
+                                   "conv_big_kernel<1, 128, 2, 2, 64, false, 4, false, true>"},
+                                  {"conv_big_kernel<3, 128, 1, 3, 64, false, 4, false, true>",
+                                   "conv_big_kernel<3, 128, 2, 2, 64, false, 4, false, true>"}};
+    return n[p.ks == 3 ? 1 : 0][variant];
+  }
   if (p.unit_mask != nullptr && variant < 6 && sparse_name(p.ks, variant) != nullptr &&
       p.k_pad / kVariants[variant].bk <= 128)
     return sparse_name(p.ks, variant);
