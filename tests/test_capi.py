@@ -48,3 +48,21 @@ def test_argument_validation_without_gpu():
     assert lib.drnmi_up8_logsoftmax_argmax(None, None, None, None, 2, 1, 19, 8, 8, None) == -1
     assert lib.drnmi_mask_apply_f32(-1, None, None, None, None) == -1
     assert lib.drnmi_mask_apply_f32(0, None, None, None, None) == 0
+
+
+def test_fused_second_input_never_routes_to_halo():
+    """A conv with a fused second input (x2, the folded 1x1 downsample) must go to a kernel
+    that reads x2: the halo kernel takes the same 64/128-channel shapes but has no second K
+    segment, so routing it there would silently drop the downsample term."""
+    lib = _lib.load()
+    a = _lib.ConvArgs()
+    a.n, a.h, a.w, a.cin, a.ho, a.wo, a.cout, a.cout_pad = 1, 16, 16, 64, 16, 16, 64, 128
+    a.ks, a.stride, a.pad, a.dil = 3, 1, 1, 1
+    a.k = a.k_pad = 9 * 64
+    a.dtype = a.out_dtype = _lib.DRNMI_BF16
+    a.y_sp, a.y_sc, a.tile, a.algo = 64, 1, -1, _lib.ALGO_IGEMM
+    assert lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode().startswith("conv_halo")
+    a.x2, a.cin2, a.h2, a.w2, a.stride2 = 1, 64, 32, 32, 2
+    a.k = a.k_pad = 9 * 64 + 64
+    name = lib.drnmi_conv_kernel_name(ctypes.byref(a))
+    assert name is None or not name.decode().startswith("conv_halo")

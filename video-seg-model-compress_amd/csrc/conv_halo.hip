@@ -253,7 +253,9 @@ hipError_t launch_halo(const drnmi_conv_args& p, hipStream_t s) {
 }  // namespace
 
 bool halo_conv_supported(const drnmi_conv_args& p) {
-  if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.ks != 3 || p.stride != 1 || p.pad != p.dil)
+  // (a fused second input, x2, goes to conv_big: this kernel has no second K segment)
+  if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.ks != 3 || p.stride != 1 || p.pad != p.dil ||
+      p.x2 != nullptr)
     return false;
   if ((p.cin != 64 && p.cin != 128) || (p.cout != 64 && p.cout != 128) || p.cout_pad < p.cout)
     return false;
