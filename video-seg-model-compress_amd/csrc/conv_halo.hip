@@ -35,7 +35,10 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 
 template <int ROWB>
 __device__ __forceinline__ int hswz(int row, int chunk) {
-  if constexpr (ROWB == 128) return chunk ^ ((row >> 1) & 7);
+  // 128-B rows: slot = (row & 1, chunk ^ (row & 7)) gives the 16 lanes of every ds_read_b128
+  // group 16 distinct 4-bank slots for ANY row offset (the taps shift the rows by dw), which
+  // the earlier (row >> 1) & 7 did not for odd shifts
+  if constexpr (ROWB == 128) return chunk ^ (row & 7);
   else return chunk ^ (row & 15);   // 256-B rows span all 64 banks
 }
 
