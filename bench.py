@@ -198,7 +198,12 @@ def main():
     lib = _lib.load()
     import ctypes
 
+    fused_stem = getattr(plan, "stem_fused", False)
+
     def launched_name(i):
+        if fused_stem and i <= 1:            # stem + layer1 in one launch (drnmi_stem_layer1)
+            return "" if i == 1 else lib.drnmi_stem_layer1_kernel_name(
+                ctypes.byref(plan.stem_u8), ctypes.byref(plan.args[1])).decode()
         a = plan.stem_u8 if (i == 0 and plan.stem_u8 is not None) else plan.args[i]
         if a is None:
             return ""                        # downsample folded into its block's last conv
@@ -221,6 +226,15 @@ def main():
         # conv2 bytes lose the residual read; the downsample's input + weights (not its output) join
         works[j] = (n_, fj + fi, bj - res_b + (bi - res_b))
         works[i] = (works[i][0], 0.0, 0.0)
+    if fused_stem:
+        # layer1 runs inside the stem launch; the 16-channel stem output is neither written
+        # nor read back
+        h0, w0 = plan.shapes[nodes[0].dst]
+        mid = plan.n * h0 * w0 * nodes[0].conv.out_channels * 2
+        works[0] = (works[0][0], works[0][1] + works[1][1], works[0][2] + works[1][2] - 2 * mid)
+        works[1] = (works[1][0], 0.0, 0.0)
+        density[0] = density[1] = float(sum((nd.conv.weight != 0).sum() for nd in nodes[:2])) / \
+            sum(nd.conv.weight.numel() for nd in nodes[:2])
     dense_flops = {i: w[1] for i, w in enumerate(works)}
     works = [(w[0], w[1] * density[i], w[2]) if i < len(nodes) else w for i, w in enumerate(works)]
     events = []

@@ -112,6 +112,17 @@ enum drnmi_algo { DRNMI_ALGO_IGEMM = 0, DRNMI_ALGO_PATCH = 1 };
 
 int drnmi_conv2d_bn_act(const drnmi_conv_args* args, void* stream);
 
+/* Fused stem + layer1 (bf16, csrc/patch_conv.hip stem_l1_kernel): replaces the two launches
+ *   drnmi_conv2d_bn_act(stem); drnmi_conv2d_bn_act(next)
+ * of lmodels/drn.py:132-137 (layer0 7x7 3->16 + BN + ReLU on the uint8 frame) and :201-211
+ * (layer1 3x3 16->16 + BN + ReLU) with one, bit-identical to them; the stem output is never
+ * written (stem->y is ignored).  stem: the src_u8 = 1 PATCH contract above (cin 4, cout 16,
+ * ks 7, pad 3, k = k_pad = 224); next: cin 16, cout 16, ks 3, stride 1, pad 1, dil 1,
+ * k = 144, k_pad >= 160, no residual, packed NHWC bf16 output, same n/h/w as the stem.
+ * DRNMI_EINVAL for anything else.  drnmi_stem_layer1_kernel_name: "stem_l1_kernel" or NULL. */
+int drnmi_stem_layer1(const drnmi_conv_args* stem, const drnmi_conv_args* next, void* stream);
+const char* drnmi_stem_layer1_kernel_name(const drnmi_conv_args* stem, const drnmi_conv_args* next);
+
 /* Block-sparsity map of packed weights [rows_pad][k_pad] (dtype F32 or BF16): one bit per
  * 16-row x 32-column unit, bit = 1 iff any element of the unit is nonzero (+-0 count as zero);
  * layout: row-block rb owns words [rb*W, rb*W + W), W = ceil(k_pad / 32 / 32), unit ku at bit

@@ -471,3 +471,46 @@ def test_bf16_fused_downsample_network_matches_unfused(golden_forward):
     a_u = (unfused == ref).float().mean().item()
     print(f"fused vs unfused labels {agree:.4f}; vs reference fused {a_f:.4f} unfused {a_u:.4f}")
     assert agree >= 0.99 and a_f >= 0.98
+
+
+@pytest.mark.parametrize("shape", [(2, 45, 83), (1, 64, 128), (3, 33, 130), (1, 9, 301), (2, 130, 67)])
+def test_stem_layer1_fused_bit_identical(shape):
+    """drnmi_stem_layer1 (one launch, the stem output never leaves the CU) vs stem_dma_kernel +
+    patch_dma_kernel<16, 16, ...> (two launches): bit-identical, including the zero padding of
+    layer1 at every image edge, ragged tiles and frame widths with W*3 % 4 != 0; BGR too."""
+    n, h, w = shape
+    g = torch.Generator().manual_seed(h * w)
+    frames = torch.randint(0, 256, (n, h, w, 3), dtype=torch.uint8, generator=g).to(DEV)
+    w0 = _rand((16, 3, 7, 7), 91, 0.1)
+    w1 = _rand((16, 16, 3, 3), 92, 0.2)
+    sc0, sh0 = torch.rand(16, generator=g) + 0.5, torch.rand(16, generator=g) - 0.5
+    sc1, sh1 = torch.rand(16, generator=g) + 0.5, torch.rand(16, generator=g) - 0.5
+    for bgr in (False, True):
+        y0 = ops.stem_u8(frames, w0, sc0.to(DEV), sh0.to(DEV), O.INFO_MEAN, O.INFO_STD, bgr=bgr)
+        two = ops.conv2d_bn_act(y0, w1.to(DEV), sc1.to(DEV), sh1.to(DEV), None, 1, 1, 1, True,
+                                algo=_lib.ALGO_PATCH)
+        one = ops.stem_layer1_u8(frames, w0, sc0.to(DEV), sh0.to(DEV), w1.to(DEV), sc1.to(DEV), sh1.to(DEV),
+                                 O.INFO_MEAN, O.INFO_STD, bgr=bgr)
+        torch.cuda.synchronize()
+        assert torch.equal(one, two), (bgr, (one.float() - two.float()).abs().max().item())
+
+
+def test_stem_fused_network_matches_two_launch():
+    """The bf16 video path with the stem fused (default) gives the same labels as with the
+    stem and layer1 as two launches (bit-identical layer1 output => identical network)."""
+    from drnmi import engine
+    from drnmi.drnseg import build
+    from drnmi.weights import synth_frames
+    m = build("drn_d_22", 19, seed=3, device=DEV, precision="bf16")
+    frames = torch.from_numpy(synth_frames(11, 2, 136, 200)).to(DEV)
+    assert m.plan(2, 136, 200).stem_fused
+    fused = m.segment(frames)
+    engine.FUSE_STEM = False
+    try:
+        m2 = build("drn_d_22", 19, seed=3, device=DEV, precision="bf16")
+        assert not m2.plan(2, 136, 200).stem_fused
+        two = m2.segment(frames)
+    finally:
+        engine.FUSE_STEM = True
+    assert torch.equal(fused, two)
+

@@ -362,6 +362,16 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   return static_cast<int>(e);
 }
 
+extern "C" int drnmi_stem_layer1(const drnmi_conv_args* stem, const drnmi_conv_args* next, void* stream) {
+  if (stem == nullptr || next == nullptr) return DRNMI_EINVAL;
+  return stem_l1_dispatch(*stem, *next, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" const char* drnmi_stem_layer1_kernel_name(const drnmi_conv_args* stem, const drnmi_conv_args* next) {
+  if (stem == nullptr || next == nullptr || !stem_l1_ok(*stem, *next)) return nullptr;
+  return "stem_l1_kernel";
+}
+
 extern "C" int drnmi_weight_unit_mask(const void* wgt, int32_t dtype, int32_t rows_pad, int32_t k_pad,
                                       uint32_t* mask, int32_t* nonzero_units, void* stream) {
   return weight_unit_mask(wgt, dtype, rows_pad, k_pad, mask, nonzero_units, reinterpret_cast<hipStream_t>(stream));

@@ -10,6 +10,9 @@ bool big_conv_supported(const drnmi_conv_args& p);
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s);  // variant -1 = auto
 const char* big_conv_name(const drnmi_conv_args& p, int variant);
 const char* patch_conv_name(const drnmi_conv_args& p);
+// Fused uint8 stem + the 3x3 16->16 conv after it (patch_conv.hip).
+bool stem_l1_ok(const drnmi_conv_args& p, const drnmi_conv_args& q);
+int stem_l1_dispatch(const drnmi_conv_args& p, const drnmi_conv_args& q, hipStream_t s);
 int weight_unit_mask(const void* wgt, int dtype, int rows_pad, int k_pad, uint32_t* mask, int* count, hipStream_t s);
 // W8A8 LDS-DMA implicit GEMM (conv_big.hip, config C5): dtype DRNMI_I8, cin >= 64.
 bool i8_conv_supported(const drnmi_conv_args& p);

@@ -602,6 +602,250 @@ stem_dma_kernel(const drnmi_conv_args p) {
   }
 }
 
+// ---- Fused stem + layer1 (bf16): uint8 frames -> 7x7 3->16 + BN + ReLU -> 3x3 16->16 + BN + ReLU.
+//
+// The stem's 16-channel full-resolution output (64 MB per 1024x2048 frame) is written by the
+// stem and read straight back by layer1 (lmodels/drn.py:132-137, :201-211); here it never
+// leaves the CU.  A workgroup owns an 8 x 64 tile of layer1's output; it DMAs the 16 x 73 raw
+// frame pixels behind it (two tiles ahead, as stem_dma_kernel), normalises them through the
+// per-channel table, computes the 10 x 66 stem outputs the 3x3 conv needs (a wave per 16
+// columns, each patch-row fragment feeding up to 7 stem rows; outside the image the stem
+// outputs are layer1's zero padding, not stem values),
+// keeps them in LDS as bf16, and runs layer1 from there.  Both convs keep the K layouts and
+// MFMA orders of stem_dma_kernel and patch_dma_kernel<16, 16, ...>, so the output is
+// bit-identical to the two-launch path.
+constexpr int kSLTR = 8, kSLTC = 64;                     // layer1 output tile
+constexpr int kSLSR = kSLTR + 2, kSLSC = kSLTC + 2;      // stem outputs needed: 10 x 66
+constexpr int kSLPR = kSLSR + 6, kSLPC = kSLSC + 7;      // stem input patch 16 x 73 (+1: zero kw=7 tap)
+constexpr int kSLRPW = kSLPR / 4;                        // raw rows per wave
+constexpr int kSLRawB = kSLPR * 256;                     // raw rows per ring slot
+constexpr int kSLPatchB = kSLPR * kSLPC * 8;
+constexpr int kSLStemPix = kSLSR * kSLSC;
+constexpr int kSLStemB = kSLStemPix * 32;                // 16 bf16 channels per stem pixel
+constexpr int kSLLDS = 3 * kSLRawB + kSLPatchB + kSLStemB + 3 * 256 * 2;
+static_assert(kSLPatchB % 16 == 0 && kSLStemB % 16 == 0, "16-B aligned LDS regions");
+static_assert(kSLPR % 4 == 0 && 2 * kSLSR <= 32 && kSLSR % 2 == 0, "raw rows over 4 waves; edge columns in two groups");
+
+#ifndef DRNMI_SL_WAVES
+#define DRNMI_SL_WAVES 3      // waves per SIMD the fused stem is register-allocated for
+#endif
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(DRNMI_SL_WAVES)))
+stem_l1_kernel(const drnmi_conv_args p, const drnmi_conv_args q) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* raw = smem;
+  bf16_t* patch = reinterpret_cast<bf16_t*>(smem + 3 * kSLRawB);
+  char* stile = smem + 3 * kSLRawB + kSLPatchB;
+  bf16_t* lut = reinterpret_cast<bf16_t*>(stile + kSLStemB);
+  constexpr int NK0 = 7, NK1 = 5, PFW = kSLTR * kSLTC / 64, ST = PFW;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int kq = lane >> 4;
+  const int H = p.h, W = p.w;
+  const int tiles_w = (W + kSLTC - 1) / kSLTC;
+  const int tiles_h = (H + kSLTR - 1) / kSLTR;
+  const int ntiles = p.n * tiles_w * tiles_h;
+
+  for (int i = tid; i < 3 * 256; i += kThreads) {
+    const int c = i >> 8;
+    const float v = static_cast<float>(i & 255);
+    lut[i] = f32_to_bf16((v / 255.0f - p.mean[c]) / p.std[c]);
+  }
+  const bf16_t* __restrict__ wt0 = reinterpret_cast<const bf16_t*>(p.wgt);
+  const bf16_t* __restrict__ wt1 = reinterpret_cast<const bf16_t*>(q.wgt);
+  bf16x8 wa0[NK0], wa1[NK1];
+#pragma unroll
+  for (int ks = 0; ks < NK0; ++ks)
+    wa0[ks] = *reinterpret_cast<const bf16x8*>(wt0 + static_cast<int64_t>(lane & 15) * p.k_pad + ks * 32 + 8 * kq);
+#pragma unroll
+  for (int ks = 0; ks < NK1; ++ks)
+    wa1[ks] = *reinterpret_cast<const bf16x8*>(wt1 + static_cast<int64_t>(lane & 15) * q.k_pad + ks * 32 + 8 * kq);
+  float sc0[4], sh0[4], sc1[4], sh1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sc0[j] = p.scale != nullptr ? p.scale[kq * 4 + j] : 1.f;
+    sh0[j] = p.shift[kq * 4 + j];
+    sc1[j] = q.scale != nullptr ? q.scale[kq * 4 + j] : 1.f;
+    sh1[j] = q.shift[kq * 4 + j];
+  }
+  const int frame_bytes = H * W * 3;
+  const int total = p.n * frame_bytes;          // < 2^31 (stem_l1_ok)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.x), 0, total, 0x00020000);
+  auto tile_org = [&](int b, int& n, int& oh0, int& ow0) {
+    n = b / (tiles_w * tiles_h);
+    const int rem = b - n * tiles_w * tiles_h;
+    oh0 = (rem / tiles_w) * kSLTR;
+    ow0 = (rem % tiles_w) * kSLTC;
+  };
+  auto issue = [&](int b, int slot) {           // raw rows oh0-4 .. oh0+kSLTR+3 from column ow0-4
+    int n, oh0, ow0;
+    tile_org(b, n, oh0, ow0);
+#pragma unroll
+    for (int j = 0; j < kSLRPW; ++j) {
+      const int r = wave + 4 * j;
+      const int ih = oh0 - 4 + r;
+      const int start = n * frame_bytes + (ih * W + ow0 - 4) * 3;
+      const int a0 = start >= 0 ? (start & ~3) : -((-start + 3) & ~3);
+      const int o = a0 + lane * 4;
+      const bool ok = static_cast<unsigned>(ih) < static_cast<unsigned>(H) && o >= 0;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(raw + slot * kSLRawB + r * 256), 4,
+          ok ? static_cast<unsigned>(o) : 0xffffffffu, 0, 0, 0);
+    }
+  };
+  // raw bytes -> normalised bf16 patch [12][73][4]; wave w converts the rows it DMA'd
+  // (w, w+4, w+8) with the row terms wave-uniform, lanes over the 73 columns
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  auto convert = [&](int b, int slot) {
+    int n, oh0, ow0;
+    tile_org(b, n, oh0, ow0);
+    const int iw0 = ow0 - 4;
+    const unsigned char* rb = reinterpret_cast<const unsigned char*>(raw + slot * kSLRawB);
+#pragma unroll
+    for (int j = 0; j < kSLRPW; ++j) {
+      const int r = wv + 4 * j;
+      const int ih = oh0 - 4 + r;
+      const bool row_ok = static_cast<unsigned>(ih) < static_cast<unsigned>(H);
+      const int start = n * frame_bytes + (ih * W + iw0) * 3;
+      const int a0 = start >= 0 ? (start & ~3) : -((-start + 3) & ~3);
+      // a row that reaches the batch's final partial dword reads global memory instead
+      const bool tail = start + kSLPC * 3 > (total & ~3);
+      const unsigned char* rowp = tail ? reinterpret_cast<const unsigned char*>(p.x) + start : rb + r * 256 + (start - a0);
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int pc = lane + 64 * h2;
+        if (h2 == 1 && pc >= kSLPC) break;
+        uint2 v = make_uint2(0, 0);
+        if (row_ok && static_cast<unsigned>(iw0 + pc) < static_cast<unsigned>(W)) {
+          const unsigned char* px = rowp + pc * 3;
+          int c0 = px[0], c1 = px[1], c2 = px[2];
+          if (p.bgr) { const int t = c0; c0 = c2; c2 = t; }
+          v.x = static_cast<uint32_t>(lut[c0]) | (static_cast<uint32_t>(lut[256 + c1]) << 16);
+          v.y = static_cast<uint32_t>(lut[512 + c2]);
+        }
+        *reinterpret_cast<uint2*>(patch + (r * kSLPC + pc) * 4) = v;
+      }
+    }
+  };
+
+  // layer1 B-fragment offsets (patch_dma_kernel<16, 16, 1, 4, 64>): k = tap * 16 + ci
+  int boff[NK1];
+#pragma unroll
+  for (int ks = 0; ks < NK1; ++ks) {
+    const int k0 = ks * 32 + 8 * kq;
+    const int tap = k0 / 16, ci = k0 % 16;
+    boff[ks] = tap < 9 ? (((tap / 3) * kSLSC + tap % 3) * 16 + ci) * 2 : -1;
+  }
+  const int64_t ybytes = static_cast<int64_t>(q.n) * q.ho * q.wo * 16 * 2;
+  const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
+      q.y, 0, static_cast<int>(ybytes < 0x7fffffff ? ybytes : 0x7fffffff), 0x00020000);
+
+  const int b0 = blockIdx.x;
+  const int G = gridDim.x;
+  if (b0 < ntiles) issue(b0, 0);
+  if (b0 + G < ntiles) issue(b0 + G, 1);
+  int t = 0;
+  for (int b = b0; b < ntiles; b += G, ++t) {
+    // retire tile t's raw rows: younger ops are stores(t-2), rows(t+1), stores(t-1)
+    if (t >= 2 && b + G < ntiles) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kSLRPW + 2 * ST) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (b + 2 * G < ntiles) issue(b + 2 * G, (t + 2) % 3);
+    convert(b, t % 3);
+    __syncthreads();
+
+    int n, oh0, ow0;
+    tile_org(b, n, oh0, ow0);
+    // stem.  Wave w owns stem columns 16w .. 16w+15 over the kSLSR stem rows: patch row r feeds stem
+    // row q = r - kh through kernel row kh, so each B fragment is read once and used by up to 7
+    // MFMAs (per accumulator the kh order is stem_dma_kernel's: bit-identical).  Columns 64, 65
+    // (x kSLSR rows) are two extra groups on waves 0 and 1.
+    auto stem_store = [&](const f32x4& acc, int q, int sc) {
+      const int ih = oh0 - 1 + q, iw = ow0 - 1 + sc;
+      const bool inside = static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                          static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+      float v[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v[jj] = acc[jj] * sc0[jj] + sh0[jj];
+        if (p.relu) v[jj] = fmaxf(v[jj], 0.f);
+        if (!inside) v[jj] = 0.f;                  // layer1's zero padding
+      }
+      u32x2_t o;
+      o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+      o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+      *reinterpret_cast<u32x2_t*>(stile + ((q * kSLSC + sc) * 16 + kq * 4) * 2) = o;
+    };
+    // (two passes of kSLSR / 2 stem rows: half the accumulators live at a time)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      constexpr int HR = kSLSR / 2;
+      const int sc = wv * 16 + (lane & 15);
+      f32x4 acc[HR];
+#pragma unroll
+      for (int q = 0; q < HR; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < HR + NK0 - 1; ++r) {
+        // k = kh*32 + kw*4 + c: fragment = taps kw = 2kq, 2kq+1 of patch row half*HR + r
+        const bf16_t* src = patch + ((half * HR + r) * kSLPC + sc + 2 * kq) * 4;
+        const uint2 lo = *reinterpret_cast<const uint2*>(src);
+        const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+#pragma unroll
+        for (int kh = 0; kh < NK0; ++kh) {
+          const int q = r - kh;
+          if (q >= 0 && q < HR) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa0[kh], bv, acc[q], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < HR; ++q) stem_store(acc[q], half * HR + q, sc);
+    }
+    if (wv < 2) {
+      const int e = wv * 16 + (lane & 15);         // 2 x kSLSR pixels: rows e / 2, columns 64 + e % 2
+      const int q = (e < 2 * kSLSR ? e : 2 * kSLSR - 1) / 2, sc = 64 + (e & 1);
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < NK0; ++kh) {
+        const bf16_t* src = patch + ((q + kh) * kSLPC + sc + 2 * kq) * 4;
+        const uint2 lo = *reinterpret_cast<const uint2*>(src);
+        const uint2 hi = *reinterpret_cast<const uint2*>(src + 4);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa0[kh], __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y)),
+                                                      acc, 0, 0, 0);
+      }
+      if (e < 2 * kSLSR) stem_store(acc, q, sc);
+    }
+    __syncthreads();
+
+    // layer1 from the stem tile
+#pragma unroll 2
+    for (int qq = 0; qq < PFW; ++qq) {
+      const int idx = (wave + 4 * qq) * 16 + (lane & 15);
+      const int r = idx / kSLTC, c = idx % kSLTC;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NK1; ++ks) {
+        bf16x8 bv = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+        if (boff[ks] >= 0) bv = *reinterpret_cast<const bf16x8*>(stile + boff[ks] + (r * kSLSC + c) * 32);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[ks], bv, acc, 0, 0, 0);
+      }
+      const int oh = oh0 + r, ow = ow0 + c;
+      const bool ok = oh < q.ho && ow < q.wo;
+      float v[4];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v[jj] = acc[jj] * sc1[jj] + sh1[jj];
+        if (q.relu) v[jj] = fmaxf(v[jj], 0.f);
+      }
+      u32x2_t o;
+      o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+      o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+      const unsigned pix = static_cast<unsigned>((n * q.ho + oh) * q.wo + ow);
+      __builtin_amdgcn_raw_buffer_store_b64(o, ys, ok ? (pix * 16 + kq * 4) * 2 : 0xffffffffu, 0, 0);
+    }
+  }
+}
+
 int g_num_cus = 0;
 
 template <int CIN, int COUT, int KS, int S, int TR, int TC, bool SRC_U8, bool X6 = false>
@@ -645,6 +889,29 @@ hipError_t launch_stem_dma(const drnmi_conv_args& p, hipStream_t s) {
   const int64_t cap = static_cast<int64_t>(g_num_cus) * per_cu;
   hipLaunchKernelGGL(stem_dma_kernel, dim3(static_cast<unsigned>(tiles < cap ? tiles : cap)), dim3(kThreads),
                      kStemLDS, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_stem_l1(const drnmi_conv_args& p, const drnmi_conv_args& q, hipStream_t s) {
+  static int per_cu = 0;
+  if (per_cu == 0) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(stem_l1_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kSLLDS);
+    if (e != hipSuccess) return e;
+    int dev = 0, cus = 0, blocks = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, reinterpret_cast<const void*>(stem_l1_kernel),
+                                                     kThreads, kSLLDS) != hipSuccess || blocks <= 0)
+      blocks = 1;
+    g_num_cus = cus;
+    per_cu = blocks;
+  }
+  const int64_t tiles = static_cast<int64_t>(p.n) * ((p.h + kSLTR - 1) / kSLTR) * ((p.w + kSLTC - 1) / kSLTC);
+  const int64_t cap = static_cast<int64_t>(g_num_cus) * per_cu;
+  hipLaunchKernelGGL(stem_l1_kernel, dim3(static_cast<unsigned>(tiles < cap ? tiles : cap)), dim3(kThreads),
+                     kSLLDS, s, p, q);
   return hipGetLastError();
 }
 
@@ -750,6 +1017,27 @@ const char* patch_conv_name(const drnmi_conv_args& p) {
     return dma_ok(p) ? "patch_dma_kernel<16, 32, 2, 4, 32>" : "patch_conv_kernel<16, 32, 3, 2, 4, 64, false>";
   if (p.cin == 32 && p.cout == 64 && p.ks == 3 && p.stride == 2) return "patch_conv_kernel<32, 64, 3, 2, 2, 64, false>";
   return nullptr;
+}
+
+// stem (uint8 frames, 7x7 3->16, the stem_dma_kernel contract) fused with the 3x3 16->16
+// stride-1 conv that consumes it (the patch_dma_kernel<16, 16, ...> contract)
+bool stem_l1_ok(const drnmi_conv_args& p, const drnmi_conv_args& q) {
+  const bool stem = p.src_u8 && p.dtype == DRNMI_BF16 && p.out_dtype == DRNMI_BF16 && p.cin == 4 && p.cout == 16 &&
+                    p.ks == 7 && p.stride == 1 && p.pad == 3 && p.dil == 1 && p.k == 224 && p.k_pad == 224 &&
+                    p.res == nullptr && p.x != nullptr && p.wgt != nullptr && p.shift != nullptr && p.n > 0 &&
+                    p.h > 0 && p.w >= 8 && p.ho == p.h && p.wo == p.w &&
+                    static_cast<int64_t>(p.n) * p.h * p.w * 3 < (int64_t(1) << 31);
+  const bool l1 = !q.src_u8 && q.dtype == DRNMI_BF16 && q.out_dtype == DRNMI_BF16 && q.cin == 16 && q.cout == 16 &&
+                  q.ks == 3 && q.stride == 1 && q.pad == 1 && q.dil == 1 && q.k == 144 && q.k_pad >= 160 &&
+                  q.res == nullptr && q.x2 == nullptr && q.y != nullptr && q.wgt != nullptr && q.shift != nullptr &&
+                  q.y_sc == 1 && q.y_sp == 16 && q.n == p.n && q.h == p.h && q.w == p.w && q.ho == q.h && q.wo == q.w &&
+                  static_cast<int64_t>(q.n) * q.ho * q.wo * 16 * 2 < (int64_t(1) << 31);
+  return stem && l1;
+}
+
+int stem_l1_dispatch(const drnmi_conv_args& p, const drnmi_conv_args& q, hipStream_t s) {
+  if (!stem_l1_ok(p, q)) return DRNMI_EINVAL;
+  return static_cast<int>(launch_stem_l1(p, q, s));
 }
 
 }  // namespace drnmi

@@ -68,6 +68,8 @@ SIGNATURES = {
     "drnmi_conv2d_bn_act": (ctypes.c_int, [ctypes.POINTER(ConvArgs), _VP]),
     "drnmi_conv_tile_name": (ctypes.c_char_p, [ctypes.c_int]),
     "drnmi_conv_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(ConvArgs)]),
+    "drnmi_stem_layer1": (ctypes.c_int, [ctypes.POINTER(ConvArgs), ctypes.POINTER(ConvArgs), _VP]),
+    "drnmi_stem_layer1_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(ConvArgs), ctypes.POINTER(ConvArgs)]),
     "drnmi_conv_num_tiles": (ctypes.c_int, []),
     "drnmi_frame_ingest_u8": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _VP, _VP, _I32, _I32, _VP]),
     "drnmi_nchw_to_nhwc": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _I32, _I32, _I32, _VP]),

@@ -407,6 +407,9 @@ def _uses_patch(nd: ConvNode, cin_stride: int, precision: str) -> bool:
 
 # bf16: fold 1x1 downsamples into the block's last conv (PackedNet._fuse_downsamples)
 FUSE_DOWNSAMPLE = True
+# bf16 video path: the uint8 stem and the 3x3 16->16 layer1 conv run as one kernel
+# (drnmi_stem_layer1); the stem output is never written.  Plans with keep_all keep two launches.
+FUSE_STEM = True
 
 
 def _route_name(nd: ConvNode, cin_stride: int, cin2: int = 0) -> str:
@@ -521,7 +524,21 @@ class Plan:
         self.keep_all = keep_all
         self.args = [None if i in self.skip else self._conv_args(nd) for i, nd in enumerate(g.nodes)]
         self.stem_u8 = self._stem_u8_args()
+        self.stem_fused = self._stem_fusable(reads_of)
         self.src = "nchw"
+
+    def _stem_fusable(self, reads_of) -> bool:
+        """The u8 stem and layer1 can run as one launch (drnmi_stem_layer1) when layer1 is the
+        stem output's only reader and the library takes the pair."""
+        nodes = self.packed.graph.nodes
+        if not (FUSE_STEM and self.fuse and self.stem_u8 is not None and len(nodes) > 1):
+            return False
+        if self.args[1] is None or nodes[1].x_val != nodes[0].dst:
+            return False
+        if any(nodes[0].dst in reads_of[i] for i in range(2, len(nodes))) or self.packed.quant_after.get(0):
+            return False
+        lib = _lib.load()
+        return lib.drnmi_stem_layer1_kernel_name(ctypes.byref(self.stem_u8), ctypes.byref(self.args[1])) is not None
 
     def _conv_args(self, nd: ConvNode) -> _lib.ConvArgs:
         pk = self.packed
@@ -599,14 +616,19 @@ class Plan:
     # ------------------------------------------------------------------ execution
     def run_backbone(self, stream: int, timing_hook=None):
         lib = _lib.load()
+        fused_stem = self.src == "u8" and self.stem_fused
         for i, (a, nd) in enumerate(zip(self.args, self.packed.graph.nodes)):
-            if a is None:
-                continue                          # downsample folded into the block's last conv
+            if a is None or (i == 1 and fused_stem):
+                continue                          # folded into another launch
             if i == 0 and self.src == "u8":
                 a = self.stem_u8
             if timing_hook is not None:
                 timing_hook(i, nd, True)
-            _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), f"conv {nd.name}")
+            if i == 0 and fused_stem:
+                _lib.check(lib.drnmi_stem_layer1(ctypes.byref(a), ctypes.byref(self.args[1]), ctypes.c_void_p(stream)),
+                           "stem_layer1")
+            else:
+                _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), f"conv {nd.name}")
             if timing_hook is not None:
                 timing_hook(i, nd, False)
             for v in self.packed.quant_after.get(i, ()):

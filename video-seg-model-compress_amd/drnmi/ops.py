@@ -118,8 +118,8 @@ def up8_logsoftmax_argmax(logits: torch.Tensor, up_plane: torch.Tensor, want_log
     return lp, lab
 
 
-def stem_u8(frames_u8: torch.Tensor, weight: torch.Tensor, scale, shift, mean, std, bgr=False, relu=True):
-    """Fused ingest + 7x7 stem (bf16 patch kernel): uint8 [N,H,W,3] -> bf16 NHWC [N,H,W,cout]."""
+def _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu):
+    """ConvArgs of the fused-ingest 7x7 stem (PATCH, src_u8) + the tensors they point into."""
     from .engine import STEM_U8_K
     n, h, w, _ = frames_u8.shape
     cout = weight.shape[0]
@@ -133,10 +133,8 @@ def stem_u8(frames_u8: torch.Tensor, weight: torch.Tensor, scale, shift, mean, s
     sh = torch.zeros(wpk.shape[0], device=dev)
     sc[:cout] = scale.float()
     sh[:cout] = shift.float()
-    y = torch.empty(n, h, w, cout, device=dev, dtype=torch.bfloat16)
     a = _lib.ConvArgs()
-    a.x, a.wgt, a.scale, a.shift, a.res, a.y = frames_u8.data_ptr(), wpk.data_ptr(), sc.data_ptr(), \
-        sh.data_ptr(), None, y.data_ptr()
+    a.x, a.wgt, a.scale, a.shift, a.res = frames_u8.data_ptr(), wpk.data_ptr(), sc.data_ptr(), sh.data_ptr(), None
     a.y_sn, a.y_sp, a.y_sc = h * w * cout, cout, 1
     a.n, a.h, a.w, a.cin = n, h, w, 4
     a.ho, a.wo, a.cout, a.cout_pad = h, w, cout, wpk.shape[0]
@@ -150,8 +148,43 @@ def stem_u8(frames_u8: torch.Tensor, weight: torch.Tensor, scale, shift, mean, s
     a.bgr = 1 if bgr else 0
     for i in range(3):
         a.mean[i], a.std[i] = float(mean[i]), float(std[i])
+    return a, (wpk, sc, sh)
+
+
+def stem_u8(frames_u8: torch.Tensor, weight: torch.Tensor, scale, shift, mean, std, bgr=False, relu=True):
+    """Fused ingest + 7x7 stem (bf16 patch kernel): uint8 [N,H,W,3] -> bf16 NHWC [N,H,W,cout]."""
+    n, h, w, _ = frames_u8.shape
+    a, keep = _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu)
+    y = torch.empty(n, h, w, weight.shape[0], device=frames_u8.device, dtype=torch.bfloat16)
+    a.y = y.data_ptr()
     lib = _lib.load()
-    _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr(dev))), "stem_u8")
+    _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr(frames_u8.device))), "stem_u8")
+    return y
+
+
+def stem_layer1_u8(frames_u8: torch.Tensor, w0: torch.Tensor, scale0, shift0, w1: torch.Tensor, scale1, shift1,
+                   mean, std, bgr=False):
+    """drnmi_stem_layer1: uint8 frames -> stem 7x7 3->16 + BN + ReLU -> 3x3 16->16 + BN + ReLU in one
+    launch (the stem output stays on chip) -> bf16 NHWC [N,H,W,16]."""
+    n, h, w, _ = frames_u8.shape
+    dev = frames_u8.device
+    a0, keep0 = _stem_u8_args(frames_u8, w0, scale0, shift0, mean, std, bgr, True)
+    wpk, k = pack_conv_weight(w1, 16, torch.bfloat16)
+    sc = torch.ones(wpk.shape[0], device=dev)
+    sh = torch.zeros(wpk.shape[0], device=dev)
+    sc[:16], sh[:16] = scale1.float(), shift1.float()
+    y = torch.empty(n, h, w, 16, device=dev, dtype=torch.bfloat16)
+    a1 = _lib.ConvArgs()
+    a1.x, a1.wgt, a1.scale, a1.shift, a1.res, a1.y = a0.x, wpk.data_ptr(), sc.data_ptr(), sh.data_ptr(), None, \
+        y.data_ptr()
+    a1.y_sn, a1.y_sp, a1.y_sc = h * w * 16, 16, 1
+    a1.n, a1.h, a1.w, a1.cin, a1.ho, a1.wo, a1.cout, a1.cout_pad = n, h, w, 16, h, w, 16, wpk.shape[0]
+    a1.ks, a1.stride, a1.pad, a1.dil, a1.k, a1.k_pad, a1.relu = 3, 1, 1, 1, k, wpk.shape[1], 1
+    a1.dtype = a1.out_dtype = _lib.DRNMI_BF16
+    a1.tile, a1.algo = -1, _lib.ALGO_PATCH
+    lib = _lib.load()
+    _lib.check(lib.drnmi_stem_layer1(ctypes.byref(a0), ctypes.byref(a1), ctypes.c_void_p(_lib.stream_ptr(dev))),
+               "stem_layer1")
     return y
 
 
