@@ -27,7 +27,7 @@ typedef __attribute__((address_space(1))) const void g_void_t;
 __device__ uint4 g_halo_zero[64];   // zero-initialised source of padded pixels
 
 constexpr int kTR = 4, kTC = 64;     // output block: rows x columns
-constexpr int kNST = 3;              // weight ring stages
+constexpr int kNST = 3;              // weight ring stages (4-5 stages cost a workgroup per CU: slower)
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((g_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
@@ -49,14 +49,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 // LDS bytes of the patch, rounded up to whole 1-KB DMA pieces
-__host__ __device__ constexpr int patch_bytes(int cin, int dil) {
-  return ((kTR + 2 * dil) * (kTC + 2 * dil) * cin * 2 + 1023) / 1024 * 1024;
+__host__ __device__ constexpr int patch_bytes(int cin, int dil, int tc) {
+  return ((kTR + 2 * dil) * (tc + 2 * dil) * cin * 2 + 1023) / 1024 * 1024;
 }
 
-template <int CIN, int WC>
+template <int CIN, int WC, int TC>
 __global__ void __launch_bounds__(256 * WC, 1)
 conv_halo_kernel(const drnmi_conv_args p) {
   constexpr int NW = 4 * WC;
+  constexpr int FN = TC / 16;            // pixel fragments per wave (one output row)
   constexpr int ROWB = CIN * 2;          // patch row bytes
   constexpr int CPR = ROWB / 16;         // chunks per patch row
   constexpr int RPP = 1024 / ROWB;       // patch rows per DMA piece
@@ -75,16 +76,16 @@ conv_halo_kernel(const drnmi_conv_args p) {
   const int fr = lane & 15;
   const int fq = lane >> 4;
   const int H = p.h, W = p.w, dil = p.dil;
-  const int PW = kTC + 2 * dil;
+  const int PW = TC + 2 * dil;
   const int PROWS = (kTR + 2 * dil) * PW;
-  const int tiles_x = (p.wo + kTC - 1) / kTC;
+  const int tiles_x = (p.wo + TC - 1) / TC;
   const int tiles_y = (p.ho + kTR - 1) / kTR;
   const int ntiles = p.n * tiles_y * tiles_x;
   const int tile = xcd_remap(blockIdx.x, ntiles);
   const int n = tile / (tiles_y * tiles_x);
   const int trem = tile - n * tiles_y * tiles_x;
   const int oh0 = (trem / tiles_x) * kTR;
-  const int ow0 = (trem - (trem / tiles_x) * tiles_x) * kTC;
+  const int ow0 = (trem - (trem / tiles_x) * tiles_x) * TC;
   const uint16_t* __restrict__ x = reinterpret_cast<const uint16_t*>(p.x);
   const uint16_t* __restrict__ wt = reinterpret_cast<const uint16_t*>(p.wgt);
   constexpr int NCB = CIN / 64;
@@ -94,7 +95,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
   // weights (scale == NULL); those loads go out ahead of the DMA and hide under it
   const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
   const int oh = oh0 + wp;
-  f32x4 acc[4][4];
+  f32x4 acc[4][FN];
 #pragma unroll
   for (int fm = 0; fm < 4; ++fm) {
     const int co = wc * 64 + fm * 16 + fq * 4;
@@ -104,12 +105,12 @@ conv_halo_kernel(const drnmi_conv_args p) {
       a0 = f32x4{sh.x, sh.y, sh.z, sh.w};
     }
 #pragma unroll
-    for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = a0;
+    for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = a0;
   }
   if (p.scale == nullptr && res != nullptr && oh < p.ho) {
-    uint2 rv[4][4];
+    uint2 rv[4][FN];
 #pragma unroll
-    for (int fn = 0; fn < 4; ++fn) {
+    for (int fn = 0; fn < FN; ++fn) {
       const int ow = ow0 + fn * 16 + fr;
       const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + (ow < p.wo ? ow : p.wo - 1);
 #pragma unroll
@@ -119,7 +120,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-      for (int fn = 0; fn < 4; ++fn) {
+      for (int fn = 0; fn < FN; ++fn) {
         acc[fm][fn][0] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x & 0xffff));
         acc[fm][fn][1] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x >> 16));
         acc[fm][fn][2] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y & 0xffff));
@@ -167,7 +168,8 @@ conv_halo_kernel(const drnmi_conv_args p) {
 
   for (int t = 0; t < nk; ++t) {
     // retire step t (the patch went out before every weight piece, so it is retired too)
-    if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(A_PIECES) : "memory");
+    // younger: the weight pieces of steps t+1 .. t+kNST-2
+    if (t + kNST - 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"((kNST - 2) * A_PIECES) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -177,13 +179,16 @@ conv_halo_kernel(const drnmi_conv_args p) {
     const int tap = t - cb * 9;
     const int dh = (tap / 3) * dil, dw = (tap - (tap / 3) * 3) * dil;
     const int prow0 = (wp + dh) * PW + dw;            // patch row of this wave's pixel 0
-    bf16x8 af[4], bfr[4];
+    bf16x8 af[4], bfr[FN];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         const int r = wc * 64 + f * 16 + fr;
         af[f] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + hswz<128>(r, sub * 4 + fq) * 16);
+      }
+#pragma unroll
+      for (int f = 0; f < FN; ++f) {
         const int pr = prow0 + f * 16 + fr;
         bfr[f] = *reinterpret_cast<const bf16x8*>(patch + pr * ROWB + hswz<ROWB>(pr, cb * 8 + sub * 4 + fq) * 16);
       }
@@ -194,7 +199,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
-        for (int fn = 0; fn < 4; ++fn)
+        for (int fn = 0; fn < FN; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
     }
   }
@@ -202,7 +207,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
   // --- epilogue: lane owns channels co..co+3 of pixel (oh0 + wp, ow0 + fn*16 + fr)
   if (oh >= p.ho) return;
 #pragma unroll
-  for (int fn = 0; fn < 4; ++fn) {
+  for (int fn = 0; fn < FN; ++fn) {
     const int ow = ow0 + fn * 16 + fr;
     if (ow >= p.wo) continue;
     const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow;
@@ -238,18 +243,26 @@ conv_halo_kernel(const drnmi_conv_args p) {
   }
 }
 
+// output-block width.  32 columns for the 64 -> 64 conv (three workgroups per CU instead of two)
+// measured the same as 64 (128.0 vs 128.3 us, D-22 layer3, 8 frames)
+#ifndef DRNMI_HALO_TC_64_64
+#define DRNMI_HALO_TC_64_64 64
+#endif
+constexpr int halo_tc(int cin, int cout) { return cin == 64 && cout == 64 ? DRNMI_HALO_TC_64_64 : 64; }
+
 template <int CIN, int WC>
 hipError_t launch_halo(const drnmi_conv_args& p, hipStream_t s) {
-  const int lds = kNST * 64 * WC * 128 + patch_bytes(CIN, p.dil);
+  constexpr int TC = halo_tc(CIN, 64 * WC);
+  const int lds = kNST * 64 * WC * 128 + patch_bytes(CIN, p.dil, TC);
   static int attr_lds = 0;
   if (attr_lds < lds) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<CIN, WC>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<CIN, WC, TC>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_lds = lds;
   }
-  const int64_t tiles = static_cast<int64_t>(p.n) * ((p.ho + kTR - 1) / kTR) * ((p.wo + kTC - 1) / kTC);
-  hipLaunchKernelGGL((conv_halo_kernel<CIN, WC>), dim3(static_cast<unsigned>(tiles)), dim3(256 * WC), lds, s, p);
+  const int64_t tiles = static_cast<int64_t>(p.n) * ((p.ho + kTR - 1) / kTR) * ((p.wo + TC - 1) / TC);
+  hipLaunchKernelGGL((conv_halo_kernel<CIN, WC, TC>), dim3(static_cast<unsigned>(tiles)), dim3(256 * WC), lds, s, p);
   return hipGetLastError();
 }
 
@@ -265,7 +278,7 @@ bool halo_conv_supported(const drnmi_conv_args& p) {
   if (p.k != 9 * p.cin || p.k_pad != p.k || p.y_sc != 1 || p.y_sp != p.cout || p.dil < 1 || p.dil > 8)
     return false;
   const int wc = p.cout / 64;
-  return kNST * 64 * wc * 128 + patch_bytes(p.cin, p.dil) <= 160 * 1024;
+  return kNST * 64 * wc * 128 + patch_bytes(p.cin, p.dil, halo_tc(p.cin, p.cout)) <= 160 * 1024;
 }
 
 int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
@@ -276,9 +289,12 @@ int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   return static_cast<int>(e);
 }
 
+#define DRNMI_STR2(x) #x
+#define DRNMI_STR(x) DRNMI_STR2(x)
 const char* halo_conv_name(const drnmi_conv_args& p) {
-  if (p.cin == 64) return p.cout == 64 ? "conv_halo_kernel<64, 1>" : "conv_halo_kernel<64, 2>";
-  return p.cout == 64 ? "conv_halo_kernel<128, 1>" : "conv_halo_kernel<128, 2>";
+  if (p.cin == 64)
+    return p.cout == 64 ? "conv_halo_kernel<64, 1, " DRNMI_STR(DRNMI_HALO_TC_64_64) ">" : "conv_halo_kernel<64, 2, 64>";
+  return p.cout == 64 ? "conv_halo_kernel<128, 1, 64>" : "conv_halo_kernel<128, 2, 64>";
 }
 
 }  // namespace drnmi
