@@ -23,6 +23,7 @@ SHAPES = [  # name, cin, cout, ks, stride, dil, H(in), W(in), residual
     ("l3 64x64 +res", 64, 64, 3, 1, 1, 256, 512, True),
     ("l3.0c1 32->64 s2", 32, 64, 3, 2, 1, 512, 1024, False),
     ("l3.0ds 32->64 1x1 s2", 32, 64, 1, 2, 1, 512, 1024, False),
+    ("l4.0ds 64->128 1x1 s2", 64, 128, 1, 2, 1, 256, 512, False),
     ("seg 512->19 1x1", 512, 19, 1, 1, 1, 128, 256, False),
 ]
 dev = "cuda"

@@ -1026,6 +1026,10 @@ int auto_variant(const drnmi_conv_args& p) {
   if (DRNMI_AUTO_PERSIST && p.cout % 256 == 0) return 7;
   // cout <= 32 (the seg 1x1) also takes the 64-wide BK-32 tile: 57 vs 66 us on the D-22 seg conv
   // at batch 8 (scripts/conv_micro.py) — two workgroups fit per CU where the 32-wide 3 x 36 KB ring fits one
+  // 64 -> 128 (D-22 layer4.0 conv1 / downsample, stride 2): the 64-wide BK-32 tile too, two
+  // workgroups per CU against one for the 128 x 256 x 3-stage ring: 98 vs 116 us (3x3), 50 vs
+  // 75 us (1x1) at batch 8 (scripts/conv_micro.py); the fused-x2 instantiations are bases 0/1
+  if (p.cin <= 64 && p.cout % 256 != 0 && p.x2 == nullptr) return 2;
   return p.cout % 256 == 0 ? 1 : p.cout % 128 == 0 ? 0 : 2;
 }
 
