@@ -137,10 +137,13 @@ def cpu_baseline(args, seconds):
     sd = synth_state_dict(m, 0)
     frames = synth_frames(7, 2, args.height, args.width)
 
+    labels = {}
+
     def one(i):
         x = O.preprocess_u8(frames[i % 2:i % 2 + 1])
         lp, _, _ = O.drnseg_forward(sd, args.arch, x)
-        return torch.max(lp, 1)[1].cpu().numpy()
+        labels[i % 2] = torch.max(lp, 1)[1][0].cpu().numpy()
+        return labels[i % 2]
 
     one(0)                                   # warm-up frame (untimed)
     n, t0 = 0, time.perf_counter()
@@ -162,7 +165,26 @@ def cpu_baseline(args, seconds):
     return {"value": n / el, "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{n} frames of {args.height}x{args.width} after 1 warm-up frame, batch 1, "
                       f"oracle/drn_oracle.py fp32 NCHW torch-CPU ({threads} threads = all affine host cores "
-                      f"within the cgroup quota, {cpu_model})"}
+                      f"within the cgroup quota, {cpu_model})"}, (frames, labels)
+
+
+def parity_vs_ref(args, model, frames, ref_labels, dev):
+    """The measured path's labels on the CPU baseline's frames vs the oracle's (the reference
+    restated, pinned to its goldens): pixel agreement and mIoU with the reference labels as
+    ground truth (BASELINE.json metric "mIoU vs ref"; semantic_seg.py:293-300 fast_hist)."""
+    import numpy as np
+    import torch
+
+    from drnmi import metrics
+    from drnmi.drnseg import INFO_MEAN, INFO_STD
+    got = model.segment(torch.from_numpy(frames).to(dev), INFO_MEAN, INFO_STD, False).long()
+    ref = torch.from_numpy(np.stack([ref_labels[i] for i in range(len(frames))])).long().to(dev)
+    hist = metrics.fast_hist(got.flatten(), ref.flatten(), 19)
+    return {"frames": len(frames), "precision": args.precision,
+            "label_agreement": float((got == ref).float().mean()),
+            "label_mismatches": int((got != ref).sum()),
+            "miou_vs_ref": float(metrics.miou(hist.cpu().numpy())),
+            "reference": "oracle/drn_oracle.py fp32 torch-CPU forward, same weights and frames"}
 
 
 def main():
@@ -338,7 +360,9 @@ def main():
     if host is not None:
         out["host_frames"] = host
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        out["cpu_baseline"], (bframes, blabels) = cpu_baseline(args, args.cpu_seconds)
+        if not args.prune:                   # the oracle runs the unpruned synthetic weights
+            out["parity_vs_ref"] = parity_vs_ref(args, model, bframes, blabels, dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

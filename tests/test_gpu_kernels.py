@@ -514,3 +514,24 @@ def test_stem_fused_network_matches_two_launch():
         engine.FUSE_STEM = True
     assert torch.equal(fused, two)
 
+
+
+def test_up8_labels_only_matches_logprob_argmax_at_near_ties():
+    """The labels-only head skips the log-softmax except where the top two up-sampled logits
+    are within 2^-16; there it must reproduce torch.max over the log-probs exactly, including
+    the lower-index choice when the rounding of (v - max) - lse merges the top two."""
+    from drnmi.weights import bilinear_up_kernel
+    c, h, w = 19, 24, 40
+    g = torch.Generator().manual_seed(77)
+    logits = torch.randn(2, c, h, w, generator=g) * 3
+    # near-ties between classes 3 and 11 (11 ahead by a few ulp) on every input pixel
+    logits[:, 11] = logits[:, 3] + logits[:, 3].abs() * 2.0 ** -22
+    logits[:, 3] += 4.0                     # make them the top two
+    logits[:, 11] += 4.0
+    upw = torch.from_numpy(bilinear_up_kernel(16)).to(DEV)
+    lp, lab = ops.up8_logsoftmax_argmax(logits.to(DEV), upw)
+    _, lab8 = ops.up8_logsoftmax_argmax(logits.to(DEV), upw, want_logprobs=False, label_dtype=torch.uint8)
+    torch.cuda.synchronize()
+    assert torch.equal(lab8.long(), lab)
+    assert torch.equal(lab, torch.max(lp, 1)[1])
+    assert int((lab == 3).sum()) > 0 and int((lab == 11).sum()) > 0

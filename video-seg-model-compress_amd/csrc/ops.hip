@@ -201,14 +201,31 @@ up8_lsm_quad_kernel(const float* __restrict__ logits, const float* __restrict__ 
   int arg[4] = {0, 0, 0, 0};
   if (logprobs == nullptr) {
     // Labels only: lp_c = (v_c - max) - lse is a monotone map of v_c, so the argmax of the
-    // up-sampled logits is the argmax of the log-probs (a tie created by the rounding of that
-    // map needs two logits within ~1 ulp of lse: below fp32 summation-order noise).
+    // up-sampled logits is the argmax of the log-probs -- except where the rounding of that map
+    // merges the top two (|lp| < 4 + gap, so only gaps below a few 2^-22): there torch.max over
+    // the log-probs returns the lower class index.  Pixels whose top-2 gap is under 2^-16 take
+    // the log-prob path below (same arithmetic as the logprobs branch), so the labels are those
+    // of argmax(log_softmax) bit for bit; the rest skip the 19 exps.
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      float best = v[0][p];
+      float best = v[0][p], second = -INFINITY;
 #pragma unroll
-      for (int k = 1; k < NC; ++k)
-        if (v[k][p] > best) { best = v[k][p]; arg[p] = k; }
+      for (int k = 1; k < NC; ++k) {
+        if (v[k][p] > best) { second = best; best = v[k][p]; arg[p] = k; }
+        else if (v[k][p] > second) second = v[k][p];
+      }
+      if (best - second < 0x1p-16f) {
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) sum += expf(v[k][p] - vmax[p]);
+        const float lse = logf(sum);
+        float bl = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+          const float lp = (v[k][p] - vmax[p]) - lse;
+          if (lp > bl) { bl = lp; arg[p] = k; }
+        }
+      }
     }
   } else {
     float lse[4];
