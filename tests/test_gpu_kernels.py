@@ -147,6 +147,9 @@ def test_up8_logsoftmax_argmax(h, w):
     _, lab8 = ops.up8_logsoftmax_argmax(logits.to(DEV), upw.to(DEV), want_logprobs=False,
                                         label_dtype=torch.uint8)
     assert torch.equal(lab8.cpu().long(), lab.cpu())
+    _, lab64 = ops.up8_logsoftmax_argmax(logits.to(DEV), upw.to(DEV), want_logprobs=False,
+                                         label_dtype=torch.int64)   # labels-only 8-row kernel, int64
+    assert torch.equal(lab64.cpu(), lab.cpu())
 
 
 @pytest.mark.parametrize("use_bits,from_disk", [(False, False), (True, False), (True, True)])

@@ -262,6 +262,98 @@ up8_lsm_quad_kernel(const float* __restrict__ logits, const float* __restrict__ 
   }
 }
 
+// Labels-only head (no log-prob planes requested: the seg_video path).  The 8 output rows
+// oy = 8*i1-4 .. 8*i1+3 all read input rows (i1-1, i1), so a thread owns 4 output columns x
+// those 8 rows: the 4 taps per class are loaded once for 32 pixels (the quad kernel re-loads
+// them for every output row).  Per pixel: the quad kernel's labels-only arithmetic, near-tie
+// fallback and argmax order, so the labels are identical.
+template <int NC, int LABEL_DTYPE>
+__global__ void __launch_bounds__(256)
+up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict__ up_w,
+                      void* __restrict__ labels, int h, int w) {
+  __shared__ float wk[256];
+  wk[threadIdx.x] = up_w[threadIdx.x];
+  __syncthreads();
+
+  const int H = h * 8, W = w * 8;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i1 = blockIdx.y, i0 = i1 - 1;
+  const int n = blockIdx.z;
+  if (4 * q >= W) return;
+
+  const int j1 = (q + 1) >> 1, j0 = j1 - 1;
+  const bool vi0 = i0 >= 0, vi1 = i1 < h, vj0 = j0 >= 0, vj1 = j1 < w;
+  const int ci0 = vi0 ? i0 : 0, ci1 = vi1 ? i1 : 0, cj0 = vj0 ? j0 : 0, cj1 = vj1 ? j1 : 0;
+  const int64_t plane = static_cast<int64_t>(h) * w;
+  const float* src = logits + static_cast<int64_t>(n) * NC * plane;
+  float s00[NC], s01[NC], s10[NC], s11[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    const float* s = src + k * plane;
+    s00[k] = s[ci0 * w + cj0];
+    s01[k] = s[ci0 * w + cj1];
+    s10[k] = s[ci1 * w + cj0];
+    s11[k] = s[ci1 * w + cj1];
+  }
+  const int kx1_0 = 4 * q + 4 - 8 * j1;   // kx1 of column p is kx1_0 + p, kx0 = kx1 + 8
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int oy_begin = max(0, 8 * i1 - 4), oy_end = min(H, 8 * i1 + 4);
+  for (int oy = oy_begin; oy < oy_end; ++oy) {
+    const int ky1 = oy + 4 - 8 * i1, ky0 = ky1 + 8;
+    int arg[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int kx1 = kx1_0 + p, kx0 = kx1 + 8;
+      const float w00 = (vi0 && vj0) ? wk[ky0 * 16 + kx0] : 0.f;
+      const float w01 = (vi0 && vj1) ? wk[ky0 * 16 + kx1] : 0.f;
+      const float w10 = (vi1 && vj0) ? wk[ky1 * 16 + kx0] : 0.f;
+      const float w11 = (vi1 && vj1) ? wk[ky1 * 16 + kx1] : 0.f;
+      float v[NC];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        float a = s00[k] * w00;
+        a = fmaf(s01[k], w01, a);
+        a = fmaf(s10[k], w10, a);
+        a = fmaf(s11[k], w11, a);
+        v[k] = a;
+      }
+      float best = v[0], second = -INFINITY;
+      int am = 0;
+#pragma unroll
+      for (int k = 1; k < NC; ++k) {
+        if (v[k] > best) { second = best; best = v[k]; am = k; }
+        else if (v[k] > second) second = v[k];
+      }
+      if (best - second < 0x1p-16f) {
+        float vmax = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) vmax = fmaxf(vmax, v[k]);
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) sum += expf(v[k] - vmax);
+        const float lse = logf(sum);
+        float bl = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+          const float lp = (v[k] - vmax) - lse;
+          if (lp > bl) { bl = lp; am = k; }
+        }
+      }
+      arg[p] = am;
+    }
+    const int64_t pix = static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy) * W + 4 * q;
+    if (LABEL_DTYPE == DRNMI_U8) {
+      const uint32_t packed = static_cast<uint32_t>(arg[0]) | (static_cast<uint32_t>(arg[1]) << 8) |
+                              (static_cast<uint32_t>(arg[2]) << 16) | (static_cast<uint32_t>(arg[3]) << 24);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(labels) + pix) = packed;
+    } else {
+      int64_t* o = reinterpret_cast<int64_t*>(labels) + pix;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) o[p] = arg[p];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- bilinear x8 (use_torch_up)
 // nn.UpsamplingBilinear2d(scale_factor=8) (lmodels/drnseg.py:285-287): bilinear with
 // align_corners=True, output 8h x 8w.  Source index and weights as ATen's CPU kernel:
@@ -491,6 +583,15 @@ extern "C" int drnmi_up8_logsoftmax_argmax(const float* logits, const float* up_
   const int W = w * 8;
   dim3 grid(static_cast<unsigned>((W + 255) / 256), static_cast<unsigned>(h * 8), static_cast<unsigned>(n));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (c == 19 && logprobs == nullptr && labels != nullptr) {   // labels only: 8-row kernel
+    dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
+    if (label_dtype == DRNMI_I64) {
+      hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_I64>), go, dim3(256), 0, s, logits, up_w, labels, h, w);
+    } else {
+      hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_U8>), go, dim3(256), 0, s, logits, up_w, labels, h, w);
+    }
+    return static_cast<int>(hipGetLastError());
+  }
   if (c == 19) {   // Cityscapes classes: quad kernel
     dim3 gq(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h * 8), static_cast<unsigned>(n));
     if (label_dtype == DRNMI_I64) {
