@@ -36,9 +36,7 @@ def conv2d_bn_act(x_nhwc: torch.Tensor, weight: torch.Tensor, scale=None, shift=
     n, h, w, cs = x_nhwc.shape
     cout, cin, ks, _ = weight.shape
     dt = x_nhwc.dtype
-    if fold_scale:
-        if packed is not None:
-            raise ValueError("fold_scale packs its own weights")
+    if fold_scale and packed is None:   # (with `packed`, the caller folded the scale already)
         if scale is not None:
             weight = weight * scale.to(weight.device).float().view(-1, 1, 1, 1)
     if packed is None:
