@@ -1,6 +1,7 @@
 """Diagnostic: time the halo-family kernels on the DRN-D-22 layer3/layer4 3x3 shapes (bf16,
 8 frames of 1024x2048 input, BN scale folded = the engine's launch), by forced tile id:
-17 = conv_halo_kernel, 18 = rolling-window kernel.  python scripts/halo_micro.py [tiles...]"""
+17 = conv_halo_kernel (tile 18, the rolling-window experiment, is in git history:
+commit dc4061a).  python scripts/halo_micro.py [tiles...]"""
 import os
 import sys
 
@@ -10,7 +11,7 @@ import torch  # noqa: E402
 
 from drnmi import ops  # noqa: E402
 
-TILES = [int(t) for t in sys.argv[1:]] or [17, 18]
+TILES = [int(t) for t in sys.argv[1:]] or [17]
 B = int(os.environ.get("B", "8"))
 SHAPES = [("l3 64x64 +res", 64, 64, 256, 512), ("l4 128x128 +res", 128, 128, 128, 256)]
 for name, cin, cout, h, w in SHAPES:

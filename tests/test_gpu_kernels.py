@@ -317,27 +317,6 @@ def test_null_scale_seeds_accumulator(shape):
     assert ran >= 2
 
 
-@pytest.mark.parametrize("n,h,w,dil,relu,with_res", [(3, 37, 70, 1, True, True), (2, 64, 128, 1, True, False),
-                                                    (8, 256, 512, 1, True, True), (1, 9, 300, 2, False, True),
-                                                    (2, 130, 66, 4, True, True), (1, 3, 5, 1, True, True)])
-def test_halo_rw_bit_identical_to_halo(n, h, w, dil, relu, with_res):
-    """The rolling-window 64 -> 64 kernel (weights in registers, persistent strip walk, LDS
-    row ring; tile 18) == conv_halo_kernel (tile 17) bit for bit: same operands, K order and
-    accumulator seeding.  Covers partial blocks/strips, several strip segments, dil 1/2/4."""
-    g = torch.Generator().manual_seed(81 + h)
-    x = torch.randn(n, h, w, 64, generator=g).bfloat16().to(DEV)
-    wt = (torch.randn(64, 64, 3, 3, generator=g) * (2.0 / 576) ** 0.5).to(DEV)
-    sc = (torch.rand(64, generator=g) + 0.5).to(DEV)
-    sh = (torch.rand(64, generator=g) - 0.5).to(DEV)
-    res = torch.randn(n, h, w, 64, generator=g).bfloat16().to(DEV) if with_res else None
-    kw = dict(stride=1, padding=dil, dilation=dil, relu=relu, fold_scale=True)
-    a = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=17, **kw)
-    b = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=18, **kw)
-    auto = ops.conv2d_bn_act(x, wt, sc, sh, res, **kw)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b) and torch.equal(auto, b)
-
-
 def test_forced_tile_larger_than_weights_is_rejected():
     """A 256-channel tile over a 128-row packed weight must be refused, not read past it."""
     x = torch.randn(1, 16, 16, 128, device=DEV).bfloat16()

@@ -925,8 +925,7 @@ constexpr Variant kVariants[] = {
     {256, 64, "conv_pp_kernel<3>", "conv_pp_kernel<1>"},
 };
 constexpr int kPingPong = 12;
-constexpr int kHalo = 13;   // conv_halo.hip (tile id 17): conv_halo_kernel
-constexpr int kHaloRw = 14; // conv_halo.hip (tile id 18): rolling-window kernel (cin = cout = 64)
+constexpr int kHalo = 13;   // conv_halo.hip (tile id 17)
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 template <int KS, bool PERSIST>
@@ -1106,8 +1105,7 @@ bool big_conv_supported(const drnmi_conv_args& p) {
 
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   // the halo kernel (cin/cout 64-128) stays dense: it beats unit skipping on those shapes
-  if (variant == kHalo || variant == kHaloRw) return halo_conv_dispatch(p, s, variant == kHalo ? 0 : 1);
-  if (variant < 0 && halo_conv_supported(p)) return halo_conv_dispatch(p, s);
+  if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_dispatch(p, s);
   if (!big_conv_supported(p)) return DRNMI_ENOTSUP;
   if (variant < 0) variant = auto_variant(p);
   if (variant >= kNumVariants) return DRNMI_ENOTSUP;
@@ -1141,8 +1139,7 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 }
 
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
-  if (variant == kHalo || variant == kHaloRw) return halo_conv_name(p, variant == kHalo ? 0 : 1);
-  if (variant < 0 && halo_conv_supported(p)) return halo_conv_name(p);
+  if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_name(p);
   if (variant < 0) variant = auto_variant(p);
   if (variant >= kNumVariants) return nullptr;
   if (p.x2 != nullptr) {

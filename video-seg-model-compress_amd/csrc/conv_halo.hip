@@ -243,245 +243,6 @@ conv_halo_kernel(const drnmi_conv_args p) {
   }
 }
 
-// ---------------------------------------------------------------- rolling-window variant
-// cin = cout = 64, stride 1, dil <= 4: DRN-D layer3 BasicBlock convs (lmodels/drn.py:49-65;
-// the D-54 layer3 Bottleneck 3x3, :86-106).  conv_halo_kernel re-fetches the whole 64 x 576
-// weight matrix (74 KB) and a 6-row patch for every 4 x 64 block, and its one-block lifetime
-// leaves the patch load exposed.  Here the weights live in registers (a wave owns 32 output
-// channels: 9 taps x 2 K halves x 2 row fragments = 36 A fragments, 144 VGPRs), and one
-// persistent workgroup of 8 waves walks a column strip of 4 x 64 blocks downwards.  The input
-// rows sit in an LDS ring of 8 + 2 dil row slots; the 4 rows block t+1 adds are DMA'd while
-// block t computes, so each input row is fetched once per strip segment.  Same MFMA operands,
-// K order and accumulator seeding as conv_halo_kernel: the output is bit-identical.
-constexpr int kRwSlotPix = 72;                  // pixel rows per ring slot: 64 + 2 dil, padded to 8
-constexpr int kRwSlotBytes = kRwSlotPix * 128;  // 9 KB = 9 whole DMA pieces
-__host__ __device__ constexpr int rw_slots(int dil) { return 8 + 2 * dil; }
-
-__device__ uint2 g_rw_sink[64];                 // target of the epilogue stores of masked lanes
-// diagnostic ablations (scripts/build_variant_src.sh, never in the shipped build): bit 1 no
-// MFMAs, 2 no in-loop DMA, 4 no stores, 8 no fragment reads
-#ifndef DRNMI_RW_ABL
-#define DRNMI_RW_ABL 0
-#endif
-constexpr int kRwRows = 2;                      // output rows per wave (4 waves: 2 rows x 2 channel halves)
-constexpr int kRwStores = kRwRows * 2 * 4;      // epilogue stores per lane per block
-
-template <bool RES>
-__global__ void __launch_bounds__(256, 1)
-conv_halo_rw_kernel(const drnmi_conv_args p, int segs) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int ch = wave & 1;               // output channels ch*32 .. +32
-  const int wr0 = (wave >> 1) * 2;       // output rows wr0, wr0+1 of the block
-  const int fr = lane & 15;
-  const int fq = lane >> 4;
-  const int H = p.h, W = p.w, dil = p.dil, pad = p.pad;
-  const int NS = rw_slots(dil);
-  const int tiles_x = (p.wo + 63) / 64, tiles_y = (p.ho + 3) / 4;
-  const int strip = blockIdx.x / segs, seg = blockIdx.x - strip * segs;
-  const int n = strip / tiles_x;
-  const int ow0 = (strip - n * tiles_x) * 64;
-  const int t_begin = static_cast<int>(static_cast<int64_t>(seg) * tiles_y / segs);
-  const int t_end = static_cast<int>(static_cast<int64_t>(seg + 1) * tiles_y / segs);
-  if (t_begin >= t_end) return;          // whole workgroup
-  const uint16_t* __restrict__ x = reinterpret_cast<const uint16_t*>(p.x);
-  const uint16_t* __restrict__ wt = reinterpret_cast<const uint16_t*>(p.wgt);
-  const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
-  uint16_t* __restrict__ y = reinterpret_cast<uint16_t*>(p.y);
-
-  // input rows [r0, r0 + nr) of this strip -> ring slots (ir mod NS); 9 pieces per row,
-  // dealt over the waves.  Out-of-image pixels and the slot's padding come from the zero page.
-  const char* zero_src = reinterpret_cast<const char*>(g_halo_zero) + lane * 16;
-  const int lr = lane >> 3, ls = lane & 7;
-  const int pw = 64 + 2 * dil;
-  auto load_piece = [&](int r0, int pc) {
-    {
-      const int rr = pc / 9, j = pc - rr * 9;
-      const int ir = r0 + rr;
-      const int slot = (ir % NS + NS) % NS;
-      const int c = j * 8 + lr;
-      const int R = slot * kRwSlotPix + c;
-      const int iw = ow0 - pad + c;
-      const bool ok = c < pw && static_cast<unsigned>(ir) < static_cast<unsigned>(H) &&
-                      static_cast<unsigned>(iw) < static_cast<unsigned>(W);
-      const void* src = ok ? static_cast<const void*>(x + ((static_cast<int64_t>(n) * H + ir) * W + iw) * 64 +
-                                                      hswz<128>(R, ls) * 8)
-                           : static_cast<const void*>(zero_src);
-      glds16(src, smem + slot * kRwSlotBytes + j * 1024);
-    }
-  };
-  // prologue rows: a runtime count (the wait after them is vmcnt(0))
-  for (int pc = wave; pc < (4 + 2 * dil) * 9; pc += 4) load_piece(4 * t_begin - pad, pc);
-  // the 4 rows a block adds: exactly 9 pieces per wave, unrolled, so the compiler can count
-  // them when it places its own waits for the residual registers (a runtime trip count makes
-  // it fall back to vmcnt(0), which would expose the DMA and store latency every block)
-  auto load_rows4 = [&](int r0) {
-#pragma unroll
-    for (int i = 0; i < 9; ++i) load_piece(r0, wave + 4 * i);
-  };
-
-  // the weights, once: A fragment (tap, K half, row fragment) of packed column tap*64 + half*32
-  bf16x8 af[9][2][2];
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int fm = 0; fm < 2; ++fm) {
-        const int r = ch * 32 + fm * 16 + fr;
-        af[tap][sub][fm] = *reinterpret_cast<const bf16x8*>(wt + static_cast<int64_t>(r) * p.k_pad + tap * 64 +
-                                                            sub * 32 + fq * 8);
-      }
-
-  // residual of block t (lane: channels co..co+3 of pixel (oh, ow0 + fn*16 + fr))
-  uint2 rv[kRwRows][2][4];
-  auto load_res = [&](int t) {
-#pragma unroll
-    for (int rw = 0; rw < kRwRows; ++rw) {
-      const int oh = min(4 * t + wr0 + rw, p.ho - 1);
-#pragma unroll
-      for (int fn = 0; fn < 4; ++fn) {
-        const int ow = min(ow0 + fn * 16 + fr, p.wo - 1);
-        const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow;
-#pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
-          rv[rw][fm][fn] = *reinterpret_cast<const uint2*>(res + m * p.cout + ch * 32 + fm * 16 + fq * 4);
-      }
-    }
-  };
-  if (RES) load_res(t_begin);
-  float4 sh[2];
-#pragma unroll
-  for (int fm = 0; fm < 2; ++fm) sh[fm] = *reinterpret_cast<const float4*>(p.shift + ch * 32 + fm * 16 + fq * 4);
-  // fragment byte offset within a slot for (kw, K half): pixel kw*dil + fr (+ fn*16), swizzled
-  // chunk; slot bases are multiples of 72 pixel rows, so the swizzle depends on kw*dil + fr only
-  int lane_off[3][2];
-#pragma unroll
-  for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      const int r = kw * dil + fr;
-      lane_off[kw][sub] = r * 128 + hswz<128>(r, sub * 4 + fq) * 16;
-    }
-
-  // accumulator seeding: shift (+ residual) of block t; for t > t_begin it runs at the end of
-  // block t-1, after its results are packed and before its stores, so the compiler's wait for
-  // the residual registers (loaded a whole block earlier) covers neither fresh DMA nor stores
-  f32x4 acc[kRwRows][2][4];
-  auto seed = [&]() {
-#pragma unroll
-    for (int rw = 0; rw < kRwRows; ++rw)
-#pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < 4; ++fn) {
-          acc[rw][fm][fn] = f32x4{sh[fm].x, sh[fm].y, sh[fm].z, sh[fm].w};
-          if (RES) {
-            acc[rw][fm][fn][0] += bf16_to_f32(static_cast<uint16_t>(rv[rw][fm][fn].x & 0xffff));
-            acc[rw][fm][fn][1] += bf16_to_f32(static_cast<uint16_t>(rv[rw][fm][fn].x >> 16));
-            acc[rw][fm][fn][2] += bf16_to_f32(static_cast<uint16_t>(rv[rw][fm][fn].y & 0xffff));
-            acc[rw][fm][fn][3] += bf16_to_f32(static_cast<uint16_t>(rv[rw][fm][fn].y >> 16));
-          }
-        }
-  };
-  seed();
-  // everything the prologue issued has landed (a builtin wait, so the compiler's own wait
-  // placement knows the weight registers are ready inside the loop)
-  __builtin_amdgcn_s_waitcnt(0);
-
-  for (int t = t_begin; t < t_end; ++t) {
-    // block t's rows (and residual) went out a whole block ago, before block t-1's stores:
-    // vmcnt(kRwStores) (encoding: vmcnt[3:0] | expcnt 7 << 4 | lgkmcnt 0 << 8 | vmcnt[5:4] << 14)
-    static_assert(kRwStores == 16, "wait encoding below is vmcnt(16)");
-    if (t > t_begin) __builtin_amdgcn_s_waitcnt(0x4070);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (RES && t + 1 < t_end) load_res(t + 1);
-    // every wave is past block t-1: the slots of its first 4 rows take block t+1's new rows
-    if ((DRNMI_RW_ABL & 2) == 0 && t + 1 < t_end) load_rows4(4 * (t + 1) - pad + 2 * dil);
-    __builtin_amdgcn_sched_barrier(0);
-
-    // slot byte base of the input row under (row rw, tap row kh): wave-uniform
-    int slot_base[kRwRows][3];
-#pragma unroll
-    for (int rw = 0; rw < kRwRows; ++rw)
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const int ir = 4 * t + wr0 + rw - pad + kh * dil;
-        slot_base[rw][kh] = ((ir % NS + NS) % NS) * kRwSlotBytes;
-      }
-    auto load_b = [&](bf16x8 (&dst)[kRwRows][4], int st) {
-      const int tap = st >> 1, sub = st & 1;
-      const int kh = tap / 3, kw = tap - kh * 3;
-#pragma unroll
-      for (int rw = 0; rw < kRwRows; ++rw) {
-        const char* b = smem + slot_base[rw][kh] + lane_off[kw][sub];
-#pragma unroll
-        for (int fn = 0; fn < 4; ++fn) dst[rw][fn] = *reinterpret_cast<const bf16x8*>(b + fn * 2048);
-      }
-    };
-    // 18 K steps (tap, K half); the fragments of step s+1 are read during step s's MFMAs
-    bf16x8 bfr[2][kRwRows][4];
-    load_b(bfr[0], 0);
-#pragma unroll
-    for (int st = 0; st < 18; ++st) {
-      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): step st's fragments have landed
-      if ((DRNMI_RW_ABL & 8) == 0 && st + 1 < 18) load_b(bfr[(st + 1) & 1], st + 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int rw = 0; rw < kRwRows; ++rw)
-#pragma unroll
-        for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < 4; ++fn) {
-            if constexpr ((DRNMI_RW_ABL & 1) != 0)
-              asm volatile("" :: "v"(af[st >> 1][st & 1][fm]), "v"(bfr[st & 1][rw][fn]));
-            else
-              acc[rw][fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[st >> 1][st & 1][fm], bfr[st & 1][rw][fn],
-                                                                        acc[rw][fm][fn], 0, 0, 0);
-          }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-
-    // epilogue: pack, seed the next block, then always kRwStores stores per lane (masked lanes
-    // write the sink) so the wait count at the top holds
-    uint2 o[kRwRows][2][4];
-#pragma unroll
-    for (int rw = 0; rw < kRwRows; ++rw)
-#pragma unroll
-      for (int fm = 0; fm < 2; ++fm)
-#pragma unroll
-        for (int fn = 0; fn < 4; ++fn) {
-          float v[4] = {acc[rw][fm][fn][0], acc[rw][fm][fn][1], acc[rw][fm][fn][2], acc[rw][fm][fn][3]};
-          if (p.relu) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-          }
-          o[rw][fm][fn].x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
-          o[rw][fm][fn].y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
-        }
-    if (t + 1 < t_end) seed();
-#pragma unroll
-    for (int rw = 0; rw < kRwRows; ++rw) {
-      const int oh = 4 * t + wr0 + rw;
-#pragma unroll
-      for (int fn = 0; fn < 4; ++fn) {
-        const int ow = ow0 + fn * 16 + fr;
-        const bool ok = oh < p.ho && ow < p.wo;
-        const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow;
-#pragma unroll
-        for (int fm = 0; fm < 2; ++fm) {
-          uint2* dst = ok ? reinterpret_cast<uint2*>(y + m * p.cout + ch * 32 + fm * 16 + fq * 4) : g_rw_sink + lane;
-          if constexpr ((DRNMI_RW_ABL & 4) != 0) asm volatile("" :: "v"(o[rw][fm][fn].x), "v"(dst));
-          else *dst = o[rw][fm][fn];
-        }
-      }
-    }
-  }
-}
-
 // output-block width.  32 columns for the 64 -> 64 conv (three workgroups per CU instead of two)
 // measured the same as 64 (128.0 vs 128.3 us, D-22 layer3, 8 frames)
 #ifndef DRNMI_HALO_TC_64_64
@@ -505,56 +266,6 @@ hipError_t launch_halo(const drnmi_conv_args& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-int cu_count() {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      ncu = v;
-    else
-      ncu = 256;
-  }
-  return ncu;
-}
-
-// DRNMI_HALO_RW=0 keeps the 64 -> 64 convs on conv_halo_kernel (A/B runs)
-bool rw_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("DRNMI_HALO_RW");
-    on = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  return on == 1;
-}
-
-bool halo_rw_supported(const drnmi_conv_args& p) {
-  return p.cin == 64 && p.cout == 64 && p.dil <= 4 && p.scale == nullptr && rw_enabled();
-}
-
-hipError_t launch_halo_rw(const drnmi_conv_args& p, hipStream_t s) {
-  const int lds = rw_slots(p.dil) * kRwSlotBytes;
-  static int attr_lds = 0;
-  if (attr_lds < lds) {
-    for (const void* f : {reinterpret_cast<const void*>(&conv_halo_rw_kernel<true>),
-                          reinterpret_cast<const void*>(&conv_halo_rw_kernel<false>)}) {
-      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (e != hipSuccess) return e;
-    }
-    attr_lds = lds;
-  }
-  const int tiles_x = (p.wo + 63) / 64, tiles_y = (p.ho + 3) / 4;
-  const int64_t strips = static_cast<int64_t>(p.n) * tiles_x;
-  // one workgroup per CU: split each strip into segments until the CUs are covered
-  const int64_t want = (cu_count() + strips - 1) / strips;
-  const int segs = static_cast<int>(want < 1 ? 1 : (want > tiles_y ? tiles_y : want));
-  if (p.res != nullptr)
-    hipLaunchKernelGGL(conv_halo_rw_kernel<true>, dim3(static_cast<unsigned>(strips * segs)), dim3(256), lds, s, p, segs);
-  else
-    hipLaunchKernelGGL(conv_halo_rw_kernel<false>, dim3(static_cast<unsigned>(strips * segs)), dim3(256), lds, s, p, segs);
-  return hipGetLastError();
-}
-
 }  // namespace
 
 bool halo_conv_supported(const drnmi_conv_args& p) {
@@ -570,21 +281,17 @@ bool halo_conv_supported(const drnmi_conv_args& p) {
   return kNST * 64 * wc * 128 + patch_bytes(p.cin, p.dil, halo_tc(p.cin, p.cout)) <= 160 * 1024;
 }
 
-int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s, int form) {
+int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!halo_conv_supported(p)) return DRNMI_ENOTSUP;
-  if (form == 1 && !halo_rw_supported(p)) return DRNMI_ENOTSUP;
   hipError_t e;
-  if (form != 0 && halo_rw_supported(p)) e = launch_halo_rw(p, s);
-  else if (p.cin == 64) e = p.cout == 64 ? launch_halo<64, 1>(p, s) : launch_halo<64, 2>(p, s);
+  if (p.cin == 64) e = p.cout == 64 ? launch_halo<64, 1>(p, s) : launch_halo<64, 2>(p, s);
   else e = p.cout == 64 ? launch_halo<128, 1>(p, s) : launch_halo<128, 2>(p, s);
   return static_cast<int>(e);
 }
 
 #define DRNMI_STR2(x) #x
 #define DRNMI_STR(x) DRNMI_STR2(x)
-const char* halo_conv_name(const drnmi_conv_args& p, int form) {
-  if (form == 1 && !halo_rw_supported(p)) return nullptr;
-  if (form != 0 && halo_rw_supported(p)) return "conv_halo_rw_kernel";
+const char* halo_conv_name(const drnmi_conv_args& p) {
   if (p.cin == 64)
     return p.cout == 64 ? "conv_halo_kernel<64, 1, " DRNMI_STR(DRNMI_HALO_TC_64_64) ">" : "conv_halo_kernel<64, 2, 64>";
   return p.cout == 64 ? "conv_halo_kernel<128, 1, 64>" : "conv_halo_kernel<128, 2, 64>";

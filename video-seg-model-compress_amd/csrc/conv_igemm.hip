@@ -262,7 +262,6 @@ constexpr TileDesc kTiles[] = {
     {256, 256, "dma256k32p"}, {128, 128, "dma128k32p"},   // p = persistent
     {256, 256, "pp256"},                                   // ping-pong 4-phase schedule
     {128, 128, "halo"},                                    // conv_halo.hip, 4x64 pixel block
-    {64, 64, "halo_rw"},                                   // conv_halo.hip, rolling window (64 -> 64)
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 

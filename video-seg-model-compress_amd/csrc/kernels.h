@@ -20,9 +20,8 @@ int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
 const char* i8_conv_name(const drnmi_conv_args& p);
 // Halo-patch 3x3 stride-1 conv, cin/cout 64 or 128 (conv_halo.hip).
 bool halo_conv_supported(const drnmi_conv_args& p);
-// form: -1 auto (the rolling-window kernel where it applies), 0 conv_halo_kernel, 1 rolling window
-int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s, int form = -1);
-const char* halo_conv_name(const drnmi_conv_args& p, int form = -1);
+int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
+const char* halo_conv_name(const drnmi_conv_args& p);
 // fp32-accurate 6-product split-bf16 implicit GEMM (conv_x6.hip): dtype DRNMI_F32X3, cin >= 32.
 bool x6_conv_supported(const drnmi_conv_args& p);
 int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
