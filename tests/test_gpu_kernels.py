@@ -317,6 +317,39 @@ def test_null_scale_seeds_accumulator(shape):
     assert ran >= 2
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout,dil,with_res,fold", [
+    (2, 9, 256, 256, 256, 2, True, True), (1, 5, 512, 512, 512, 4, True, True),
+    (2, 6, 256, 128, 256, 2, False, True), (1, 4, 256, 512, 512, 1, False, False),
+    (3, 3, 256, 64, 256, 4, True, True), (1, 2, 768, 256, 512, 1, True, True)])
+def test_strip_kernel_bit_identical(n, h, w, cin, cout, dil, with_res, fold):
+    """Strip-staged B (tile 18, conv_strip_kernel: one DMA of 256 + 2 dil input pixels per
+    (channel block, tap row), read by the three kw taps at row offset kw*dil) == the per-tap
+    gather of the same 256 x 256 tile (tile 5) bit for bit, and auto-routing takes it for
+    wo % 256 == 0.  Image borders (top/bottom rows, left/right strip ends) are in every case."""
+    g = torch.Generator().manual_seed(90 + h * w + cin)
+    x = torch.randn(n, h, w, cin, generator=g).bfloat16().to(DEV)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (9 * cout)) ** 0.5).to(DEV)
+    sc = (torch.rand(cout, generator=g) + 0.5).to(DEV)
+    sh = (torch.rand(cout, generator=g) - 0.5).to(DEV)
+    res = torch.randn(n, h, w, cout, generator=g).bfloat16().to(DEV) if with_res else None
+    kw = dict(stride=1, padding=dil, dilation=dil, relu=True, fold_scale=fold)
+    a = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=5, **kw)
+    b = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=18, **kw)
+    auto = ops.conv2d_bn_act(x, wt, sc, sh, res, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(auto, b)
+    ref = _ref_conv(x.float().permute(0, 3, 1, 2).cpu(), wt.bfloat16().float().cpu(), sc.cpu(), sh.cpu(),
+                    res.float().permute(0, 3, 1, 2).cpu() if with_res else None, 1, dil, dil, True)
+    assert (b.float().permute(0, 3, 1, 2).cpu() - ref).abs().max().item() <= 1.5e-2 * ref.abs().max().item()
+
+
+def test_strip_kernel_refuses_unaligned_rows():
+    x = torch.randn(1, 4, 200, 256, device=DEV).bfloat16()
+    wt = torch.randn(256, 256, 3, 3, device=DEV) * 0.02
+    with pytest.raises(RuntimeError, match="ENOTSUP"):
+        ops.conv2d_bn_act(x, wt, padding=2, dilation=2, tile=18)
+
+
 def test_forced_tile_larger_than_weights_is_rejected():
     """A 256-channel tile over a 128-row packed weight must be refused, not read past it."""
     x = torch.randn(1, 16, 16, 128, device=DEV).bfloat16()

@@ -371,11 +371,25 @@ struct BigCfg {
   static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-template <typename T, int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE, bool X2 = false>
+// STRIP (3x3 stride-1 convs whose tiles are whole 256-pixel runs of one output row, wo % 256
+// == 0: DRN-D layer5..8 at 1024x2048): the B operand of the three taps (kh, kw = 0..2) of one
+// 64-channel block is the same input row shifted by kw*dil pixels, so it is DMA'd once per
+// (channel block, kh) as a strip of 256 + 2 dil pixel rows into one of two strip buffers and the
+// three K steps read it at row offset kw*dil.  B DMA drops from 3 x 256 to 256 + 2 dil rows per
+// three steps (~8 to ~5.4 DMA pieces per wave per step, 64 to ~43 KB of LDS writes).  The next
+// (cb, kh) strip is issued in shares during the current group's three steps.  The K order, the
+// MFMAs and the epilogue are unchanged: the output is bit-identical to the non-strip kernel.
+constexpr int kStripPieces = 33;                     // ceil((256 + 2 * 4) / 8) 1-KB pieces, dil <= 4
+constexpr int kStripBytes = kStripPieces * 1024;
+
+template <typename T, int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool SPARSE, bool X2 = false,
+          bool STRIP = false>
 __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   using K = KT<T>;
   using C = BigCfg<WCO, WC, NST, BK, NWP, K::ESZ>;
   static_assert(!SPARSE || K::ESZ == 2, "unit skipping: bf16 only");
+  static_assert(!STRIP || (KS == 3 && NST == 2 && BK == 64 && K::ESZ == 2 && !PERSIST && !SPARSE && !X2 &&
+                           C::NW == 8), "strip mode: the 256 x 256 bf16 3x3 instantiation only");
   constexpr int CE = 16 / K::ESZ;   // elements per 16-B chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -419,8 +433,15 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   int b_off[C::B_INSTR];
   int b2_off[X2 ? C::B_INSTR : 1];   // x2 element offset of the row's chunk (x2 steps)
   const char* zero_src = reinterpret_cast<const char*>(g_zero_page) + lane * 16;
+  int s_n = 0, s_oh = 0, s_ow0 = 0;   // STRIP: the tile's image, output row and first column
 
   auto setup = [&](int px0, int co0) {
+    if constexpr (STRIP) {
+      s_n = px0 / hw_o;
+      const int q = px0 - s_n * hw_o;
+      s_oh = q / p.wo;
+      s_ow0 = q - s_oh * p.wo;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r = (wave * C::A_INSTR + i) * C::RPI + lrow;
@@ -472,6 +493,11 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   };
   // one DMA instruction ("piece") of a step: pieces [0, A_INSTR) weights, then pixel rows
   auto issue_piece = [&](const StepP& sp, int stage, int i) {
+    if constexpr (STRIP) {                         // A only: B comes as strips
+      if (i < C::A_INSTR)
+        glds16(wt + (a_par[i & 1] + i * C::RPI * p.k_pad + sp.k0), smem + stage * C::A_BYTES + (wave * C::A_INSTR + i) * 1024);
+      return;
+    }
     char* sa = smem + stage * C::STAGE;
     if (i < C::A_INSTR) {
       glds16(wt + (a_par[i & 1] + i * C::RPI * p.k_pad + sp.k0), sa + (wave * C::A_INSTR + i) * 1024);
@@ -492,6 +518,25 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
     const StepP sp = step_params(kt);
 #pragma unroll
     for (int i = 0; i < C::GLDS; ++i) issue_piece(sp, stage, i);
+  };
+  // STRIP: share sh (0..4) of the strip of group g = K steps 3g..3g+2 (channel block g / 3, tap
+  // row kh = g % 3): strip row R = input pixel (oh - pad + kh dil, ow0 - pad + R), 16-B chunk c
+  // at slot c ^ (R & 7) (conflict-free for the 16 consecutive rows of a fragment read at any
+  // kw*dil offset)
+  const int ngroups = nk / 3;
+  auto issue_strip = [&](int g, int sh) {
+    const int j = wave + 8 * sh;
+    if (j >= kStripPieces) return;                 // wave-uniform
+    const int R = j * 8 + lrow;
+    const int cb = g / 3, kh = g - cb * 3;
+    const int ih = s_oh - p.pad + kh * dil;
+    const int iw = s_ow0 - p.pad + R;
+    const bool ok = R < kBPX + 2 * dil && static_cast<unsigned>(ih) < static_cast<unsigned>(H) &&
+                    static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+    const void* src = ok ? static_cast<const void*>(x + ((static_cast<int64_t>(s_n) * H + ih) * W + iw) * cin + cb * BK +
+                                                    (lslot ^ (R & 7)) * CE)
+                         : static_cast<const void*>(zero_src);
+    glds16(src, smem + NST * C::A_BYTES + (g & 1) * kStripBytes + j * 1024);
   };
 
 
@@ -534,6 +579,10 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   if constexpr (K::ESZ == 2) init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);   // residual loads ahead of the DMA
   else zero_tile(acc);
   for (int t = 0; t < NST - 1 && t < nlive; ++t) issue(kt_at(t), t);
+  if constexpr (STRIP) {
+#pragma unroll
+    for (int sh = 0; sh < 5; ++sh) issue_strip(0, sh);
+  }
 
   while (true) {
     // t runs over the (live) K-step positions; kt_at(t) is the K step itself
@@ -547,10 +596,15 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 
-      const char* sa = smem + cur * C::STAGE;
-      const char* sb = sa + C::A_BYTES;
+      const char* sa = smem + cur * (STRIP ? C::A_BYTES : C::STAGE);
+      const char* sb = STRIP ? smem + NST * C::A_BYTES + ((t / 3) & 1) * kStripBytes : sa + C::A_BYTES;
+      const int kwd = STRIP ? (t % 3) * dil : 0;   // STRIP: strip row offset of this step's tap
+      // STRIP: this step also issues shares 2 (t % 3), +1 of the next group's strip (clamped: the
+      // last group re-fetches its own strip, identical bytes, into the buffer being read)
+      const int sg = (t / 3 + 1 < ngroups) ? t / 3 + 1 : ngroups - 1;
+      constexpr int GL = STRIP ? C::A_INSTR + 2 : C::GLDS;
       constexpr int NG = C::SUB * C::GR;
-      constexpr int PPG = (C::GLDS + C::GR - 1) / C::GR;   // DMA pieces per group (first substep)
+      constexpr int PPG = (GL + C::GR - 1) / C::GR;   // DMA pieces per group (first substep)
       const bool nxt = (DRNMI_ABLATE & 1) ? false : (DRNMI_PIN ? true : t + NST - 1 < nlive);
       const StepP sp = step_params(kt_at(t + NST - 1 < nlive ? t + NST - 1 : nlive - 1));
       const int nst = (t + NST - 1) % NST;
@@ -571,7 +625,12 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
 #pragma unroll
         for (int fn = 0; fn < C::FN; ++fn) {
           const int r = wp * C::PXW + fn * 16 + fr;
-          dst[fn] = *reinterpret_cast<const typename K::frag*>(sb + r * C::ROWB + swzb<C::ROWB>(r, c) * 16);
+          if constexpr (STRIP) {
+            const int R = r + kwd;
+            dst[fn] = *reinterpret_cast<const typename K::frag*>(sb + R * C::ROWB + (c ^ (R & 7)) * 16);
+          } else {
+            dst[fn] = *reinterpret_cast<const typename K::frag*>(sb + r * C::ROWB + swzb<C::ROWB>(r, c) * 16);
+          }
         }
       };
       load_b(bfr[0], 0);
@@ -613,7 +672,13 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         if (q < C::GR && nxt) {
 #pragma unroll
           for (int k = 0; k < PPG; ++k)
-            if (q * PPG + k < C::GLDS) issue_piece(sp, nst, q * PPG + k);
+            if constexpr (STRIP) {
+              const int i = q * PPG + k;
+              if (i < C::A_INSTR) issue_piece(sp, nst, i);
+              else if (i < GL) issue_strip(sg, 2 * (t % 3) + (i - C::A_INSTR));
+            } else {
+              if (q * PPG + k < C::GLDS) issue_piece(sp, nst, q * PPG + k);
+            }
         }
         if constexpr (DRNMI_PIN) __builtin_amdgcn_sched_barrier(0);
       }
@@ -649,6 +714,12 @@ template <int KS, int WCO, int WC, int NST, int BK, bool PERSIST, int NWP, bool 
 __global__ void __launch_bounds__(64 * NWP * WC, 1)
 conv_big_kernel(const drnmi_conv_args p) {
   conv_big_body<uint16_t, KS, WCO, WC, NST, BK, PERSIST, NWP, SPARSE, X2>(p);
+}
+
+// Strip-staged B operand (see conv_big_body STRIP): the 256 x 256 3x3 tile for wo % 256 == 0.
+__global__ void __launch_bounds__(512, 1)
+conv_strip_kernel(const drnmi_conv_args p) {
+  conv_big_body<uint16_t, 3, 128, 2, 2, 64, false, 4, false, false, true>(p);
 }
 
 // W8A8 (config C5): the same LDS-DMA pipeline over int8 elements, BK int8 channels per K step
@@ -902,6 +973,38 @@ hipError_t launch_big(const drnmi_conv_args& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+constexpr int kStripLds = 2 * 256 * 128 + 2 * kStripBytes;   // 2 A stages + 2 strips (130 KB)
+
+hipError_t launch_strip(const drnmi_conv_args& p, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_strip_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kStripLds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const int64_t blocks = (M / kBPX) * ((p.cout + 255) / 256);
+  hipLaunchKernelGGL(conv_strip_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), kStripLds, s, p);
+  return hipGetLastError();
+}
+
+// DRNMI_STRIP=0 keeps every launch on the per-tap B gather (A/B runs)
+bool strip_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("DRNMI_STRIP");
+    on = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
+
+// a 256-pixel tile is a run of one output row, the strip of 256 + 2 dil rows fits its buffer
+bool strip_ok(const drnmi_conv_args& p) {
+  return p.ks == 3 && p.stride == 1 && p.pad == p.dil && p.dil >= 1 && p.dil <= 4 && p.wo % kBPX == 0 &&
+         p.x2 == nullptr && p.unit_mask == nullptr && p.cin % 64 == 0 && p.k == 9 * p.cin;
+}
+
 struct Variant {
   int bco, bk;
   const char* name3;
@@ -926,6 +1029,7 @@ constexpr Variant kVariants[] = {
 };
 constexpr int kPingPong = 12;
 constexpr int kHalo = 13;   // conv_halo.hip (tile id 17)
+constexpr int kStrip = 14;  // conv_strip_kernel (tile id 18); auto routes variant 1 there when strip_ok
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 template <int KS, bool PERSIST>
@@ -1107,7 +1211,14 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   // the halo kernel (cin/cout 64-128) stays dense: it beats unit skipping on those shapes
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_dispatch(p, s);
   if (!big_conv_supported(p)) return DRNMI_ENOTSUP;
+  const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
+  if (variant == kStrip || (auto_pick && variant == 1 && strip_enabled() && strip_ok(p))) {
+    if (!strip_ok(p) || p.cin < 64) return DRNMI_ENOTSUP;
+    if ((p.cout + 255) / 256 * 256 > p.cout_pad) return DRNMI_EINVAL;
+    const hipError_t e = launch_strip(p, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
   if (variant >= kNumVariants) return DRNMI_ENOTSUP;
   const Variant& v = kVariants[variant];
   if (p.cin < v.bk) return DRNMI_ENOTSUP;                            // a K step must fit in one tap
@@ -1140,7 +1251,10 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_name(p);
+  const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
+  if (variant == kStrip || (auto_pick && variant == 1 && strip_enabled() && strip_ok(p)))
+    return strip_ok(p) && p.cin >= 64 ? "conv_strip_kernel" : nullptr;
   if (variant >= kNumVariants) return nullptr;
   if (p.x2 != nullptr) {
     if (variant != 0 && variant != 1) return nullptr;
