@@ -52,8 +52,9 @@ def test_argument_validation_without_gpu():
 
 def test_fused_second_input_never_routes_to_halo():
     """A conv with a fused second input (x2, the folded 1x1 downsample) must go to a kernel
-    that reads x2: the halo kernel takes the same 64/128-channel shapes but has no second K
-    segment, so routing it there would silently drop the downsample term."""
+    that reads x2: the halo kernel takes it only in its fused-downsample form (scale folded,
+    no residual, cin2 32/64, rows padded to 64-column steps); anything else must not route
+    there, or the downsample term would be dropped silently."""
     lib = _lib.load()
     a = _lib.ConvArgs()
     a.n, a.h, a.w, a.cin, a.ho, a.wo, a.cout, a.cout_pad = 1, 16, 16, 64, 16, 16, 64, 128
@@ -64,5 +65,14 @@ def test_fused_second_input_never_routes_to_halo():
     assert lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode().startswith("conv_halo")
     a.x2, a.cin2, a.h2, a.w2, a.stride2 = 1, 64, 32, 32, 2
     a.k = a.k_pad = 9 * 64 + 64
+    # scale = NULL (folded) and no residual: the halo kernel's fused-downsample form takes it
+    assert lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode().startswith("conv_halo_kernel")
+    a.cin2, a.k, a.k_pad = 32, 9 * 64 + 32, 9 * 64 + 32   # k_pad must be k rounded up to 64
+    assert lib.drnmi_conv_kernel_name(ctypes.byref(a)) is None or \
+        not lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode().startswith("conv_halo")
+    a.k_pad = 9 * 64 + 64
+    assert lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode().startswith("conv_halo_kernel")
+    sc = (ctypes.c_float * 64)()
+    a.scale = ctypes.cast(sc, ctypes.c_void_p).value      # an unfolded scale: not the halo x2 form
     name = lib.drnmi_conv_kernel_name(ctypes.byref(a))
     assert name is None or not name.decode().startswith("conv_halo")

@@ -441,10 +441,16 @@ def test_conv_x6_fp32_accuracy(case):
     (2, 16, 24, 256, 256, 3, 2, 128, 1, 16, 24),     # layer5.0: conv2 + 1x1 downsample 128 -> 256
     (1, 12, 20, 512, 512, 3, 4, 256, 1, 12, 20),     # layer6.0: dilation 4, 256 -> 512
     (1, 9, 13, 256, 1024, 1, 1, 512, 2, 18, 26),     # Bottleneck conv3 + stride-2 downsample
+    (2, 33, 70, 64, 64, 3, 1, 32, 2, 66, 140),       # layer3.0: halo conv2 + 1x1 s2 downsample 32 -> 64
+    (1, 20, 40, 128, 128, 3, 1, 64, 2, 40, 80),      # layer4.0: halo conv2 + 1x1 s2 downsample 64 -> 128
+    (3, 7, 130, 64, 64, 3, 1, 32, 2, 13, 259),       # ragged blocks, odd x2 extent
 ])
 def test_conv_fused_downsample(case):
     """drnmi_conv_args.x2: y = relu(conv(x, w) + conv1x1_s(x2, w2) + shift) as one launch (the
-    downsample folded into the block's last conv) vs torch fp32 on the same bf16 operands."""
+    downsample folded into the block's last conv) vs torch fp32 on the same bf16 operands.
+    conv_big takes cin2 % 64 == 0 (k_pad = k); the halo kernel (64/128-channel 3x3) takes cin2
+    32/64 with weight rows zero-padded to 64-column steps, and on a shape both take the two are
+    bit-identical (same K order and accumulator start)."""
     n, h, w, cin, cout, ks, dil, cin2, s2, h2, w2 = case
     g = torch.Generator().manual_seed(cin + cin2)
     x = (torch.randn(n, h, w, cin, generator=g)).to(torch.bfloat16)
@@ -457,9 +463,11 @@ def test_conv_fused_downsample(case):
         + F.conv2d(x2.float().permute(0, 3, 1, 2), wd.float(), stride=s2) + sh.view(1, -1, 1, 1)
     ref = torch.relu(ref).permute(0, 2, 3, 1)
     k1 = ks * ks * cin
-    wpk = torch.zeros(cout, k1 + cin2, dtype=torch.bfloat16)
+    halo = cin in (64, 128) and cout in (64, 128) and ks == 3
+    kp = (k1 + cin2 + 63) // 64 * 64 if halo else k1 + cin2
+    wpk = torch.zeros(cout, kp, dtype=torch.bfloat16)
     wpk[:, :k1] = wt.permute(0, 2, 3, 1).reshape(cout, k1)
-    wpk[:, k1:] = wd.reshape(cout, cin2)
+    wpk[:, k1:k1 + cin2] = wd.reshape(cout, cin2)
     ho, wo = h, w
     y = torch.empty(n, ho, wo, cout, dtype=torch.bfloat16, device=DEV)
     xd, x2d, wpd, shd = x.to(DEV), x2.to(DEV), wpk.to(DEV), sh.to(DEV)
@@ -468,16 +476,23 @@ def test_conv_fused_downsample(case):
     a.y_sn, a.y_sp, a.y_sc = ho * wo * cout, cout, 1
     a.n, a.h, a.w, a.cin, a.ho, a.wo, a.cout, a.cout_pad = n, h, w, cin, ho, wo, cout, cout
     a.ks, a.stride, a.pad, a.dil = ks, 1, pad, dil
-    a.k = a.k_pad = k1 + cin2
+    a.k, a.k_pad = k1 + cin2, kp
     a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_BF16, _lib.DRNMI_BF16, -1, _lib.ALGO_IGEMM
     a.x2, a.cin2, a.h2, a.w2, a.stride2 = x2d.data_ptr(), cin2, h2, w2, s2
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
-    assert name.startswith("conv_big_kernel"), name
+    assert name.startswith("conv_halo_kernel" if halo else "conv_big_kernel"), name
     _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds")
     torch.cuda.synchronize()
     err = (y.float().cpu() - ref).abs().max().item()
     print(f"{name} {case}: max-abs {err:.3e} (|y| {ref.abs().max().item():.2f})")
     assert err <= 0.02 * max(1.0, ref.abs().max().item())
+    if halo and kp == k1 + cin2:          # conv_big takes it too (tile 4: the 128 x 256 X2 form)
+        yb = torch.empty_like(y)
+        a.y, a.tile = yb.data_ptr(), 4
+        _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds big")
+        torch.cuda.synchronize()
+        assert torch.equal(yb, y)
+        a.y = y.data_ptr()
     # no kernel without x2 support may take it silently
     a.tile = 0
     assert _lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())) < 0
@@ -492,7 +507,7 @@ def test_bf16_fused_downsample_network_matches_unfused(golden_forward):
     m = build("drn_d_22", 19, seed=int(golden_forward[case + "/meta"][0]), device=DEV, precision="bf16")
     frames = torch.from_numpy(golden_forward[case + "/frames"]).to(DEV)
     pk_plan = m.plan(2, 128, 256)
-    assert len(pk_plan.skip) == 2
+    assert len(pk_plan.skip) == 4          # layer3.0 / layer4.0 (halo) and layer5.0 / layer6.0 (conv_big)
     fused = m.segment(frames).long()
     engine.FUSE_DOWNSAMPLE = False
     try:

@@ -15,6 +15,12 @@
 //   * K step = (64-channel block, tap), taps innermost; A = weights [cout][64] per step.
 //   * MFMA v_mfma_f32_16x16x32_bf16, A = weights (rows = channels), B = pixels: wave
 //     (wc, wp) owns channels wc*64..+64 of output row wp (64 pixels), 4 x 4 fragments.
+//   * Fused second input (x2 != NULL: the block's 1x1 stride-s downsample folded into its last
+//     conv, lmodels/drn.py:181-186, as in conv_big): cin2 (32 or 64) more K columns
+//     [W | W_ds | 0-pad to 64] streamed through the same weight ring as one or two extra 32-wide
+//     K halves after the taps; their B fragments (x2 at (oh*s2, ow*s2), 16 B per lane) are
+//     plain global loads issued before the patch DMA, so the residual branch is never written
+//     to HBM or read back.  k = 9 cin + cin2, k_pad = round_up(k, 64).
 #include "common.h"
 #include "kernels.h"
 
@@ -89,7 +95,10 @@ conv_halo_kernel(const drnmi_conv_args p) {
   const uint16_t* __restrict__ x = reinterpret_cast<const uint16_t*>(p.x);
   const uint16_t* __restrict__ wt = reinterpret_cast<const uint16_t*>(p.wgt);
   constexpr int NCB = CIN / 64;
-  const int nk = 9 * NCB;
+  const int nk = 9 * NCB;                       // tap steps
+  const bool fused = p.x2 != nullptr;
+  const int nx = fused ? (p.cin2 + 63) / 64 : 0; // x2 steps (64 K columns each)
+  const int nk_all = nk + nx;
 
   // --- accumulator start: 0, or shift + residual when the BN scale is folded into the
   // weights (scale == NULL); those loads go out ahead of the DMA and hide under it
@@ -106,6 +115,23 @@ conv_halo_kernel(const drnmi_conv_args p) {
     }
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = a0;
+  }
+  // x2 fragments (fused downsample): sub-step j of x2 step e is channel block (2e + j) * 32
+  bf16x8 x2f[2][FN];
+  if (fused) {
+    const uint16_t* __restrict__ x2 = reinterpret_cast<const uint16_t*>(p.x2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const int ow = ow0 + fn * 16 + fr;
+        x2f[j][fn] = bf16x8{};
+        if (j * 32 < p.cin2 && oh < p.ho && ow < p.wo) {
+          const int64_t q = (static_cast<int64_t>(n) * p.h2 + static_cast<int64_t>(oh) * p.stride2) * p.w2 +
+                            static_cast<int64_t>(ow) * p.stride2;
+          x2f[j][fn] = *reinterpret_cast<const bf16x8*>(x2 + q * p.cin2 + j * 32 + fq * 8);
+        }
+      }
   }
   if (p.scale == nullptr && res != nullptr && oh < p.ho) {
     uint2 rv[4][FN];
@@ -155,13 +181,14 @@ conv_halo_kernel(const drnmi_conv_args p) {
     a_off[i] = r * p.k_pad + (hswz<128>(r, lslot)) * 8;
   }
   auto a_col = [&](int kt) {
+    if (kt >= nk) return 9 * CIN + (kt - nk) * 64;   // x2 columns
     const int cb = kt / 9;
     return (kt - cb * 9) * CIN + cb * 64;
   };
   auto issue_a = [&](int kt, int i) {
     glds16(wt + a_off[i] + a_col(kt), ring + (kt % kNST) * A_STAGE + (wave * A_PIECES + i) * 1024);
   };
-  for (int t = 0; t < kNST - 1 && t < nk; ++t)
+  for (int t = 0; t < kNST - 1 && t < nk_all; ++t)
 #pragma unroll
     for (int i = 0; i < A_PIECES; ++i) issue_a(t, i);
 
@@ -169,11 +196,11 @@ conv_halo_kernel(const drnmi_conv_args p) {
   for (int t = 0; t < nk; ++t) {
     // retire step t (the patch went out before every weight piece, so it is retired too)
     // younger: the weight pieces of steps t+1 .. t+kNST-2
-    if (t + kNST - 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" :: "n"((kNST - 2) * A_PIECES) : "memory");
+    if (t + kNST - 2 < nk_all) asm volatile("s_waitcnt vmcnt(%0)" :: "n"((kNST - 2) * A_PIECES) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    const bool nxt = t + kNST - 1 < nk;
+    const bool nxt = t + kNST - 1 < nk_all;
     const char* sa = ring + (t % kNST) * A_STAGE;
     const int cb = t / 9;
     const int tap = t - cb * 9;
@@ -201,6 +228,34 @@ conv_halo_kernel(const drnmi_conv_args p) {
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
           acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+    }
+  }
+  // fused downsample: the x2 K steps, B fragments from registers (a 32-channel x2 has one
+  // live K half; the zero-padded second half of its weight step is skipped)
+  for (int t = nk; t < nk_all; ++t) {
+    if (t + kNST - 2 < nk_all) asm volatile("s_waitcnt vmcnt(%0)" :: "n"((kNST - 2) * A_PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + kNST - 1 < nk_all) {
+#pragma unroll
+      for (int i = 0; i < A_PIECES; ++i) issue_a(t + kNST - 1, i);
+    }
+    const char* sa = ring + (t % kNST) * A_STAGE;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      if ((t - nk) * 64 + sub * 32 >= p.cin2) break;
+      bf16x8 af[4];
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int r = wc * 64 + f * 16 + fr;
+        af[f] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + hswz<128>(r, sub * 4 + fq) * 16);
+      }
+#pragma unroll
+      for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], x2f[(t - nk) * 2 + sub][fn], acc[fm][fn], 0, 0, 0);
     }
   }
 
@@ -269,14 +324,21 @@ hipError_t launch_halo(const drnmi_conv_args& p, hipStream_t s) {
 }  // namespace
 
 bool halo_conv_supported(const drnmi_conv_args& p) {
-  // (a fused second input, x2, goes to conv_big: this kernel has no second K segment)
-  if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.ks != 3 || p.stride != 1 || p.pad != p.dil ||
-      p.x2 != nullptr)
+  if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.ks != 3 || p.stride != 1 || p.pad != p.dil)
     return false;
   if ((p.cin != 64 && p.cin != 128) || (p.cout != 64 && p.cout != 128) || p.cout_pad < p.cout)
     return false;
-  if (p.k != 9 * p.cin || p.k_pad != p.k || p.y_sc != 1 || p.y_sp != p.cout || p.dil < 1 || p.dil > 8)
+  if (p.y_sc != 1 || p.y_sp != p.cout || p.dil < 1 || p.dil > 8) return false;
+  if (p.x2 != nullptr) {
+    // fused downsample: cin2 32 or 64 columns after the taps, rows zero-padded to whole 64-column
+    // weight steps; the accumulators start from shift only (no residual, scale folded)
+    if ((p.cin2 != 32 && p.cin2 != 64) || p.stride2 < 1 || p.res != nullptr || p.scale != nullptr ||
+        p.k != 9 * p.cin + p.cin2 || p.k_pad != (p.k + 63) / 64 * 64 || p.h2 < 1 || p.w2 < 1 ||
+        (p.ho - 1) * p.stride2 >= p.h2 || (p.wo - 1) * p.stride2 >= p.w2)
+      return false;
+  } else if (p.k != 9 * p.cin || p.k_pad != p.k) {
     return false;
+  }
   const int wc = p.cout / 64;
   return kNST * 64 * wc * 128 + patch_bytes(p.cin, p.dil, halo_tc(p.cin, p.cout)) <= 160 * 1024;
 }

@@ -330,13 +330,24 @@ class PackedNet:
                     or ds.conv.kernel_size[0] != 1 or ds.conv.padding[0] != 0 or reads.get(nd.res) != 1):
                 continue
             cin2 = self.cstride[ds.src]
-            if cin2 % 64 != 0 or ds.cout_pad != nd.cout_pad or nd.k_pad != nd.k:
+            if ds.cout_pad != nd.cout_pad or nd.k_pad != nd.k:
                 continue
-            if not _route_name(nd, nd.cin_stride).startswith("conv_big") or \
-                    not _route_name(nd, nd.cin_stride, cin2).startswith("conv_big"):
+            # conv_big takes cin2 % 64 == 0 with k_pad == k; the halo kernel (layer3/4 3x3,
+            # cin2 32 or 64) takes rows zero-padded to whole 64-column steps
+            k = nd.k + cin2
+            if cin2 % 64 == 0 and _route_name(nd, nd.cin_stride).startswith("conv_big") and \
+                    _route_name(nd, nd.cin_stride, cin2).startswith("conv_big"):
+                k_pad = k
+            elif cin2 in (32, 64) and _route_name(nd, nd.cin_stride).startswith("conv_halo") and \
+                    _route_name(nd, nd.cin_stride, cin2, (k + 63) // 64 * 64).startswith("conv_halo"):
+                k_pad = (k + 63) // 64 * 64
+            else:
                 continue
-            nd.fused = {"wpk": torch.cat([nd.wpk, ds.wpk[:, :cin2]], dim=1).contiguous(),
-                        "shift": (nd.shift + ds.shift).contiguous(), "k": nd.k + cin2,
+            parts = [nd.wpk, ds.wpk[:, :cin2]]
+            if k_pad > k:
+                parts.append(torch.zeros(nd.wpk.shape[0], k_pad - k, dtype=nd.wpk.dtype, device=nd.wpk.device))
+            nd.fused = {"wpk": torch.cat(parts, dim=1).contiguous(),
+                        "shift": (nd.shift + ds.shift).contiguous(), "k": k, "k_pad": k_pad,
                         "x2_val": ds.src, "stride2": ds.conv.stride[0], "ds": j}
             ds.fused_into = i
 
@@ -412,9 +423,10 @@ FUSE_DOWNSAMPLE = True
 FUSE_STEM = True
 
 
-def _route_name(nd: ConvNode, cin_stride: int, cin2: int = 0) -> str:
-    """Kernel the bf16 launch of `nd` (optionally with a fused cin2-channel second input) goes to,
-    probed on a 16x16 map through drnmi_conv_kernel_name (routing does not depend on size)."""
+def _route_name(nd: ConvNode, cin_stride: int, cin2: int = 0, k_pad: int | None = None) -> str:
+    """Kernel the bf16 launch of `nd` (optionally with a fused cin2-channel second input, weight
+    rows of k_pad columns) goes to, probed on a 16x16 map through drnmi_conv_kernel_name
+    (routing does not depend on size)."""
     c = nd.conv
     a = _lib.ConvArgs()
     a.n, a.h, a.w, a.cin = 1, 16, 16, cin_stride
@@ -423,7 +435,7 @@ def _route_name(nd: ConvNode, cin_stride: int, cin2: int = 0) -> str:
     a.wo = a.ho
     a.cout, a.cout_pad = c.out_channels, nd.cout_pad
     a.k = a.ks * a.ks * cin_stride + cin2
-    a.k_pad = a.k
+    a.k_pad = a.k if k_pad is None else k_pad
     a.dtype, a.out_dtype, a.y_sp, a.y_sc = _lib.DRNMI_BF16, _lib.DRNMI_BF16, c.out_channels, 1
     a.scale = None
     a.tile, a.algo = -1, _lib.ALGO_IGEMM
@@ -578,7 +590,7 @@ class Plan:
         if fused:
             f = fused
             a.wgt, a.shift, a.res = f["wpk"].data_ptr(), f["shift"].data_ptr(), None
-            a.k = a.k_pad = f["k"]
+            a.k, a.k_pad = f["k"], f["k_pad"]
             a.x2 = self.bufs[f["x2_val"]].data_ptr()
             a.cin2 = pk.cstride[f["x2_val"]]
             a.h2, a.w2 = self.shapes[f["x2_val"]]
