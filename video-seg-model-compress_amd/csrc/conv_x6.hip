@@ -148,23 +148,34 @@ conv_x6_kernel(const drnmi_conv_args p) {
     }
   }
 
-  auto issue = [&](int kt, int stage) {
+  // one DMA piece ("instruction") of K step kt: pieces [0, A_PW) weights, then pixel rows
+  struct StepP { int k0, dh, dw, toff; };
+  auto step_params = [&](int kt) {
+    StepP sp;
     const int cb = kt / (KS * KS);
     const int tap = kt - cb * (KS * KS);
-    const int k0 = (tap << lc) + cb * kBK;
-    const int dh = (tap / KS) * dil;
-    const int dw = (tap - (tap / KS) * KS) * dil;
-    const int toff = (dh * W + dw) * cin + cb * kBK;
+    sp.k0 = (tap << lc) + cb * kBK;
+    sp.dh = (tap / KS) * dil;
+    sp.dw = (tap - (tap / KS) * KS) * dil;
+    sp.toff = (sp.dh * W + sp.dw) * cin + cb * kBK;
+    return sp;
+  };
+  auto issue_piece = [&](const StepP& sp, int stage, int i) {
     char* sa = smem + stage * C::STAGE;
-#pragma unroll
-    for (int i = 0; i < C::A_PW; ++i) glds16(wt + a_off[i] + k0, sa + (wave * C::A_PW + i) * 1024);
-#pragma unroll
-    for (int j = 0; j < C::B_PW; ++j) {
-      const bool ok = static_cast<unsigned>(b_ih[j] + dh) < static_cast<unsigned>(H) &&
-                      static_cast<unsigned>(b_iw[j] + dw) < static_cast<unsigned>(W);
-      const void* src = ok ? static_cast<const void*>(x + (b_off[j] + toff)) : static_cast<const void*>(zero_src);
+    if (i < C::A_PW) {
+      glds16(wt + a_off[i] + sp.k0, sa + (wave * C::A_PW + i) * 1024);
+    } else {
+      const int j = i - C::A_PW;
+      const bool ok = static_cast<unsigned>(b_ih[j] + sp.dh) < static_cast<unsigned>(H) &&
+                      static_cast<unsigned>(b_iw[j] + sp.dw) < static_cast<unsigned>(W);
+      const void* src = ok ? static_cast<const void*>(x + (b_off[j] + sp.toff)) : static_cast<const void*>(zero_src);
       glds16(src, sa + C::A_BYTES + (wave * C::B_PW + j) * 1024);
     }
+  };
+  auto issue = [&](int kt, int stage) {
+    const StepP sp = step_params(kt);
+#pragma unroll
+    for (int i = 0; i < C::GLDS; ++i) issue_piece(sp, stage, i);
   };
 
   f32x4 acc[C::FM][C::FN];
@@ -175,6 +186,11 @@ conv_x6_kernel(const drnmi_conv_args p) {
 
   for (int t = 0; t < C::NST - 1 && t < nk; ++t) issue(t, t);
 
+  // per step: B fragments read and split once; then per channel fragment fm, its three A
+  // planes are read and the next step's DMA pieces go out between the MFMA groups (PPF per
+  // group, behind the A reads), pinned with sched_barrier (a one-group-ahead A prefetch needs
+  // 12 more VGPRs than the 2-waves-per-SIMD budget leaves: it spilled)
+  constexpr int PPF = (C::GLDS + C::FM - 1) / C::FM;
   for (int t = 0; t < nk; ++t) {
     const int newer = ((nk - 1) < (t + C::NST - 2) ? (nk - 1) : (t + C::NST - 2)) - t;
     if (C::NST >= 3 && newer >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::GLDS) : "memory");
@@ -182,7 +198,9 @@ conv_x6_kernel(const drnmi_conv_args p) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     // the stage read at step t-1 is free for every wave: refill it with step t + NST - 1
-    if (t + C::NST - 1 < nk) issue(t + C::NST - 1, (t + C::NST - 1) % C::NST);
+    const bool nxt = t + C::NST - 1 < nk;
+    const StepP spn = step_params(nxt ? t + C::NST - 1 : t);
+    const int nst = (t + C::NST - 1) % C::NST;
 
     const char* sa = smem + (t % C::NST) * C::STAGE;
     const char* sb = sa + C::A_BYTES;
@@ -194,13 +212,27 @@ conv_x6_kernel(const drnmi_conv_args p) {
       const float4 hi4 = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq + 1) * 16);
       split3(lo4, hi4, b1[fn], b2[fn], b3[fn]);
     }
-#pragma unroll
-    for (int fm = 0; fm < C::FM; ++fm) {
+    auto load_a = [&](bf16x8 (&dst)[3], int fm) {
       const int r = wc * WCO + fm * 16 + fr;
       const char* ar = sa + r * 64 + swz64(r, fq) * 16;
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(ar);
-      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(ar + C::A_PLANE);
-      const bf16x8 a3 = *reinterpret_cast<const bf16x8*>(ar + 2 * C::A_PLANE);
+      dst[0] = *reinterpret_cast<const bf16x8*>(ar);
+      dst[1] = *reinterpret_cast<const bf16x8*>(ar + C::A_PLANE);
+      dst[2] = *reinterpret_cast<const bf16x8*>(ar + 2 * C::A_PLANE);
+    };
+#pragma unroll
+    for (int fm = 0; fm < C::FM; ++fm) {
+      bf16x8 af[3];
+      load_a(af, fm);
+      // the group's DMA pieces go out while its three A reads are in flight
+      if (nxt) {
+#pragma unroll
+        for (int k = 0; k < PPF; ++k)
+          if (fm * PPF + k < C::GLDS) issue_piece(spn, nst, fm * PPF + k);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8& a1 = af[0];
+      const bf16x8& a2 = af[1];
+      const bf16x8& a3 = af[2];
       // smallest terms first; independent accumulators between dependent MFMAs
 #pragma unroll
       for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, b1[fn], acc[fm][fn], 0, 0, 0);
@@ -214,6 +246,7 @@ conv_x6_kernel(const drnmi_conv_args p) {
       for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2[fn], acc[fm][fn], 0, 0, 0);
 #pragma unroll
       for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[fn], acc[fm][fn], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
