@@ -118,6 +118,23 @@ def test_weights_repack_after_mask_apply(golden_forward, tmp_path):
     _, ref, _ = O.drnseg_forward(sd, "drn_d_22", x.cpu())
     assert (l1.cpu() - ref).abs().max().item() <= 1e-3
     assert (l1 - l0).abs().max().item() > 1e-3
+    # the repack runs once per weight change, not on every later call (the repack key must be
+    # the parameters' state, not a plan key)
+    from drnmi.engine import PackedNet
+    calls = []
+    orig = PackedNet.pack
+    PackedNet.pack = lambda self, *a, **k: (calls.append(1), orig(self, *a, **k))[1]
+    try:
+        for _ in range(3):
+            m(x)
+        assert not calls
+        with torch.no_grad():
+            m.seg.bias.add_(0.0)          # in-place: bumps the version counter
+        for _ in range(3):
+            m(x)
+        assert len(calls) == 1
+    finally:
+        PackedNet.pack = orig
 
 
 def test_bf16_segment_matches_bf16_forward_labels(golden_forward):

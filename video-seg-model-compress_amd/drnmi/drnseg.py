@@ -285,12 +285,12 @@ class DRNSeg(nn.Module):
         if key != self._pack_key:
             if self.precision in self._packed:
                 self._packed[self.precision].pack()
-                for key, plan in list(self._plans.items()):
-                    if key[0] == self.precision:
+                for pkey, plan in list(self._plans.items()):
+                    if pkey[0] == self.precision:
                         try:
                             plan.refresh_weight_ptrs()
                         except RuntimeError:      # the repack changed the plan's launch structure
-                            del self._plans[key]
+                            del self._plans[pkey]
             self._pack_key = key
         if self.precision == "int8" and self._act_scales is None:
             raise RuntimeError("precision 'int8' needs activation scales: call calibrate_int8(frames) first")
