@@ -23,6 +23,34 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// Exact three-way split of 8 fp32 values into bf16 fragments, x = x1 + x2 + x3 (round to
+// nearest even at each step; x - x1 and (x - x1) - x2 are exact in fp32 by Sterbenz): the
+// fp32x arithmetic (include/drnmi.h DRNMI_F32X3).  Works on value pairs: one
+// v_cvt_pk_bf16_f32 is a fragment dword, and its halves widen back to fp32 by a shift (low)
+// and a mask (high), so no per-element register packing is needed.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_bf16x2(f32x2_t v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+}
+__device__ __forceinline__ f32x2_t widen_bf16x2(uint32_t h) {
+  return f32x2_t{__uint_as_float(h << 16), __uint_as_float(h & 0xffff0000u)};
+}
+__device__ __forceinline__ void split3(const float4& lo4, const float4& hi4, bf16x8& b1, bf16x8& b2, bf16x8& b3) {
+  const f32x2_t x[4] = {f32x2_t{lo4.x, lo4.y}, f32x2_t{lo4.z, lo4.w}, f32x2_t{hi4.x, hi4.y}, f32x2_t{hi4.z, hi4.w}};
+  uint32_t u1[4], u2[4], u3[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u1[i] = pk_bf16x2(x[i]);
+    const f32x2_t r1 = x[i] - widen_bf16x2(u1[i]);
+    u2[i] = pk_bf16x2(r1);
+    u3[i] = pk_bf16x2(r1 - widen_bf16x2(u2[i]));
+  }
+  b1 = __builtin_bit_cast(bf16x8, make_uint4(u1[0], u1[1], u1[2], u1[3]));
+  b2 = __builtin_bit_cast(bf16x8, make_uint4(u2[0], u2[1], u2[2], u2[3]));
+  b3 = __builtin_bit_cast(bf16x8, make_uint4(u3[0], u3[1], u3[2], u3[3]));
+}
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static constexpr int kDtype = DRNMI_F32;

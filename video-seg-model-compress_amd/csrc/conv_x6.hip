@@ -53,21 +53,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 __device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }    // bf16 A rows
 __device__ __forceinline__ int swz128(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }   // fp32 B rows
 
-// Exact three-way split of 8 fp32 values into bf16 fragments (round-to-nearest-even each
-// step; x - x1 and (x - x1) - x2 are exact in fp32 by Sterbenz).
-__device__ __forceinline__ void split3(const float4& lo4, const float4& hi4, bf16x8& b1, bf16x8& b2, bf16x8& b3) {
-  const float x[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const __bf16 h = static_cast<__bf16>(x[i]);
-    const float r1 = x[i] - static_cast<float>(h);
-    const __bf16 m = static_cast<__bf16>(r1);
-    const float r2 = r1 - static_cast<float>(m);
-    b1[i] = h;
-    b2[i] = m;
-    b3[i] = static_cast<__bf16>(r2);
-  }
-}
 
 template <int WCO, int WC>
 struct X6Cfg {
@@ -204,20 +189,43 @@ conv_x6_kernel(const drnmi_conv_args p) {
 
     const char* sa = smem + (t % C::NST) * C::STAGE;
     const char* sb = sa + C::A_BYTES;
+    // B: all fragments read now; fn 0, 1 split now, fn 2, 3 inside the first MFMA group so
+    // their VALU work overlaps the MFMAs of fn 0, 1 (each accumulator keeps its product order)
     bf16x8 b1[C::FN], b2[C::FN], b3[C::FN];
+    float4 blo[C::FN], bhi[C::FN];
 #pragma unroll
     for (int fn = 0; fn < C::FN; ++fn) {
       const int r = wp * 64 + fn * 16 + fr;
-      const float4 lo4 = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq) * 16);
-      const float4 hi4 = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq + 1) * 16);
-      split3(lo4, hi4, b1[fn], b2[fn], b3[fn]);
+      blo[fn] = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq) * 16);
+      bhi[fn] = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq + 1) * 16);
     }
+#pragma unroll
+    for (int fn = 0; fn < C::FN / 2; ++fn) split3(blo[fn], bhi[fn], b1[fn], b2[fn], b3[fn]);
     auto load_a = [&](bf16x8 (&dst)[3], int fm) {
       const int r = wc * WCO + fm * 16 + fr;
       const char* ar = sa + r * 64 + swz64(r, fq) * 16;
       dst[0] = *reinterpret_cast<const bf16x8*>(ar);
       dst[1] = *reinterpret_cast<const bf16x8*>(ar + C::A_PLANE);
       dst[2] = *reinterpret_cast<const bf16x8*>(ar + 2 * C::A_PLANE);
+    };
+    // the six products of fragments fn0 <= fn < fn1, smallest terms first, independent
+    // accumulators between dependent MFMAs
+    auto mfma6 = [&](int fm, const bf16x8 (&af)[3], int fn0, int fn1) {
+      const bf16x8& a1 = af[0];
+      const bf16x8& a2 = af[1];
+      const bf16x8& a3 = af[2];
+#pragma unroll
+      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, b1[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b2[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b3[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b1[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2[fn], acc[fm][fn], 0, 0, 0);
+#pragma unroll
+      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[fn], acc[fm][fn], 0, 0, 0);
     };
 #pragma unroll
     for (int fm = 0; fm < C::FM; ++fm) {
@@ -230,22 +238,14 @@ conv_x6_kernel(const drnmi_conv_args p) {
           if (fm * PPF + k < C::GLDS) issue_piece(spn, nst, fm * PPF + k);
       }
       __builtin_amdgcn_sched_barrier(0);
-      const bf16x8& a1 = af[0];
-      const bf16x8& a2 = af[1];
-      const bf16x8& a3 = af[2];
-      // smallest terms first; independent accumulators between dependent MFMAs
+      if (fm == 0) {
+        mfma6(0, af, 0, C::FN / 2);
 #pragma unroll
-      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, b1[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b2[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b3[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b1[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[fn], acc[fm][fn], 0, 0, 0);
+        for (int fn = C::FN / 2; fn < C::FN; ++fn) split3(blo[fn], bhi[fn], b1[fn], b2[fn], b3[fn]);
+        mfma6(0, af, C::FN / 2, C::FN);
+      } else {
+        mfma6(fm, af, 0, C::FN);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   }

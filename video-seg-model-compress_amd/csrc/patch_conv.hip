@@ -41,19 +41,6 @@ struct PatchCfg {
   static_assert(TC % 16 == 0, "tile columns in 16-pixel fragments");
 };
 
-// Exact three-way split of 8 fp32 values into bf16 fragments (fp32x mode; as conv_x6.hip).
-__device__ __forceinline__ void split3(const float4& lo4, const float4& hi4, bf16x8& b1, bf16x8& b2, bf16x8& b3) {
-  const float x[8] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const __bf16 h = static_cast<__bf16>(x[i]);
-    const float r1 = x[i] - static_cast<float>(h);
-    const __bf16 m = static_cast<__bf16>(r1);
-    b1[i] = h;
-    b2[i] = m;
-    b3[i] = static_cast<__bf16>(r1 - static_cast<float>(m));
-  }
-}
 
 // X6 (fp32x mode, dtype DRNMI_F32X3): fp32 input patch in LDS, weights as three bf16 planes in
 // registers, every B fragment split exactly into three bf16 terms and the six products above
