@@ -33,6 +33,9 @@ typedef __attribute__((address_space(1))) const void g_void_t;
 __device__ uint4 g_halo_zero[64];   // zero-initialised source of padded pixels
 
 constexpr int kTR = 4, kTC = 64;     // output block: rows x columns
+#ifndef DRNMI_HALO_ABL
+#define DRNMI_HALO_ABL 0             // diagnostic builds only: bit 0 skips the patch DMA
+#endif
 constexpr int kNST = 3;              // weight ring stages (4-5 stages cost a workgroup per CU: slower)
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
@@ -97,7 +100,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
   constexpr int NCB = CIN / 64;
   const int nk = 9 * NCB;                       // tap steps
   const bool fused = p.x2 != nullptr;
-  const int nx = fused ? (p.cin2 + 63) / 64 : 0; // x2 steps (64 K columns each)
+  const int nx = fused ? 1 : 0;                  // x2 steps (cin2 <= 64: one 64-column step)
   const int nk_all = nk + nx;
 
   // --- accumulator start: 0, or shift + residual when the BN scale is folded into the
@@ -160,7 +163,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
     const char* zero_src = reinterpret_cast<const char*>(g_halo_zero) + lane * 16;
     const int lr = lane / CPR, ls = lane % CPR;
     const int64_t img = static_cast<int64_t>(n) * H;
-    for (int pc = wave; pc < npieces; pc += NW) {
+    for (int pc = wave; pc < ((DRNMI_HALO_ABL & 1) ? 0 : npieces); pc += NW) {
       const int row = pc * RPP + lr;
       const int pr = row / PW;
       const int ih = oh0 - p.pad + pr;
@@ -206,45 +209,49 @@ conv_halo_kernel(const drnmi_conv_args p) {
     const int tap = t - cb * 9;
     const int dh = (tap / 3) * dil, dw = (tap - (tap / 3) * 3) * dil;
     const int prow0 = (wp + dh) * PW + dw;            // patch row of this wave's pixel 0
-    bf16x8 af[4], bfr[FN];
+    // both K halves' fragments are read up front (the second half's reads are in flight under
+    // the first half's MFMAs; the two waves of a SIMD run these phases in lockstep after the
+    // barrier, so a read issued right before its MFMAs would expose the LDS latency)
+    bf16x8 af[2][4], bfr[2][FN];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         const int r = wc * 64 + f * 16 + fr;
-        af[f] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + hswz<128>(r, sub * 4 + fq) * 16);
+        af[sub][f] = *reinterpret_cast<const bf16x8*>(sa + r * 128 + hswz<128>(r, sub * 4 + fq) * 16);
       }
 #pragma unroll
       for (int f = 0; f < FN; ++f) {
         const int pr = prow0 + f * 16 + fr;
-        bfr[f] = *reinterpret_cast<const bf16x8*>(patch + pr * ROWB + hswz<ROWB>(pr, cb * 8 + sub * 4 + fq) * 16);
+        bfr[sub][f] = *reinterpret_cast<const bf16x8*>(patch + pr * ROWB + hswz<ROWB>(pr, cb * 8 + sub * 4 + fq) * 16);
       }
       if (sub == 0 && nxt) {
 #pragma unroll
         for (int i = 0; i < A_PIECES; ++i) issue_a(t + kNST - 1, i);
       }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
 #pragma unroll
       for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], bfr[fn], acc[fm][fn], 0, 0, 0);
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[sub][fm], bfr[sub][fn], acc[fm][fn], 0, 0, 0);
     }
   }
-  // fused downsample: the x2 K steps, B fragments from registers (a 32-channel x2 has one
-  // live K half; the zero-padded second half of its weight step is skipped)
-  for (int t = nk; t < nk_all; ++t) {
-    if (t + kNST - 2 < nk_all) asm volatile("s_waitcnt vmcnt(%0)" :: "n"((kNST - 2) * A_PIECES) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // fused downsample: the x2 K step (cin2 <= 64: one 64-column weight step), B fragments from
+  // registers; a 32-channel x2 has one live K half (the zero-padded second half is skipped).
+  // Static fragment indices only: a runtime index would put x2f in scratch memory.
+  if (fused) {
+    const int t = nk;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (t + kNST - 1 < nk_all) {
-#pragma unroll
-      for (int i = 0; i < A_PIECES; ++i) issue_a(t + kNST - 1, i);
-    }
     const char* sa = ring + (t % kNST) * A_STAGE;
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      if ((t - nk) * 64 + sub * 32 >= p.cin2) break;
+      if (sub * 32 >= p.cin2) break;
       bf16x8 af[4];
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
@@ -255,7 +262,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
       for (int fm = 0; fm < 4; ++fm)
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
-          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], x2f[(t - nk) * 2 + sub][fn], acc[fm][fn], 0, 0, 0);
+          acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[fm], x2f[sub][fn], acc[fm][fn], 0, 0, 0);
     }
   }
 
