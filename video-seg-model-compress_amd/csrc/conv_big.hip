@@ -67,7 +67,11 @@ constexpr int kMinCin = 32;   // every K step lies inside one tap
 template <int ROWB>
 __device__ __forceinline__ int swzb(int row, int chunk) {
   if constexpr (ROWB == 128) return chunk ^ ((row >> 1) & 7);   // 128-B rows
-  else return chunk ^ ((row >> 2) & 3);                        //  64-B rows
+  // 64-B rows: the 16 rows of a fragment read span 4 banks-quads per row residue; the four
+  // ds_read_b128 lane groups take chunk patterns (0,1,1,0) / (1,0,0,1) / (2,3,3,2) / (3,2,2,3)
+  // over row quarters r >> 2 = 0..3, so XOR-ing 3 into rows 8..15 of each 16 makes every group
+  // conflict-free (the former (row >> 2) & 3 left every group 2-way)
+  else return chunk ^ (((row >> 3) & 1) * 3);
 }
 template <int BK>
 __device__ __forceinline__ int swz(int row, int chunk) { return swzb<BK * 2>(row, chunk); }   // bf16 rows
