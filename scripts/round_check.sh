@@ -14,10 +14,11 @@ tail -1 $OUT/smoke.log
 timeout -k 10 300 python -u $R/bench.py > $OUT/bench_bf16.json 2> $OUT/bench_bf16.err || { echo bench bf16 failed; tail -5 $OUT/bench_bf16.err; exit 1; }
 timeout -k 10 300 python -u $R/bench.py --precision fp32 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/bench_fp32.json 2> $OUT/bench_fp32.err || { echo bench fp32 failed; exit 1; }
 timeout -k 10 300 python -u $R/bench.py --precision fp32x --steps 5 --warmup 2 > $OUT/bench_fp32x.json 2> $OUT/bench_fp32x.err || { echo bench fp32x failed; exit 1; }
+timeout -k 10 300 python -u $R/bench.py --precision int8 --no-cpu-baseline > $OUT/bench_int8.json 2> $OUT/bench_int8.err || { echo bench int8 failed; exit 1; }
 timeout -k 10 300 python -u $R/bench.py --host-frames --no-cpu-baseline > $OUT/bench_host.json 2> $OUT/bench_host.err || { echo bench host failed; exit 1; }
 python3 - <<PY
 import json
-for n in ("bf16", "fp32", "fp32x", "host"):
+for n in ("bf16", "fp32", "fp32x", "int8", "host"):
     d = json.loads(open("$OUT/bench_%s.json" % n).read().strip().splitlines()[-1])
     print(n, round(d["value"], 1), d["roofline"]["kernel"], d["roofline"]["frac"], d.get("host_frames", {}).get("value"),
           d.get("cpu_baseline", {}).get("value"), d.get("cpu_baseline", {}).get("cores"))
