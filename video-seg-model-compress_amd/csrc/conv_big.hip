@@ -1050,11 +1050,7 @@ hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
     case 2: return launch_big<KS, 64, 1, 4, 32, PERSIST>(p, s);    //  64 x 256 tile, 4 waves, 4 x 20 KB
     case 3: return launch_big<KS, 32, 1, 3, 64, PERSIST>(p, s);    //  32 x 256 tile, 4 waves, 3 x 36 KB
     case 4: return launch_big<KS, 128, 2, 4, 32, PERSIST>(p, s);   // 256 x 256 tile, 8 waves, 4 x 32 KB
-#if defined(DRNMI_V5_NST3)    // diagnostic builds only: the 128 x 256 BK-32 tile on a 3 x 24 KB ring (2 WGs per CU)
-    case 5: return launch_big<KS, 128, 1, 3, 32, PERSIST>(p, s);
-#else
     case 5: return launch_big<KS, 128, 1, 4, 32, PERSIST>(p, s);   // 128 x 256 tile, 4 waves, 4 x 24 KB
-#endif
     default: return hipErrorInvalidValue;
   }
 }
