@@ -9,6 +9,7 @@ import pytest
 import torch
 
 import train_case as TC
+from drnmi import torch_ops  # noqa: F401  (registers torch.ops.drnmi.* for tests run on their own)
 from oracle import drn_oracle as O
 
 pytestmark = pytest.mark.gpu

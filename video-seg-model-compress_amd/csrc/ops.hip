@@ -301,45 +301,58 @@ up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict_
   for (int oy = oy_begin; oy < oy_end; ++oy) {
     const int ky1 = oy + 4 - 8 * i1, ky0 = ky1 + 8;
     int arg[4];
+    // two pixels per packed fp32 op (v_pk_mul_f32 / v_pk_fma_f32: the same per-element rounding
+    // as the scalar mul + fma chain), then per pixel a running top-2 with one v_med3 per class
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int kx1 = kx1_0 + p, kx0 = kx1 + 8;
-      const float w00 = (vi0 && vj0) ? wk[ky0 * 16 + kx0] : 0.f;
-      const float w01 = (vi0 && vj1) ? wk[ky0 * 16 + kx1] : 0.f;
-      const float w10 = (vi1 && vj0) ? wk[ky1 * 16 + kx0] : 0.f;
-      const float w11 = (vi1 && vj1) ? wk[ky1 * 16 + kx1] : 0.f;
-      float v[NC];
+    for (int pp = 0; pp < 2; ++pp) {
+      f32x2_t w00, w01, w10, w11;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int kx1 = kx1_0 + 2 * pp + e, kx0 = kx1 + 8;
+        w00[e] = (vi0 && vj0) ? wk[ky0 * 16 + kx0] : 0.f;
+        w01[e] = (vi0 && vj1) ? wk[ky0 * 16 + kx1] : 0.f;
+        w10[e] = (vi1 && vj0) ? wk[ky1 * 16 + kx0] : 0.f;
+        w11[e] = (vi1 && vj1) ? wk[ky1 * 16 + kx1] : 0.f;
+      }
+      f32x2_t v[NC];
 #pragma unroll
       for (int k = 0; k < NC; ++k) {
-        float a = s00[k] * w00;
-        a = fmaf(s01[k], w01, a);
-        a = fmaf(s10[k], w10, a);
-        a = fmaf(s11[k], w11, a);
+        f32x2_t a = f32x2_t{s00[k], s00[k]} * w00;
+        a = __builtin_elementwise_fma(f32x2_t{s01[k], s01[k]}, w01, a);
+        a = __builtin_elementwise_fma(f32x2_t{s10[k], s10[k]}, w10, a);
+        a = __builtin_elementwise_fma(f32x2_t{s11[k], s11[k]}, w11, a);
         v[k] = a;
       }
-      float best = v[0], second = -INFINITY;
-      int am = 0;
 #pragma unroll
-      for (int k = 1; k < NC; ++k) {
-        if (v[k] > best) { second = best; best = v[k]; am = k; }
-        else if (v[k] > second) second = v[k];
-      }
-      if (best - second < 0x1p-16f) {
-        float vmax = -INFINITY;
+      for (int e = 0; e < 2; ++e) {
+        // best >= second throughout, so med3(best, second, x) is the new second for every x
+        // (x > best: old best; second < x <= best: x; else second) -- the if / else-if chain
+        float best = v[0][e], second = -INFINITY;
+        int am = 0;
 #pragma unroll
-        for (int k = 0; k < NC; ++k) vmax = fmaxf(vmax, v[k]);
-        float sum = 0.f;
-#pragma unroll
-        for (int k = 0; k < NC; ++k) sum += expf(v[k] - vmax);
-        const float lse = logf(sum);
-        float bl = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < NC; ++k) {
-          const float lp = (v[k] - vmax) - lse;
-          if (lp > bl) { bl = lp; am = k; }
+        for (int k = 1; k < NC; ++k) {
+          const float x = v[k][e];
+          am = x > best ? k : am;
+          second = __builtin_amdgcn_fmed3f(best, second, x);
+          best = fmaxf(best, x);
         }
+        if (best - second < 0x1p-16f) {
+          float vmax = -INFINITY;
+#pragma unroll
+          for (int k = 0; k < NC; ++k) vmax = fmaxf(vmax, v[k][e]);
+          float sum = 0.f;
+#pragma unroll
+          for (int k = 0; k < NC; ++k) sum += expf(v[k][e] - vmax);
+          const float lse = logf(sum);
+          float bl = -INFINITY;
+#pragma unroll
+          for (int k = 0; k < NC; ++k) {
+            const float lp = (v[k][e] - vmax) - lse;
+            if (lp > bl) { bl = lp; am = k; }
+          }
+        }
+        arg[2 * pp + e] = am;
       }
-      arg[p] = am;
     }
     const int64_t pix = static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy) * W + 4 * q;
     if (LABEL_DTYPE == DRNMI_U8) {
