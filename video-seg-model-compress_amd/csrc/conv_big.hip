@@ -392,8 +392,8 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
   using K = KT<T>;
   using C = BigCfg<WCO, WC, NST, BK, NWP, K::ESZ>;
   static_assert(!SPARSE || K::ESZ == 2, "unit skipping: bf16 only");
-  static_assert(!STRIP || (KS == 3 && NST == 2 && BK == 64 && K::ESZ == 2 && !PERSIST && !SPARSE && !X2 &&
-                           C::NW == 8), "strip mode: the 256 x 256 bf16 3x3 instantiation only");
+  static_assert(!STRIP || (KS == 3 && NST == 2 && C::ROWB == 128 && !PERSIST && !SPARSE && !X2 && C::NW == 8),
+                "strip mode: the 256 x 256 3x3 instantiations with 128-B rows (bf16 BK 64, int8 BK 128)");
   constexpr int CE = 16 / K::ESZ;   // elements per 16-B chunk
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -724,6 +724,13 @@ conv_big_kernel(const drnmi_conv_args p) {
 __global__ void __launch_bounds__(512, 1)
 conv_strip_kernel(const drnmi_conv_args p) {
   conv_big_body<uint16_t, 3, 128, 2, 2, 64, false, 4, false, false, true>(p);
+}
+
+// int8 strip-staged B: conv_i8_kernel<3, 128, 2, 2, 128> with the STRIP B path (int8 rows of 128
+// channels are 128 B, the bf16 layout): same MFMA order, bit-identical to the per-tap gather.
+__global__ void __launch_bounds__(512, 1)
+conv_i8_strip_kernel(const drnmi_conv_args p) {
+  conv_big_body<int8_t, 3, 128, 2, 2, 128, false, 4, false, false, true>(p);
 }
 
 // W8A8 (config C5): the same LDS-DMA pipeline over int8 elements, BK int8 channels per K step
@@ -1180,10 +1187,32 @@ bool i8_conv_supported(const drnmi_conv_args& p) {
          (p.out_dtype == DRNMI_F32 || p.out_dtype == DRNMI_BF16 || p.out_dtype == DRNMI_I8);
 }
 
+bool i8_strip_ok(const drnmi_conv_args& p) {
+  return i8_variant(p) == 0 && p.cin % 128 == 0 && strip_enabled() && strip_ok(p);
+}
+
+hipError_t launch_i8_strip(const drnmi_conv_args& p, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_i8_strip_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kStripLds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const int64_t blocks = (M / kBPX) * ((p.cout + 255) / 256);
+  hipLaunchKernelGGL(conv_i8_strip_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), kStripLds, s, p);
+  return hipGetLastError();
+}
+
 int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!i8_conv_supported(p)) return DRNMI_ENOTSUP;
   const int v = i8_variant(p);
   if ((p.cout + kI8Variants[v].bco - 1) / kI8Variants[v].bco * kI8Variants[v].bco > p.cout_pad) return DRNMI_EINVAL;
+  if (p.ks == 3 && i8_strip_ok(p)) {
+    const hipError_t e = launch_i8_strip(p, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
   const hipError_t e = p.ks == 3 ? launch_i8_variant<3>(p, v, s) : launch_i8_variant<1>(p, v, s);
   return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
 }
@@ -1191,6 +1220,7 @@ int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
 const char* i8_conv_name(const drnmi_conv_args& p) {
   if (!i8_conv_supported(p)) return nullptr;
   const int v = i8_variant(p);
+  if (p.ks == 3 && i8_strip_ok(p)) return "conv_i8_strip_kernel";
   return p.ks == 3 ? kI8Variants[v].name3 : kI8Variants[v].name1;
 }
 
