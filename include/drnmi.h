@@ -95,8 +95,9 @@ typedef struct drnmi_conv_args {
 
 /* Algorithms behind drnmi_conv2d_bn_act:
  *  DRNMI_ALGO_IGEMM  NHWC implicit GEMM (any power-of-two cin >= 8, any ks/stride/dil; bf16 or
- *                    fp32).  tile -1 picks the bf16 LDS-DMA kernel (tiles 4..7: 128/256/64/32
- *                    output channels x 256 pixels; cin >= 64, ks 1 or 3) when it applies, else a
+ *                    fp32).  tile -1 picks the bf16 LDS-DMA kernel (tiles 4..7: 128/256/64/64
+ *                    output channels x 256 pixels, tile 6 with 32-channel K steps, tile 7 with
+ *                    64; cin >= 64, ks 1 or 3) when it applies, else a
  *                    register-staged tile 0..3 by cout.
  *  DRNMI_ALGO_PATCH  bf16-only small-channel direct conv for the full-resolution layers
  *                    (lmodels/drn.py:132-137 layer0, :201-211 layer1/layer2): the input tile

@@ -1027,13 +1027,13 @@ constexpr Variant kVariants[] = {
     {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, false, 4, false, false>", "conv_big_kernel<1, 128, 1, 3, 64, false, 4, false, false>"},
     {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, false, 4, false, false>", "conv_big_kernel<1, 128, 2, 2, 64, false, 4, false, false>"},
     {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, false, 4, false, false>", "conv_big_kernel<1, 64, 1, 4, 32, false, 4, false, false>"},
-    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, false, 4, false, false>", "conv_big_kernel<1, 32, 1, 3, 64, false, 4, false, false>"},
+    {64, 64, "conv_big_kernel<3, 64, 1, 2, 64, false, 4, false, false>", "conv_big_kernel<1, 64, 1, 2, 64, false, 4, false, false>"},
     {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, false, 4, false, false>", "conv_big_kernel<1, 128, 2, 4, 32, false, 4, false, false>"},
     {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, false, 4, false, false>", "conv_big_kernel<1, 128, 1, 4, 32, false, 4, false, false>"},
     {128, 64, "conv_big_kernel<3, 128, 1, 3, 64, true, 4, false, false>", "conv_big_kernel<1, 128, 1, 3, 64, true, 4, false, false>"},
     {256, 64, "conv_big_kernel<3, 128, 2, 2, 64, true, 4, false, false>", "conv_big_kernel<1, 128, 2, 2, 64, true, 4, false, false>"},
     {64, 32, "conv_big_kernel<3, 64, 1, 4, 32, true, 4, false, false>", "conv_big_kernel<1, 64, 1, 4, 32, true, 4, false, false>"},
-    {32, 64, "conv_big_kernel<3, 32, 1, 3, 64, true, 4, false, false>", "conv_big_kernel<1, 32, 1, 3, 64, true, 4, false, false>"},
+    {64, 64, "conv_big_kernel<3, 64, 1, 2, 64, true, 4, false, false>", "conv_big_kernel<1, 64, 1, 2, 64, true, 4, false, false>"},
     {256, 32, "conv_big_kernel<3, 128, 2, 4, 32, true, 4, false, false>", "conv_big_kernel<1, 128, 2, 4, 32, true, 4, false, false>"},
     {128, 32, "conv_big_kernel<3, 128, 1, 4, 32, true, 4, false, false>", "conv_big_kernel<1, 128, 1, 4, 32, true, 4, false, false>"},
     {256, 64, "conv_pp_kernel<3>", "conv_pp_kernel<1>"},
@@ -1055,7 +1055,7 @@ hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
     case 1: return launch_big<KS, 128, 2, 2, 64, PERSIST>(p, s);   // 256 x 256 tile, 8 waves, 2 x 64 KB
 #endif
     case 2: return launch_big<KS, 64, 1, 4, 32, PERSIST>(p, s);    //  64 x 256 tile, 4 waves, 4 x 20 KB
-    case 3: return launch_big<KS, 32, 1, 3, 64, PERSIST>(p, s);    //  32 x 256 tile, 4 waves, 3 x 36 KB
+    case 3: return launch_big<KS, 64, 1, 2, 64, PERSIST>(p, s);    //  64 x 256 tile, 4 waves, 2 x 40 KB
     case 4: return launch_big<KS, 128, 2, 4, 32, PERSIST>(p, s);   // 256 x 256 tile, 8 waves, 4 x 32 KB
     case 5: return launch_big<KS, 128, 1, 4, 32, PERSIST>(p, s);   // 128 x 256 tile, 4 waves, 4 x 24 KB
     default: return hipErrorInvalidValue;
@@ -1144,7 +1144,13 @@ int auto_variant(const drnmi_conv_args& p) {
   // 64 -> 128 (D-22 layer4.0 conv1 / downsample, stride 2): the 64-wide BK-32 tile too, two
   // workgroups per CU against one for the 128 x 256 x 3-stage ring: 98 vs 116 us (3x3), 50 vs
   // 75 us (1x1) at batch 8 (scripts/conv_micro.py); the fused-x2 instantiations are bases 0/1
-  if (p.cin <= 64 && p.cout % 256 != 0 && p.x2 == nullptr) return 2;
+  if (p.cin <= 64 && p.cout % 256 != 0 && p.x2 == nullptr) {
+    // cin == 64 3x3 (D-22 layer4.0 conv1, stride 2): the 64-wide tile with 64-channel K steps on a
+    // 2 x 40 KB ring halves the K steps of the BK-32 tile at the same DMA bytes: 93.6 vs 102 us
+    // at batch 8 (profiles/r3k_tile_64w_bk64_ab.txt)
+    if (p.cin == 64 && p.ks == 3) return 3;
+    return 2;
+  }
   return p.cout % 256 == 0 ? 1 : p.cout % 128 == 0 ? 0 : 2;
 }
 
