@@ -11,6 +11,11 @@ timing barrier and the max-over-ranks of the elapsed time).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+`--gpus N` without a torchrun environment spawns the N rank processes itself (before any GPU
+call; one device each, RCCL rendezvous on 127.0.0.1); under torchrun WORLD_SIZE must equal N.
+The default bf16 line also carries `exact_mode`: the fp32-accurate (fp32x) engine on the same
+weights and frames, timed in the same process, with its own dominant-kernel roofline and parity.
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -28,7 +33,7 @@ sys.path.insert(0, REPO)
 METRIC = "frames/sec @1024x2048 DRN-D-22 on 1/2/4/8 MI355X; mIoU vs ref; %HBM roofline"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -53,7 +58,129 @@ def parse():
                     help="also time the PCIe-inclusive pipeline: frames in pinned host memory, H2D on a copy "
                          "stream overlapped with the previous batch's compute (reported as 'host_frames'; "
                          "the headline value stays HBM-resident)")
-    return ap.parse_args()
+    ap.add_argument("--no-exact-mode", action="store_true",
+                    help="skip the exact_mode (fp32x) sub-measurement of the default bf16 line")
+    ap.add_argument("--exact-steps", type=int, default=5)
+    ap.add_argument("--stub-step", action="store_true",
+                    help="test hook: no GPU; gloo ranks run a CPU stand-in step through the same launcher, "
+                         "seeding, timing and max-over-ranks code (tests/test_bench_launcher.py)")
+    return ap.parse_args(argv)
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` outside torchrun: start N rank processes of this script (one
+    per GPU, LOCAL_RANK = RANK = r) with a 127.0.0.1 rendezvous, before this process touches the
+    GPU, and return the worst exit code.  The reference's multi-GPU entry does the same through
+    torch.multiprocessing + init_process_group (semantic_seg_multigpu.py:467-468)."""
+    import socket
+    import subprocess
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rcs = [None] * n
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+                    if rcs[i] not in (None, 0):      # one rank failed: the others would hang in a collective
+                        for q in procs:
+                            if q.poll() is None:
+                                q.terminate()
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return max(abs(rc) for rc in rcs)
+
+
+def resolve_world(args, environ=os.environ):
+    """(world, rank, local_rank) of this process, or None when it must spawn the ranks itself.
+    A torchrun environment whose WORLD_SIZE differs from --gpus is refused."""
+    if environ.get("WORLD_SIZE") is None:
+        if args.gpus > 1:
+            return None
+        return 1, 0, 0
+    world = int(environ["WORLD_SIZE"])
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch with matching values)")
+    return world, int(environ.get("RANK", "0")), int(environ.get("LOCAL_RANK", "0"))
+
+
+def timed_region(step, steps, world, dev):
+    """K timed steps bracketed by barrier + device sync on both sides; the slowest rank's
+    elapsed time defines the job (max over ranks).  Returns (job_seconds, own_seconds)."""
+    import torch
+    import torch.distributed as dist
+    from drnmi.dist import max_over_ranks
+    cuda = dev.type == "cuda"
+    if cuda:
+        torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    if cuda:
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+    if cuda:
+        torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    own = time.perf_counter() - t0
+    return max_over_ranks(own, device=dev), own
+
+
+def gather_ranks(vals, world, dev):
+    """[[v0, v1, ...] per rank] of a few host floats (per-rank bookkeeping in the JSON line)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=dev)
+    if world == 1:
+        return [t.tolist()]
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def frame_seed(rank: int) -> int:
+    """Per-rank synthetic frame stream: every rank segments different frames."""
+    return 1000 + rank
+
+
+def stub_main(args, world, rank):
+    """CPU stand-in for the GPU step (test hook): gloo ranks, per-rank seeded uint8 frames of the
+    requested shape, a reduction over them as the 'step'; same timing and JSON fields."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("gloo")
+    g = torch.Generator().manual_seed(frame_seed(rank))
+    frames = torch.randint(0, 256, (args.batch, args.height, args.width, 3), dtype=torch.uint8, generator=g)
+    acc = [0.0]
+
+    def step(timed):
+        acc[0] += float(frames.float().mean())
+
+    for _ in range(args.warmup):
+        step(False)
+    el, own = timed_region(step, args.steps, world, dev)
+    per = gather_ranks([frame_seed(rank), float(frames.long().sum()), own], world, dev)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": world * args.batch * args.steps / el, "unit": "frames/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": el / args.steps * 1e3, "scaling": "weak", "data": "stub (CPU test hook)",
+                          "per_rank": [{"rank": r, "frame_seed": int(v[0]), "frame_sum": int(v[1]),
+                                        "seconds": v[2]} for r, v in enumerate(per)]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def pruned_model(args, dev):
@@ -168,7 +295,7 @@ def cpu_baseline(args, seconds):
                       f"within the cgroup quota, {cpu_model})"}, (frames, labels)
 
 
-def parity_vs_ref(args, model, frames, ref_labels, dev):
+def parity_vs_ref(args, model, frames, ref_labels, dev, precision=None):
     """The measured path's labels on the CPU baseline's frames vs the oracle's (the reference
     restated, pinned to its goldens): pixel agreement and mIoU with the reference labels as
     ground truth (BASELINE.json metric "mIoU vs ref"; semantic_seg.py:293-300 fast_hist)."""
@@ -180,46 +307,27 @@ def parity_vs_ref(args, model, frames, ref_labels, dev):
     got = model.segment(torch.from_numpy(frames).to(dev), INFO_MEAN, INFO_STD, False).long()
     ref = torch.from_numpy(np.stack([ref_labels[i] for i in range(len(frames))])).long().to(dev)
     hist = metrics.fast_hist(got.flatten(), ref.flatten(), 19)
-    return {"frames": len(frames), "precision": args.precision,
+    return {"frames": len(frames), "precision": precision or args.precision,
             "label_agreement": float((got == ref).float().mean()),
             "label_mismatches": int((got != ref).sum()),
             "miou_vs_ref": float(metrics.miou(hist.cpu().numpy())),
             "reference": "oracle/drn_oracle.py fp32 torch-CPU forward, same weights and frames"}
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-
-    from drnmi import _lib
-    from drnmi.dist import max_over_ranks
-    from drnmi.drnseg import INFO_MEAN, INFO_STD, build
-    from drnmi.roofline import kernel_peak, network_roofline, node_work
-
-    if args.prune:
-        model, n_pruned = pruned_model(args, dev)
-    else:
-        model = build(args.arch, 19, seed=0, device=dev,
-                      precision="bf16" if args.precision == "int8" else args.precision)
-    if args.precision == "int8":
-        model = calibrate(model, args, dev)
-    B, H, W = args.batch, args.height, args.width
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    frames = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
-    plan = model.plan(B, H, W, device=dev)     # the plan model.segment() runs (same key)
-    works = node_work(plan)
-    lib = _lib.load()
+def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
+    """Time `steps` seg_video steps of `model` over `frames` (resident in HBM) after `warmup`
+    untimed ones.  Returns the job time and the dominant kernel's per-launch HIP-event record
+    (timed region) plus a per-kernel table (one fully instrumented step after it)."""
     import ctypes
 
+    import torch
+    from drnmi import _lib
+    from drnmi.drnseg import INFO_MEAN, INFO_STD
+    from drnmi.roofline import launch_work
+
+    B, H, W = frames.shape[0], frames.shape[1], frames.shape[2]
+    plan = model.plan(B, H, W, device=dev)     # the plan model.segment() runs (same key)
+    lib = _lib.load()
     fused_stem = getattr(plan, "stem_fused", False)
 
     def launched_name(i):
@@ -232,35 +340,19 @@ def main():
         return lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
 
     names = [launched_name(i) for i in range(len(plan.args))]
-    # useful work of a pruned layer: dense FLOPs x the density of its weights, on
-    # dense and sparse kernels alike (the dense kernel multiplies the zeros too)
     nodes = plan.packed.graph.nodes
+    # per-launch work (roofline.launch_work): a folded downsample's FLOPs and input run inside its
+    # block's last conv, the fused stem launch carries layer1; useful work of a pruned layer
+    #  = dense FLOPs x the density of its weights, on dense and sparse kernels alike
+    works = launch_work(plan)
     density = [float((nd.conv.weight != 0).sum()) / nd.conv.weight.numel() for nd in nodes]
-    # a folded-away downsample's FLOPs run inside its block's last conv: attribute them there
-    # (its input read too; the residual is never written or read)
-    works = list(works)
-    for i in sorted(getattr(plan, "skip", ())):
-        j = nodes[i].fused_into
-        n_, fj, bj = works[j]
-        fi, bi = works[i][1], works[i][2]
-        oh, ow = plan.shapes[nodes[j].dst]
-        res_b = plan.n * oh * ow * nodes[j].conv.out_channels * 2      # the bf16 residual tensor
-        # conv2 bytes lose the residual read; the downsample's input + weights (not its output) join
-        works[j] = (n_, fj + fi, bj - res_b + (bi - res_b))
-        works[i] = (works[i][0], 0.0, 0.0)
     if fused_stem:
-        # layer1 runs inside the stem launch; the 16-channel stem output is neither written
-        # nor read back
-        h0, w0 = plan.shapes[nodes[0].dst]
-        mid = plan.n * h0 * w0 * nodes[0].conv.out_channels * 2
-        works[0] = (works[0][0], works[0][1] + works[1][1], works[0][2] + works[1][2] - 2 * mid)
-        works[1] = (works[1][0], 0.0, 0.0)
         density[0] = density[1] = float(sum((nd.conv.weight != 0).sum() for nd in nodes[:2])) / \
             sum(nd.conv.weight.numel() for nd in nodes[:2])
     dense_flops = {i: w[1] for i, w in enumerate(works)}
     works = [(w[0], w[1] * density[i], w[2]) if i < len(nodes) else w for i, w in enumerate(works)]
     events = []
-    pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * len(names) * max(args.steps, 2))]
+    pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * len(names) * max(steps, 2))]
     watch = [None]        # None: every launch; else only launches of this kernel name
 
     def hook(i, nd, before):
@@ -272,7 +364,7 @@ def main():
 
     def step(timed, x=frames):
         # the public API a seg_video user calls: DRNSeg.segment -> torch.ops.drnmi.segment
-        model.timing_hook = hook if (timed and not args.no_kernel_events) else None
+        model.timing_hook = hook if (timed and kernel_events) else None
         return model.segment(x, INFO_MEAN, INFO_STD, False)
 
     def collect():
@@ -291,7 +383,7 @@ def main():
         events.clear()
         return per_
 
-    for _ in range(max(args.warmup - 1, 0)):
+    for _ in range(max(warmup - 1, 0)):
         step(False)
     # last warm-up step instrumented: it names the dominant kernel (the template instance, as
     # rocprofv3 names it, with the largest total time); inside the timed region only that
@@ -300,17 +392,7 @@ def main():
     warm = collect()
     dominant = max(warm, key=lambda k: sum(warm[k]["d"])) if warm else None
     watch[0] = dominant
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = max_over_ranks(time.perf_counter() - t0, device=dev)   # the slowest rank defines the job
+    el, own = timed_region(step, steps, world, dev)
     timed_per = collect()
     # per-kernel table: one fully instrumented step after the timed region
     watch[0] = None
@@ -319,11 +401,85 @@ def main():
     if dominant in timed_per:
         per[dominant] = timed_per[dominant]
     model.timing_hook = None
-    host = host_frames_run(args, model, step, world, dev) if args.host_frames else None
+    return {"el": el, "own": own, "plan": plan, "names": names, "density": density, "per": per,
+            "dominant": dominant, "timed": timed_per.get(dominant), "step": step}
 
-    durs = timed_per[dominant]["d"] if dominant in timed_per else []
-    flops = timed_per[dominant]["f"] if dominant in timed_per else []
-    nr = network_roofline(plan)
+
+def roofline_block(args, m, precision):
+    """The dominant kernel's roofline object from a measure() record."""
+    from drnmi.roofline import kernel_peak
+    t = m["timed"]
+    if not t:
+        return None, None
+    durs, flops = t["d"], t["f"]
+    avg_d = sum(durs) / len(durs)
+    avg_f = sum(flops) / len(flops)
+    ach = avg_f / avg_d / 1e12
+    peak = kernel_peak(m["dominant"], m["plan"].packed.base) / 1e12
+    traffic, traffic_src = pmc_traffic(args, m["dominant"], precision)
+    roof = {"bound": "mfma", "kernel": m["dominant"], "achieved": round(ach, 2), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
+            "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+            "dense_equivalent_achieved": round(sum(t["fd"]) / len(durs) / avg_d / 1e12, 2),
+            "launches": len(durs), "avg_launch_us": round(avg_d * 1e6, 2),
+            "avg_launch_gflop": round(avg_f / 1e9, 3),
+            "share_of_step": round(sum(durs) / m["el"], 3)}
+    kernels = {k: {"launches": len(v["d"]), "avg_us": round(sum(v["d"]) / len(v["d"]) * 1e6, 1),
+                   "tflops": round(sum(v["f"]) / sum(v["d"]) / 1e12, 1),
+                   "gbps": round(sum(v["b"]) / sum(v["d"]) / 1e9, 1)}
+               for k, v in sorted(m["per"].items(), key=lambda kv: -sum(kv[1]["d"]))}
+    return roof, kernels
+
+
+def network_block(m, steps, B):
+    from drnmi.roofline import network_roofline
+    nr = network_roofline(m["plan"])
+    step_s = m["el"] / steps
+    return {"t_star_ms_per_frame": nr["t_star_fused_s"] / B * 1e3,
+            "t_star_per_layer_ms_per_frame": nr["t_star_s"] / B * 1e3,
+            "measured_ms_per_frame": step_s / B * 1e3,
+            "frac": nr["t_star_fused_s"] / step_s,
+            "frac_per_layer": nr["t_star_s"] / step_s,
+            "t_star_note": "frac = fused floor (the launches the plan issues, charged the bytes they move: "
+                           "drnmi/roofline.py launch_work); frac_per_layer charges every layer its unfused bytes",
+            "gflop_per_frame": nr["flops"] / B / 1e9, "gb_per_frame": nr["fused_bytes"] / B / 1e9,
+            "gb_per_frame_per_layer": nr["bytes"] / B / 1e9,
+            "achieved_tflops": nr["flops"] / step_s / 1e12}
+
+
+def main(argv=None):
+    args = parse(argv)
+    wr = resolve_world(args)
+    if wr is None:                            # --gpus N outside torchrun: spawn the ranks
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv))
+    world, rank, local = wr
+    if args.stub_step:
+        return stub_main(args, world, rank)
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from drnmi.drnseg import build
+
+    if args.prune:
+        model, n_pruned = pruned_model(args, dev)
+    else:
+        model = build(args.arch, 19, seed=0, device=dev,
+                      precision="bf16" if args.precision == "int8" else args.precision)
+    if args.precision == "int8":
+        model = calibrate(model, args, dev)
+    B, H, W = args.batch, args.height, args.width
+    g = torch.Generator(device=dev).manual_seed(frame_seed(rank))
+    frames = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
+    m = measure(args, model, frames, args.steps, args.warmup, world, dev, not args.no_kernel_events)
+    el, names, density = m["el"], m["names"], m["density"]
+    host = host_frames_run(args, model, m["step"], world, dev) if args.host_frames else None
+    per_rank = gather_ranks([frame_seed(rank), m["own"]], world, dev)
+
     total_frames = world * B * args.steps
     out = {
         "metric": METRIC,
@@ -345,6 +501,9 @@ def main():
                    "arch": args.arch, "height": H, "width": W, "frames_per_gpu_step": B,
                    "global_batch": B * world, "parallelism": f"dp{world} (frames sharded, no data-path collective)"},
     }
+    if world > 1:
+        out["per_rank"] = [{"rank": r, "frame_seed": int(v[0]), "frames": B * args.steps, "seconds": round(v[1], 6)}
+                           for r, v in enumerate(per_rank)]
     if args.prune:
         sparse = [i for i, nm in enumerate(names) if nm.startswith("conv_big_kernel") and nm.endswith("true>")]
         out["config"]["workload"] = out["config"]["workload"].replace("dense inference", f"{args.prune} pruned inference")
@@ -354,36 +513,35 @@ def main():
                                          "kernels": "K-step compaction" if args.block_sparse else "dense",
                                          "flops": "useful (dense x weight density); dense-equivalent in "
                                                   "roofline.dense_equivalent_achieved"}
-    traffic, traffic_src = pmc_traffic(args, dominant) if durs else (None, None)
-    if durs:
-        avg_d = sum(durs) / len(durs)
-        avg_f = sum(flops) / len(flops)
-        ach = avg_f / avg_d / 1e12
-        peak = kernel_peak(dominant, plan.packed.base) / 1e12
-        out["roofline"] = {"bound": "mfma", "kernel": dominant, "achieved": round(ach, 2), "peak": peak,
-                           "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
-                           "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                           "dense_equivalent_achieved": round(sum(per[dominant]["fd"]) / len(durs) / avg_d / 1e12, 2),
-                           "launches": len(durs), "avg_launch_us": round(avg_d * 1e6, 2),
-                           "avg_launch_gflop": round(avg_f / 1e9, 3),
-                           "share_of_step": round(sum(durs) / el, 3)}
+    roof, kernels = roofline_block(args, m, args.precision)
+    if roof is not None:
+        out["roofline"] = roof
         out["kernels_source"] = ("dominant kernel: HIP events around its launches in the timed region; "
                                  "the others: one fully instrumented step after it")
-        out["kernels"] = {k: {"launches": len(v["d"]), "avg_us": round(sum(v["d"]) / len(v["d"]) * 1e6, 1),
-                              "tflops": round(sum(v["f"]) / sum(v["d"]) / 1e12, 1),
-                              "gbps": round(sum(v["b"]) / sum(v["d"]) / 1e9, 1)}
-                          for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1]["d"]))}
-    out["network_roofline"] = {"t_star_ms_per_frame": nr["t_star_s"] / B * 1e3,
-                               "measured_ms_per_frame": el / args.steps / B * 1e3,
-                               "frac": nr["t_star_s"] / (el / args.steps),
-                               "gflop_per_frame": nr["flops"] / B / 1e9, "gb_per_frame": nr["bytes"] / B / 1e9,
-                               "achieved_tflops": nr["flops"] * args.steps / el / 1e12}
+        out["kernels"] = kernels
+    out["network_roofline"] = network_block(m, args.steps, B)
     if host is not None:
         out["host_frames"] = host
+    exact = None
+    if (world == 1 and args.precision == "bf16" and not args.prune and not args.no_exact_mode
+            and not args.no_kernel_events):
+        # exact-argmax mode (north star: labels bit-exact vs the reference): the fp32-accurate
+        # split-bf16 engine on the same weights and frames, timed in this process
+        xm = build(args.arch, 19, seed=0, device=dev, precision="fp32x")
+        mx = measure(args, xm, frames, args.exact_steps, 2, world, dev)
+        xroof, _ = roofline_block(args, mx, "fp32x")
+        exact = {"precision": "fp32x", "value": B * args.exact_steps / mx["el"], "unit": "frames/s",
+                 "steps": args.exact_steps, "warmup": 2, "ms_per_step": mx["el"] / args.exact_steps * 1e3,
+                 "roofline": xroof, "network_roofline": network_block(mx, args.exact_steps, B),
+                 "arithmetic": "fp32-accurate: exact 3-way bf16 split of weights and activations, the six "
+                               "products above 2^-24 on the bf16 MFMA, fp32 accumulation (peak 2.5 PF / 6)"}
+        out["exact_mode"] = exact
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], (bframes, blabels) = cpu_baseline(args, args.cpu_seconds)
         if not args.prune:                   # the oracle runs the unpruned synthetic weights
             out["parity_vs_ref"] = parity_vs_ref(args, model, bframes, blabels, dev)
+            if exact is not None:
+                exact["parity_vs_ref"] = parity_vs_ref(args, xm, bframes, blabels, dev, "fp32x")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -439,13 +597,13 @@ def host_frames_run(args, model, step, world, dev):
                     "headline: the headline times HBM-resident frames)"}
 
 
-def pmc_traffic(args, kernel):
+def pmc_traffic(args, kernel, precision=None):
     """HBM bytes per launch of `kernel` from the newest committed PMC capture of this exact
     workload (profiles/*_pmc_traffic.json, made by scripts/pmc_traffic.sh: FETCH_SIZE x 2 +
     WRITE_SIZE, MI355X_MICROARCH.md §HBM); PMC counters cannot be read inside the timed run."""
     import glob
     want = {"arch": args.arch, "height": args.height, "width": args.width, "frames_per_gpu_step": args.batch,
-            "precision": args.precision}
+            "precision": precision or args.precision}
     here = os.path.dirname(os.path.abspath(__file__))
     for f in sorted(glob.glob(os.path.join(here, "profiles", "*_pmc_traffic.json")), reverse=True):
         try:

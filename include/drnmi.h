@@ -88,7 +88,12 @@ typedef struct drnmi_conv_args {
    * [w | w2] (k = ks*ks*cin + cin2).  This folds a BasicBlock / Bottleneck 1x1 downsample
    * (lmodels/drn.py:181-186, its BN scale folded into w2, shifts summed) into the block's last
    * conv, so the residual branch is never written to HBM.  x2: NHWC [n][h2][w2][cin2], sampled at
-   * (oh*stride2, ow*stride2); cin2 % 64 == 0, res must be NULL.  x2 = NULL: unused.           */
+   * (oh*stride2, ow*stride2); res must be NULL.  x2 = NULL: unused.  Two accepted forms:
+   *   conv_big (cin >= 256 tiles): cin2 % 64 == 0 and k_pad == k;
+   *   conv_halo (stride-1 3x3 with cin = cout 64 or 128, layer3/layer4): cin2 == 32 or 64,
+   *     k_pad = round_up(k, 64) with zero columns after w2, scale == NULL (BN scales folded
+   *     into the weights, shifts summed in shift).  Other combinations return
+   *     DRNMI_ERR_UNSUPPORTED.                                                               */
   const void* x2;
   int32_t cin2, h2, w2, stride2;
 } drnmi_conv_args;

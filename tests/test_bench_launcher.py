@@ -1,0 +1,68 @@
+"""bench.py's multi-GPU launcher and rank logic on CPU (gloo), the GPU step stubbed
+(`--stub-step`): `--gpus N` spawns N ranks, each rank segments its own frame stream, the job
+time is the max over ranks, and a torchrun WORLD_SIZE that disagrees with --gpus is refused.
+Reference: seg_video_old_no_plot.py:157-166 (per-frame independent loop),
+semantic_seg_multigpu.py:467-468 (one process per GPU, init_process_group)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+
+SMALL = ["--stub-step", "--steps", "3", "--warmup", "1", "--batch", "2", "--height", "16", "--width", "32"]
+
+
+def _env():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["MASTER_ADDR"] = "127.0.0.1"
+    return env
+
+
+def test_resolve_world():
+    a1 = bench.parse(["--gpus", "1"])
+    a2 = bench.parse(["--gpus", "2"])
+    assert bench.resolve_world(a1, {}) == (1, 0, 0)
+    assert bench.resolve_world(a2, {}) is None                       # must spawn its ranks
+    assert bench.resolve_world(a2, {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"}) == (2, 1, 1)
+    with pytest.raises(SystemExit):
+        bench.resolve_world(a1, {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert bench.frame_seed(0) != bench.frame_seed(1)
+
+
+def test_gpus2_spawns_two_ranks():
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", *SMALL],
+                       capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1                                            # rank 0 prints ONE line
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    ranks = d["per_rank"]
+    assert [p["rank"] for p in ranks] == [0, 1]
+    assert ranks[0]["frame_seed"] != ranks[1]["frame_seed"]
+    assert ranks[0]["frame_sum"] != ranks[1]["frame_sum"]             # different frames per rank
+    job = max(p["seconds"] for p in ranks)
+    # value = frames of all ranks / the slowest rank's time (barriers make them nearly equal)
+    assert d["value"] == pytest.approx(2 * 2 * 3 / (d["ms_per_step"] * 3 / 1e3), rel=1e-6)
+    assert d["ms_per_step"] * 3 / 1e3 == pytest.approx(job, rel=1e-6)
+
+
+def test_world_mismatch_refused():
+    env = _env()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_PORT="29999")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", *SMALL],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_single_rank_stub():
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *SMALL],
+                       capture_output=True, text=True, timeout=120, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and len(d["per_rank"]) == 1

@@ -153,3 +153,22 @@ def test_bilinear_bwd_kernel_vs_autograd():
                                                       vp(out), ctypes.c_void_p(_lib.stream_ptr())), "bwd")
         torch.cuda.synchronize()
         np.testing.assert_allclose(out.cpu().numpy(), gref.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_deepcopy_dispatches_to_its_own_weights():
+    """a deepcopy with different weights gives different logits (and the original's
+    are unchanged)."""
+    import copy
+    from drnmi.drnseg import build
+    m = build("drn_d_22", 19, seed=0, device="cuda", precision="fp32")
+    x = torch.rand(1, 3, 64, 128, device="cuda")
+    _, l0 = m(x)
+    c = copy.deepcopy(m)
+    _, lc = c(x)
+    assert torch.equal(l0, lc)
+    with torch.no_grad():
+        c.seg.bias.add_(1.0)
+    _, lc2 = c(x)
+    _, l1 = m(x)
+    assert torch.equal(l1, l0)
+    assert torch.allclose(lc2, l0 + 1.0, atol=1e-5)

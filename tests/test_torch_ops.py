@@ -68,3 +68,36 @@ def test_use_torch_up_matches_reference_structure():
     assert isinstance(b.up, torch.nn.UpsamplingBilinear2d) and b.up.scale_factor == 8
     assert [p is q for p, q in zip(a.optim_parameters(), a.optim_parameters())]
     assert len(list(b.optim_parameters())) == len(list(a.optim_parameters()))
+
+
+def test_copies_get_their_own_handle():
+    """the op handle must follow the instance -- a deepcopy / unpickled DRNSeg
+    dispatches to ITS weights, never the original's."""
+    import copy
+    import pickle
+    m = DRNSeg("drn_d_22", 19, pretrained=False).eval()
+    for c in (copy.deepcopy(m), pickle.loads(pickle.dumps(m))):
+        assert c._handle != m._handle
+        assert torch_ops._model(c._handle) is c
+        assert torch_ops._model(m._handle) is m
+        assert c._graph.nodes[0].conv is c.layer[0][0]           # the lowered graph follows the copy
+        assert c._packed == {} and c._plans == {}
+
+
+def test_repack_key_sees_swapped_parameters():
+    m = DRNSeg("drn_d_22", 19, pretrained=False).eval()
+    k0 = m._state_key()
+    assert m._state_key() == k0
+    m.layer[0][0].weight = torch.nn.Parameter(torch.zeros_like(m.layer[0][0].weight))
+    k1 = m._state_key()
+    assert k1 != k0
+    with torch.no_grad():
+        m.seg.bias.add_(1.0)                                       # in-place: version bump
+    assert m._state_key() != k1
+
+
+def test_eval_unwraps_data_parallel():
+    from drnmi.evaluate import _unwrap
+    m = DRNSeg("drn_d_22", 19, pretrained=False)
+    wrapped = torch.nn.DataParallel(m)
+    assert _unwrap(wrapped) is m and _unwrap(m) is m

@@ -89,8 +89,25 @@ class DRNSeg(nn.Module):
         self._plans = {}
         self._pack_key = None
         self._key_tensors = None     # cached parameter/buffer list of the repack key
+        self._key_ids = None         # ids of the parameter/buffer/submodule objects it was built from
+        self._key_dicts = []         # the modules' _parameters/_buffers/_modules dicts behind them
         self.timing_hook = None      # optional per-launch callback (bench.py's HIP events)
         self._handle = torch_ops.register_model(self)   # torch.ops.drnmi.* state handle
+
+    # copies and unpickled modules register a handle of their own: the handle keys the
+    # torch.ops.drnmi.* state, and a copied integer would dispatch to the ORIGINAL model's
+    # weights.  Packed weights and launch plans hold device pointers of this instance: not copied.
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st.pop("_handle", None)
+        st.update(_packed={}, _plans={}, _pack_key=None, _key_tensors=None, _key_ids=None, _key_dicts=[],
+                  timing_hook=None)
+        st.pop("_train_runner", None)
+        return st
+
+    def __setstate__(self, st):
+        super().__setstate__(st)
+        self._handle = torch_ops.register_model(self)
 
     # ----------------------------------------------------------------- reference API
     def optim_parameters(self, memo=None):
@@ -266,11 +283,15 @@ class DRNSeg(nn.Module):
     def _state_key(self):
         """Repack key: every parameter/buffer's storage and version counter (an in-place update
         -- optimizer step, apply_masks, load_state_dict -- bumps the version).  The tensor list
-        is cached (walking the module tree cost ~0.6 ms per call); _apply / load_state_dict
-        reset it."""
+        is cached (building it cost ~0.6 ms per call); _apply / load_state_dict reset it, and a
+        Parameter or buffer swapped in anywhere in the tree (conv.weight = nn.Parameter(...))
+        changes the object ids checked here, which rebuilds it."""
         ts = self._key_tensors
-        if ts is None:
+        ids = tuple(id(v) for d in self._key_dicts for v in d.values()) if ts is not None else None
+        if ts is None or ids != self._key_ids:
             ts = self._key_tensors = list(self.parameters()) + list(self.buffers())
+            self._key_dicts = [d for mod in self.modules() for d in (mod._parameters, mod._buffers, mod._modules)]
+            self._key_ids = tuple(id(v) for d in self._key_dicts for v in d.values())
         return (self.precision, tuple((t.data_ptr(), t._version) for t in ts))
 
     def _prepare(self, n, h, w, device, keep_all=False):

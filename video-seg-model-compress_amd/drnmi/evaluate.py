@@ -38,9 +38,18 @@ def _miou_of(hist: torch.Tensor) -> float:
     return round(float(np.nanmean(ious)), 2)
 
 
+def _unwrap(model):
+    """The DRNSeg inside a DataParallel / DDP wrapper (semantic_seg.py:812 and :1074 hand the
+    wrapped model to val_miou; the multigpu script hands a DDP one)."""
+    while hasattr(model, "module") and not hasattr(model, "predict"):
+        model = model.module
+    return model
+
+
 def test(eval_data_loader, model, num_classes, has_gt=True, **_unused):
     """Single-scale eval loop: model(image)[0] -> torch.max(final, 1) -> fast_hist (on the GPU)."""
     model.eval()
+    model = _unwrap(model)
     dev = _device_of(model)
     hist = torch.zeros(num_classes, num_classes, dtype=torch.int64, device=dev)
     for it, batch in enumerate(eval_data_loader):
@@ -63,6 +72,7 @@ def test_ms(eval_data_loader, model, num_classes, scales, has_gt=True, **_unused
     loader's SegListMS items: image, label, name, *scaled images) are each resized to the input
     size and summed in fp32 in the reference's order, then argmax(axis=1) and fast_hist."""
     model.eval()
+    model = _unwrap(model)
     dev = _device_of(model)
     hist = torch.zeros(num_classes, num_classes, dtype=torch.int64, device=dev)
     num_scales = len(scales)

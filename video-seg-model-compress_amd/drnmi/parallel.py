@@ -57,6 +57,12 @@ class BucketReducer:
             self.bucket_of[i] = b
 
     def reset(self):
+        """Start a step with no bucket launched.  A bucket collective still in flight (a backward
+        that raised part-way left it launched) is waited for first, so it cannot keep writing into
+        the flat gradient buffer while the next backward fills it."""
+        for h in getattr(self, "handles", ()):
+            if h is not None:
+                h.wait()
         self.pending = [set(ids) for _, _, ids in self.buckets]
         self.handles = [None] * len(self.buckets)
         self.launch_order = []
@@ -80,6 +86,7 @@ class BucketReducer:
                 h = dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
                 self.launch_order.append(b)
             h.wait()
+            self.handles[b] = None
         self.reset()
 
 
@@ -123,7 +130,9 @@ class DistributedDataParallel(nn.Module):
 
     def forward(self, *args, **kwargs):
         # a backward that raised part-way never ran _finalize: start every step from a clean
-        # reducer so no bucket stays 'launched' and the ranks cannot silently diverge
+        # reducer (reset waits for any bucket collective still in flight).  This keeps the local
+        # buffers consistent; it cannot repair a rank that skipped collectives its peers issued --
+        # such a job hangs in the peers' next collective, as torch DDP does
         self._queued = False
         if self._reducer is not None:
             self._reducer.reset()

@@ -63,14 +63,51 @@ def node_peaks(plan):
             for nd in pk.graph.nodes] + [base]
 
 
-def network_roofline(plan):
+def launch_work(plan, video: bool = True):
+    """node_work re-cut along the launches the plan really issues (rows stay index-aligned
+    with plan.args; an absorbed node's row becomes (name, 0, 0)):
+      * a 1x1 downsample folded into its block's last conv (plan.skip, lmodels/drn.py:181-186):
+        its FLOPs and its input + weight bytes move into that launch, and the residual tensor
+        is neither written by the downsample nor read by the conv;
+      * the fused stem + layer1 launch (plan.stem_fused, drn.py:132-137 + :201-211; video=True:
+        the uint8-frame segment() path): the 16-channel stem output is neither written nor read
+        back."""
+    rows = list(node_work(plan))
+    nodes = plan.packed.graph.nodes
+    esz = 2 if plan.packed.base == "bf16" else 4
+    for i in sorted(getattr(plan, "skip", ())):
+        j = nodes[i].fused_into
+        n_, fj, bj = rows[j]
+        oh, ow = plan.shapes[nodes[j].dst]
+        res_b = plan.n * oh * ow * nodes[j].conv.out_channels * (1 if nodes[j].i8 else esz)
+        fi, bi = rows[i][1], rows[i][2]
+        rows[j] = (n_, fj + fi, bj - res_b + (bi - res_b))
+        rows[i] = (rows[i][0], 0.0, 0.0)
+    if video and getattr(plan, "stem_fused", False):
+        h0, w0 = plan.shapes[nodes[0].dst]
+        mid = plan.n * h0 * w0 * nodes[0].conv.out_channels * esz
+        rows[0] = (rows[0][0], rows[0][1] + rows[1][1], rows[0][2] + rows[1][2] - 2 * mid)
+        rows[1] = (rows[1][0], 0.0, 0.0)
+    return rows
+
+
+def _t_star(rows, peaks):
+    return sum(max(f / pk_, b / HBM_PEAK_BPS) for (_, f, b), pk_ in zip(rows, peaks))
+
+
+def network_roofline(plan, video: bool = True):
+    """T* two ways: per layer (every conv charged its unfused bytes) and the fused floor (the
+    launches the plan issues, charged the bytes they move: launch_work).  The fused floor is the
+    smaller, honest bound; bench.py reports frac against it."""
     rows = node_work(plan)
     peaks = node_peaks(plan)
-    t_star = sum(max(f / pk_, b / HBM_PEAK_BPS) for (_, f, b), pk_ in zip(rows, peaks))
+    fused = launch_work(plan, video)
     return {
         "flops": sum(f for _, f, _ in rows),
         "bytes": sum(b for _, _, b in rows),
-        "t_star_s": t_star,
+        "fused_bytes": sum(b for _, _, b in fused),
+        "t_star_s": _t_star(rows, peaks),
+        "t_star_fused_s": _t_star(fused, peaks),
         "t_mfma_s": sum(f / pk_ for (_, f, _), pk_ in zip(rows, peaks)),
         "t_hbm_s": sum(b for _, _, b in rows) / HBM_PEAK_BPS,
     }
