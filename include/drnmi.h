@@ -93,7 +93,7 @@ typedef struct drnmi_conv_args {
    *   conv_halo (stride-1 3x3 with cin = cout 64 or 128, layer3/layer4): cin2 == 32 or 64,
    *     k_pad = round_up(k, 64) with zero columns after w2, scale == NULL (BN scales folded
    *     into the weights, shifts summed in shift).  Other combinations return
-   *     DRNMI_ERR_UNSUPPORTED.                                                               */
+   *     DRNMI_ENOTSUP.                                                                       */
   const void* x2;
   int32_t cin2, h2, w2, stride2;
 } drnmi_conv_args;
