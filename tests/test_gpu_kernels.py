@@ -343,6 +343,34 @@ def test_strip_kernel_bit_identical(n, h, w, cin, cout, dil, with_res, fold):
     assert (b.float().permute(0, 3, 1, 2).cpu() - ref).abs().max().item() <= 1.5e-2 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout,dil,with_res,fold", [
+    (2, 9, 256, 256, 256, 2, True, True), (1, 5, 512, 512, 512, 4, True, True),
+    (2, 6, 256, 128, 256, 2, False, True), (1, 4, 256, 512, 512, 1, False, False),
+    (1, 2, 768, 256, 512, 1, True, True), (1, 3, 256, 128, 256, 3, True, False)])
+def test_stag_kernel_bit_identical(n, h, w, cin, cout, dil, with_res, fold):
+    """conv_stag_kernel (tile 19: the strip tile with waves 4-7 half a K step behind their SIMD
+    partners, two barriers per step) == conv_strip_kernel (tile 18) bit for bit: same K order,
+    same MFMA order per accumulator, same epilogue.  Borders and dil 1..4 as in the strip test."""
+    g = torch.Generator().manual_seed(190 + h * w + cin)
+    x = torch.randn(n, h, w, cin, generator=g).bfloat16().to(DEV)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (9 * cout)) ** 0.5).to(DEV)
+    sc = (torch.rand(cout, generator=g) + 0.5).to(DEV)
+    sh = (torch.rand(cout, generator=g) - 0.5).to(DEV)
+    res = torch.randn(n, h, w, cout, generator=g).bfloat16().to(DEV) if with_res else None
+    kw = dict(stride=1, padding=dil, dilation=dil, relu=True, fold_scale=fold)
+    a = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=18, **kw)
+    b = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=19, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
+def test_stag_kernel_refuses_cin_not_multiple_of_128():
+    x = torch.randn(1, 4, 256, 64, device=DEV).bfloat16()
+    wt = torch.randn(256, 64, 3, 3, device=DEV) * 0.02
+    with pytest.raises(RuntimeError, match="ENOTSUP"):
+        ops.conv2d_bn_act(x, wt, padding=1, dilation=1, tile=19)
+
+
 def test_strip_kernel_refuses_unaligned_rows():
     x = torch.randn(1, 4, 200, 256, device=DEV).bfloat16()
     wt = torch.randn(256, 256, 3, 3, device=DEV) * 0.02
@@ -444,6 +472,8 @@ def test_conv_x6_fp32_accuracy(case):
     (2, 33, 70, 64, 64, 3, 1, 32, 2, 66, 140),       # layer3.0: halo conv2 + 1x1 s2 downsample 32 -> 64
     (1, 20, 40, 128, 128, 3, 1, 64, 2, 40, 80),      # layer4.0: halo conv2 + 1x1 s2 downsample 64 -> 128
     (3, 7, 130, 64, 64, 3, 1, 32, 2, 13, 259),       # ragged blocks, odd x2 extent
+    (2, 5, 256, 256, 256, 3, 2, 128, 1, 5, 256),     # layer5.0 on whole 256-pixel rows: conv_stag_x2_kernel
+    (1, 4, 512, 512, 512, 3, 4, 256, 1, 4, 512),     # layer6.0 on whole rows: conv_stag_x2_kernel
 ])
 def test_conv_fused_downsample(case):
     """drnmi_conv_args.x2: y = relu(conv(x, w) + conv1x1_s(x2, w2) + shift) as one launch (the
@@ -480,12 +510,20 @@ def test_conv_fused_downsample(case):
     a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_BF16, _lib.DRNMI_BF16, -1, _lib.ALGO_IGEMM
     a.x2, a.cin2, a.h2, a.w2, a.stride2 = x2d.data_ptr(), cin2, h2, w2, s2
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
-    assert name.startswith("conv_halo_kernel" if halo else "conv_big_kernel"), name
+    stag = ks == 3 and wo % 256 == 0 and cin % 128 == 0 and not halo
+    assert name.startswith("conv_halo_kernel" if halo else "conv_stag_x2_kernel" if stag else "conv_big_kernel"), name
     _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds")
     torch.cuda.synchronize()
     err = (y.float().cpu() - ref).abs().max().item()
     print(f"{name} {case}: max-abs {err:.3e} (|y| {ref.abs().max().item():.2f})")
     assert err <= 0.02 * max(1.0, ref.abs().max().item())
+    if stag:                              # == conv_big's X2 form of the same 256 x 256 tile (tile 5)
+        yb = torch.empty_like(y)
+        a.y, a.tile = yb.data_ptr(), 5
+        _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds big")
+        torch.cuda.synchronize()
+        assert torch.equal(yb, y)
+        a.y, a.tile = y.data_ptr(), -1
     if halo and kp == k1 + cin2:          # conv_big takes it too (tile 4: the 128 x 256 X2 form)
         yb = torch.empty_like(y)
         a.y, a.tile = yb.data_ptr(), 4

@@ -263,6 +263,7 @@ constexpr TileDesc kTiles[] = {
     {256, 256, "pp256"},                                   // ping-pong 4-phase schedule
     {128, 128, "halo"},                                    // conv_halo.hip, 4x64 pixel block
     {256, 256, "strip256"},                                // conv_big.hip, strip-staged B (3x3, wo % 256 == 0)
+    {256, 256, "stag256"},                                 // the strip tile, SIMD partners half a K step apart
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
