@@ -8,6 +8,6 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$1; shift
 mkdir -p $OUT
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES \
-  --output-format csv -d $OUT/clk -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" \
+  --output-format csv -d $OUT/clk -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-exact-mode "$@" \
   > $OUT/clk.log 2>&1) || { echo "pmc pass failed"; tail -5 $OUT/clk.log; exit 1; }
 python3 $R/scripts/pmc_clock.py $OUT/clk > $OUT/clock.json && cat $OUT/clock.json

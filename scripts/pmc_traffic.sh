@@ -9,6 +9,6 @@ OUT=$R/gpurun_out/$1; shift
 mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
   (cd /tmp && timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o run -- \
-    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $OUT/$c.log 2>&1) || { echo "pass $c failed"; exit 1; }
+    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-exact-mode "$@" > $OUT/$c.log 2>&1) || { echo "pass $c failed"; exit 1; }
 done
 python3 $R/scripts/pmc_traffic.py $OUT > $OUT/traffic.json && cat $OUT/traffic.json

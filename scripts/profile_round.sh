@@ -10,9 +10,9 @@ timeout -k 10 500 python -u -m pytest $R/tests -x -q -m gpu --timeout 120 --time
 rc=$?; echo "pytest rc=$rc" >> $OUT/pytest_gpu.log; tail -3 $OUT/pytest_gpu.log
 [ $rc -ne 0 ] && exit $rc
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_bf16 -o run --output-format csv -- \
-  python3 $R/bench.py --no-cpu-baseline > $OUT/bench_bf16_under_rocprof.log 2>&1) || { echo "trace bf16 failed"; exit 1; }
+  python3 $R/bench.py --no-cpu-baseline --no-exact-mode > $OUT/bench_bf16_under_rocprof.log 2>&1) || { echo "trace bf16 failed"; exit 1; }
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_int8 -o run --output-format csv -- \
-  python3 $R/bench.py --no-cpu-baseline --precision int8 > $OUT/bench_int8_under_rocprof.log 2>&1) || { echo "trace int8 failed"; exit 1; }
+  python3 $R/bench.py --no-cpu-baseline --no-exact-mode --precision int8 > $OUT/bench_int8_under_rocprof.log 2>&1) || { echo "trace int8 failed"; exit 1; }
 bash $R/scripts/pmc_traffic.sh $1/pmc_bf16 > /dev/null || exit 1
 bash $R/scripts/pmc_traffic.sh $1/pmc_int8 --precision int8 > /dev/null || exit 1
 echo done

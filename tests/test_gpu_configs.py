@@ -97,7 +97,8 @@ def test_headline_1024x2048_exact_modes_vs_oracle(precision):
         assert int(diff.sum()) <= 4 and not np.any(diff & (margin > 1e-5))
 
 
-def test_c4_d54_rmb75_finetune_step(golden_masks):
+@pytest.mark.parametrize("precision", ["fp32", "fp32x"])
+def test_c4_d54_rmb75_finetune_step(golden_masks, precision):
     from drnmi.drnseg import DRNSeg
     from drnmi.pruners import RmbPruner
     from drnmi.train import SGD, CrossEntropyLoss
@@ -118,7 +119,7 @@ def test_c4_d54_rmb75_finetune_step(golden_masks):
     t[torch.rand(t.shape, generator=g) < 0.2] = 255
     losses, g64, f64 = O.drnseg_train_steps(m.state_dict(), "drn_d_54", [x], [t], TC.LR, TC.MOMENTUM, TC.WD,
                                             masks=masks, dtype=torch.float64)
-    m = m.to(DEV).train()
+    m = m.to(DEV).train().set_precision(precision)
     for k in list(pr.mask_dict):
         pr.mask_dict[k] = pr.mask_dict[k].to(DEV)
     pr.on_gpu = True
@@ -147,7 +148,7 @@ def test_c4_d54_rmb75_finetune_step(golden_masks):
         w = m.state_dict()[k]
         assert torch.all(w[mk == 0] == 0), k
         assert abs(1 - int((w != 0).sum()) / w.numel() - 0.75) <= 0.01, k
-    print(f"C4 D-54 + RMB 75 % step: loss {float(loss):.6f} (fp64 {losses[0]:.6f}), grads rel-L2 vs fp64 "
+    print(f"C4 D-54 + RMB 75 % step ({precision}): loss {float(loss):.6f} (fp64 {losses[0]:.6f}), grads rel-L2 vs fp64 "
           f"{worst:.2e}, params after the step {worst_p:.2e}")
 
 

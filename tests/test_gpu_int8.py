@@ -58,9 +58,12 @@ CONV_CASES = [
     (1, 12, 20, 512, 512, 3, 1, 4, 4, False, "bf16"),   # dilation 4, bf16 out
     (1, 10, 10, 512, 19, 1, 1, 0, 1, False, "f32"),     # seg head: cout 19, fp32 NCHW logits
     (1, 8, 8, 256, 256, 3, 1, 1, 1, True, "f32"),
-    # whole 256-pixel output rows: the strip-staged int8 kernel (conv_i8_strip_kernel)
+    # whole 256-pixel output rows: the strip-staged int8 kernels (cin % 256 == 0: the staggered
+    # conv_i8_stag_kernel; cin 128: conv_i8_strip_kernel)
     (1, 5, 256, 256, 256, 3, 1, 2, 2, True, "i8"),
     (2, 3, 512, 128, 256, 3, 1, 4, 4, False, "bf16"),
+    (1, 4, 512, 512, 512, 3, 1, 4, 4, True, "i8"),
+    (2, 3, 256, 256, 512, 3, 1, 1, 1, False, "bf16"),
 ]
 
 
@@ -103,8 +106,9 @@ def test_conv_i8_matches_oracle(case):
     a.dtype, a.tile, a.algo = L.DRNMI_I8, -1, L.ALGO_IGEMM
     a.res_scale, a.out_scale = res_scale, out_scale
     name = lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
-    assert name.startswith("conv_i8_strip_kernel" if wo % 256 == 0 and ks == 3 and st == 1 and cin >= 128
-                           and cout % 256 == 0 else "conv_i8_kernel<"), name
+    strip = wo % 256 == 0 and ks == 3 and st == 1 and cin >= 128 and cout % 256 == 0
+    assert name.startswith(("conv_i8_stag_kernel" if cin % 256 == 0 else "conv_i8_strip_kernel") if strip
+                           else "conv_i8_kernel<"), name
     L.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), _stream()), "conv i8")
     torch.cuda.synchronize()
     ref = Q.conv_i8(x, wpk, scale, shift, cout, ks, st, pad, dil, bool(a.relu), res, res_scale,

@@ -903,10 +903,20 @@ hipError_t launch_i8_strip(const drnmi_conv_args& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// int8 staggered strip tile (conv_stag.hip): 128-channel K steps, so cin % 256 == 0 gives the
+// even number of 3-step tap groups the kernel walks in pairs
+bool i8_stag_ok(const drnmi_conv_args& p) {
+  return i8_strip_ok(p) && stag_enabled() && p.cin % 256 == 0 && p.x2 == nullptr;
+}
+
 int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!i8_conv_supported(p)) return DRNMI_ENOTSUP;
   const int v = i8_variant(p);
   if ((p.cout + kI8Variants[v].bco - 1) / kI8Variants[v].bco * kI8Variants[v].bco > p.cout_pad) return DRNMI_EINVAL;
+  if (p.ks == 3 && i8_stag_ok(p)) {
+    const hipError_t e = launch_stag(p, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
   if (p.ks == 3 && i8_strip_ok(p)) {
     const hipError_t e = launch_i8_strip(p, s);
     return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
@@ -918,6 +928,7 @@ int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
 const char* i8_conv_name(const drnmi_conv_args& p) {
   if (!i8_conv_supported(p)) return nullptr;
   const int v = i8_variant(p);
+  if (p.ks == 3 && i8_stag_ok(p)) return "conv_i8_stag_kernel";
   if (p.ks == 3 && i8_strip_ok(p)) return "conv_i8_strip_kernel";
   return p.ks == 3 ? kI8Variants[v].name3 : kI8Variants[v].name1;
 }

@@ -340,6 +340,13 @@ conv_stag_kernel(const drnmi_conv_args p) {
   conv_stag_body<uint16_t, false>(p);
 }
 
+// W8A8 (config C5): int8 rows of 128 channels are 128 B, the bf16 layout; v_mfma_i32_16x16x64_i8,
+// store_tile_i8 epilogue (bit-exact against oracle/int8_oracle.py like conv_i8_strip_kernel)
+__global__ void __launch_bounds__(512, 1)
+conv_i8_stag_kernel(const drnmi_conv_args p) {
+  conv_stag_body<int8_t, false>(p);
+}
+
 // + the fused 1x1 downsample (x2 != NULL; layer5.0 / layer6.0 conv2 of D-22)
 __global__ void __launch_bounds__(512, 1)
 conv_stag_x2_kernel(const drnmi_conv_args p) {
@@ -353,7 +360,8 @@ constexpr int kStagLds = 2 * 256 * 128 + 2 * kStripBytes;   // 2 A stages + 2 st
 hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void* f : {reinterpret_cast<const void*>(&conv_stag_kernel), reinterpret_cast<const void*>(&conv_stag_x2_kernel)}) {
+    for (const void* f : {reinterpret_cast<const void*>(&conv_stag_kernel), reinterpret_cast<const void*>(&conv_stag_x2_kernel),
+                          reinterpret_cast<const void*>(&conv_i8_stag_kernel)}) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kStagLds);
       if (e != hipSuccess) return e;
     }
@@ -361,7 +369,9 @@ hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s) {
   }
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const int64_t blocks = (M / kBPX) * ((p.cout + 255) / 256);
-  if (p.x2 != nullptr)
+  if (p.dtype == DRNMI_I8)
+    hipLaunchKernelGGL(conv_i8_stag_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), kStagLds, s, p);
+  else if (p.x2 != nullptr)
     hipLaunchKernelGGL(conv_stag_x2_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), kStagLds, s, p);
   else
     hipLaunchKernelGGL(conv_stag_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), kStagLds, s, p);

@@ -121,8 +121,9 @@ class DRNSeg(nn.Module):
             # fine-tune path: batch-stat BN + autograd through the HIP backward kernels
             if x.device.type != "cuda":
                 raise RuntimeError("drnmi.DRNSeg runs on the HIP engine only (no CPU fallback by design)")
-            if self.precision != "fp32":
-                raise NotImplementedError("the fine-tune path runs in fp32 (the reference's arithmetic)")
+            if self.precision not in ("fp32", "fp32x"):
+                raise NotImplementedError("the fine-tune path runs in fp32 (the reference's arithmetic) or fp32x "
+                                          "(fp32-accurate split-bf16 forward/dgrad convs)")
             from .train import train_forward
             return train_forward(self, x)
         if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] != 3:

@@ -18,8 +18,13 @@ bucketed RCCL all-reduce of finished buckets while earlier layers are still in b
 `CrossEntropyLoss` and `SGD` below are the HIP drop-ins for the criterion and optimizer (the
 optimizer can fuse the pruner's mask into the update: `SGD(..., pruner=p)`).
 
-Precision: fp32 throughout (the reference trains in fp32); activations NHWC with a power-of-two
-channel stride, like the inference engine.  There is no CPU or ATen fallback.
+Precision: fp32 (the reference trains in fp32; model.set_precision("fp32"), the default) or
+"fp32x": the forward and data-gradient convs with >= 32 input channels run on the fp32-accurate
+split-bf16 kernel (csrc/conv_x6.hip: exact 3-way bf16 split of weights and activations, the six
+products above 2^-24, fp32 accumulation, 2.5 PF / 6 peak) instead of the exact-f32 MFMA
+(157 TF); weight gradients, BN, the head and the small-channel convs stay exact fp32.
+Activations NHWC with a power-of-two channel stride, like the inference engine.  There is no
+CPU or ATen fallback.
 """
 from __future__ import annotations
 
@@ -40,10 +45,10 @@ def _vp(t):
 class _NodeState:
     """Per-node packed weights (forward / dgrad layouts) cached across steps."""
 
-    __slots__ = ("wf", "wd", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift")
+    __slots__ = ("wf", "wd", "wfx", "wdx", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift")
 
     def __init__(self):
-        self.wf = self.wd = self.shift = None
+        self.wf = self.wd = self.wfx = self.wdx = self.shift = None
 
 
 class TrainRunner:
@@ -130,6 +135,7 @@ class TrainRunner:
             raise RuntimeError(f"{nd.name}: expected a contiguous fp32 weight")
         _lib.check(lib.drnmi_pack_conv_weight(_vp(w), cout, cin, ks, cs, st.cout_pad, st.k_pad, 0, None, F32,
                                               _vp(st.wf), stream), f"pack {nd.name}")
+        st.wfx = self._split(st.wf, cs, st.k, st.k_pad)
         if conv.bias is not None:
             st.shift[:cout].copy_(conv.bias.detach())
 
@@ -144,12 +150,21 @@ class TrainRunner:
             st.wd = torch.empty(st.rows_d, st.kd_pad, dtype=torch.float32, device=device)
         _lib.check(lib.drnmi_pack_conv_weight(_vp(nd.conv.weight.detach()), cout, cin, ks, dys, st.rows_d,
                                               st.kd_pad, 1, None, F32, _vp(st.wd), stream), f"pack dgrad {nd.name}")
+        st.wdx = self._split(st.wd, dys, st.kd, st.kd_pad)
         return dys
 
+    def _split(self, wpk, cin_stride, k, k_pad):
+        """fp32x: the three bf16 planes of a packed fp32 weight, for the convs conv_x6 takes
+        (>= 32 input channels, k == k_pad); None keeps the launch on the exact-f32 kernel."""
+        if self.model.precision != "fp32x" or cin_stride < 32 or k != k_pad:
+            return None
+        from .engine import split3_bf16
+        return split3_bf16(wpk)
+
     def _conv(self, x, cin_stride, h, w, wpk, k, k_pad, cout_pad, cout, ks, stride, pad, dil, y, y_strides,
-              shift, res, n, ho, wo, stream, what):
+              shift, res, n, ho, wo, stream, what, wx=None):
         a = _lib.ConvArgs()
-        a.x, a.wgt, a.scale, a.shift = x.data_ptr(), wpk.data_ptr(), None, shift.data_ptr()
+        a.x, a.wgt, a.scale, a.shift = x.data_ptr(), (wx if wx is not None else wpk).data_ptr(), None, shift.data_ptr()
         a.res = res.data_ptr() if res is not None else None
         a.y = y.data_ptr()
         a.y_sn, a.y_sp, a.y_sc = y_strides
@@ -159,6 +174,8 @@ class TrainRunner:
         a.k, a.k_pad = k, k_pad
         a.relu = 0
         a.dtype = a.out_dtype = F32
+        if wx is not None:
+            a.dtype = _lib.DRNMI_F32X3           # fp32x: conv_x6 (fp32 in/out, bf16 weight planes)
         a.tile, a.algo = -1, _lib.ALGO_IGEMM
         _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), what)
 
@@ -189,7 +206,7 @@ class TrainRunner:
             if nd.out_fp32_nchw:        # seg 1x1 + bias -> fp32 NCHW logits
                 logits = torch.empty(n, cout, oh, ow, dtype=torch.float32, device=dev)
                 self._conv(vals[nd.src], cs_in, ih, iw, st.wf, st.k, st.k_pad, st.cout_pad, cout, ks, s, p, d,
-                           logits, (cout * oh * ow, 1, oh * ow), st.shift, None, n, oh, ow, stream, nd.name)
+                           logits, (cout * oh * ow, 1, oh * ow), st.shift, None, n, oh, ow, stream, nd.name, st.wfx)
                 vals[nd.dst] = logits
                 per_node.append(None)
                 continue
@@ -199,7 +216,7 @@ class TrainRunner:
             rows = n * oh * ow
             y = torch.empty(rows, cs, dtype=torch.float32, device=dev)
             self._conv(vals[nd.src], cs_in, ih, iw, st.wf, st.k, st.k_pad, st.cout_pad, cout, ks, s, p, d,
-                       y, (oh * ow * cs, cs, 1), st.shift, None, n, oh, ow, stream, nd.name)
+                       y, (oh * ow * cs, cs, 1), st.shift, None, n, oh, ow, stream, nd.name, st.wfx)
             bn = nd.bn
             if bn.momentum is None or not bn.track_running_stats:
                 raise NotImplementedError("BatchNorm2d with momentum=None / no running stats")
@@ -343,7 +360,7 @@ class TrainRunner:
                 out = prev if prev is not None else torch.empty(n * ih * iw, cs_src, dtype=torch.float32, device=dev)
                 self._conv(src, dys, hu, wu, st.wd, st.kd, st.kd_pad, st.rows_d, cin, ks, 1, pad_d, d, out,
                            (ih * iw * cs_src, cs_src, 1), self._zeros_f32(st.rows_d, dev), prev, n, ih, iw,
-                           stream, f"dgrad {nd.name}")
+                           stream, f"dgrad {nd.name}", st.wdx)
                 grads[nd.src] = out
             del dy
 
