@@ -364,6 +364,27 @@ def test_stag_kernel_bit_identical(n, h, w, cin, cout, dil, with_res, fold):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n,h,w,dil,with_res", [(2, 5, 256, 1, True), (1, 4, 512, 1, False), (1, 6, 256, 2, True)])
+def test_stag128_matches_halo_bit_identical(n, h, w, dil, with_res):
+    """128 -> 128 3x3 (D-22 layer4) on the staggered 128-channel tile (conv_stag128_kernel, tile
+    19) == the halo kernel (tile 17): same (channel block, tap) K order, same substep order, same
+    accumulator start (shift + residual), so the same bits."""
+    g = torch.Generator().manual_seed(290 + h * w)
+    x = torch.randn(n, h, w, 128, generator=g).bfloat16().to(DEV)
+    wt = (torch.randn(128, 128, 3, 3, generator=g) * (2.0 / (9 * 128)) ** 0.5).to(DEV)
+    sc = (torch.rand(128, generator=g) + 0.5).to(DEV)
+    sh = (torch.rand(128, generator=g) - 0.5).to(DEV)
+    res = torch.randn(n, h, w, 128, generator=g).bfloat16().to(DEV) if with_res else None
+    kw = dict(stride=1, padding=dil, dilation=dil, relu=True, fold_scale=True)
+    # the halo kernel's patch does not fit LDS at dil 2 with 128 channels: conv_big's 128 x 256
+    # tile (tile 4, same K order and accumulator start) is the reference there
+    a = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=17 if dil == 1 else 4, **kw)
+    b = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=19, **kw)
+    auto = ops.conv2d_bn_act(x, wt, sc, sh, res, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(auto, b)
+
+
 def test_stag_kernel_refuses_cin_not_multiple_of_128():
     x = torch.randn(1, 4, 256, 64, device=DEV).bfloat16()
     wt = torch.randn(256, 64, 3, 3, device=DEV) * 0.02
@@ -473,6 +494,7 @@ def test_conv_x6_fp32_accuracy(case):
     (1, 20, 40, 128, 128, 3, 1, 64, 2, 40, 80),      # layer4.0: halo conv2 + 1x1 s2 downsample 64 -> 128
     (3, 7, 130, 64, 64, 3, 1, 32, 2, 13, 259),       # ragged blocks, odd x2 extent
     (2, 5, 256, 256, 256, 3, 2, 128, 1, 5, 256),     # layer5.0 on whole 256-pixel rows: conv_stag_x2_kernel
+    (2, 4, 256, 128, 128, 3, 1, 64, 2, 8, 512),      # layer4.0 on whole rows: conv_stag128_x2_kernel (vs halo)
     (1, 4, 512, 512, 512, 3, 4, 256, 1, 4, 512),     # layer6.0 on whole rows: conv_stag_x2_kernel
 ])
 def test_conv_fused_downsample(case):
@@ -510,16 +532,17 @@ def test_conv_fused_downsample(case):
     a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_BF16, _lib.DRNMI_BF16, -1, _lib.ALGO_IGEMM
     a.x2, a.cin2, a.h2, a.w2, a.stride2 = x2d.data_ptr(), cin2, h2, w2, s2
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
-    stag = ks == 3 and wo % 256 == 0 and cin % 128 == 0 and not halo
-    assert name.startswith("conv_halo_kernel" if halo else "conv_stag_x2_kernel" if stag else "conv_big_kernel"), name
+    stag = ks == 3 and wo % 256 == 0 and cin % 128 == 0 and kp == k1 + cin2
+    assert name.startswith("conv_stag128_x2_kernel" if stag and cout <= 128 else "conv_stag_x2_kernel" if stag
+                           else "conv_halo_kernel" if halo else "conv_big_kernel"), name
     _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds")
     torch.cuda.synchronize()
     err = (y.float().cpu() - ref).abs().max().item()
     print(f"{name} {case}: max-abs {err:.3e} (|y| {ref.abs().max().item():.2f})")
     assert err <= 0.02 * max(1.0, ref.abs().max().item())
-    if stag:                              # == conv_big's X2 form of the same 256 x 256 tile (tile 5)
+    if stag:                              # == conv_big's X2 form of the same 256 x 256 tile (tile 5) / the halo kernel
         yb = torch.empty_like(y)
-        a.y, a.tile = yb.data_ptr(), 5
+        a.y, a.tile = yb.data_ptr(), 17 if halo else 5
         _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds big")
         torch.cuda.synchronize()
         assert torch.equal(yb, y)

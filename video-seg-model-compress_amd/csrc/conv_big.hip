@@ -702,9 +702,21 @@ bool strip_ok(const drnmi_conv_args& p) {
 // the staggered strip tile (conv_stag.hip): strip geometry, cin % 128 == 0 (an even number of
 // 3-step tap groups), optionally with the fused downsample (x2 validated by x2_ok)
 bool stag_ok(const drnmi_conv_args& p) {
+  const int tco = p.cout <= 128 ? 128 : 256;          // conv_stag128_* / conv_stag_* tile
   return p.ks == 3 && p.stride == 1 && p.pad == p.dil && p.dil >= 1 && p.dil <= 4 && p.wo % kBPX == 0 &&
-         p.unit_mask == nullptr && p.cin % 128 == 0 &&
+         p.unit_mask == nullptr && p.cin % 128 == 0 && (p.cout + tco - 1) / tco * tco <= p.cout_pad &&
          (p.x2 == nullptr ? p.k == 9 * p.cin : (p.cin2 % 64 == 0 && p.k == 9 * p.cin + p.cin2));
+}
+
+// 128-channel convs (D-22 layer4) go to the staggered 128-channel tile instead of the halo
+// kernel when both apply; DRNMI_HALO=1 keeps them on conv_halo_kernel (A/B runs)
+bool halo_preferred(const drnmi_conv_args& p) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("DRNMI_HALO");
+    on = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  return on == 1 || !(stag_enabled() && strip_enabled() && big_conv_supported(p) && stag_ok(p));
 }
 
 struct Variant {
@@ -952,17 +964,17 @@ bool big_conv_supported(const drnmi_conv_args& p) {
 
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   // the halo kernel (cin/cout 64-128) stays dense: it beats unit skipping on those shapes
-  if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_dispatch(p, s);
+  if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_dispatch(p, s);
   if (!big_conv_supported(p)) return DRNMI_ENOTSUP;
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
-  if (auto_pick && variant == 1 && strip_enabled()) {
+  if (auto_pick && strip_enabled()) {
     if (stag_enabled() && stag_ok(p)) variant = kStag;
-    else if (strip_ok(p)) variant = kStrip;
+    else if (variant == 1 && strip_ok(p)) variant = kStrip;
   }
   if (variant == kStrip || variant == kStag) {
     if (variant == kStag ? !stag_ok(p) : (!strip_ok(p) || p.cin < 64)) return DRNMI_ENOTSUP;
-    if ((p.cout + 255) / 256 * 256 > p.cout_pad) return DRNMI_EINVAL;
+    if (variant == kStrip && (p.cout + 255) / 256 * 256 > p.cout_pad) return DRNMI_EINVAL;
     const hipError_t e = variant == kStag ? launch_stag(p, s) : launch_strip(p, s);
     return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
   }
@@ -997,14 +1009,18 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 }
 
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
-  if (variant == kHalo || (variant < 0 && halo_conv_supported(p))) return halo_conv_name(p);
+  if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_name(p);
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
-  if (auto_pick && variant == 1 && strip_enabled()) {
+  if (auto_pick && strip_enabled()) {
     if (stag_enabled() && stag_ok(p)) variant = kStag;
-    else if (strip_ok(p)) variant = kStrip;
+    else if (variant == 1 && strip_ok(p)) variant = kStrip;
   }
-  if (variant == kStag) return stag_ok(p) ? (p.x2 != nullptr ? "conv_stag_x2_kernel" : "conv_stag_kernel") : nullptr;
+  if (variant == kStag) {
+    if (!stag_ok(p)) return nullptr;
+    if (p.cout <= 128) return p.x2 != nullptr ? "conv_stag128_x2_kernel" : "conv_stag128_kernel";
+    return p.x2 != nullptr ? "conv_stag_x2_kernel" : "conv_stag_kernel";
+  }
   if (variant == kStrip) return strip_ok(p) && p.cin >= 64 ? "conv_strip_kernel" : nullptr;
   if (variant >= kNumVariants) return nullptr;
   if (p.x2 != nullptr) {

@@ -51,12 +51,16 @@ namespace {
 // buffer) is fetched by the last tap group's strip shares; after the staggered loop the waves
 // re-align and run the x2 steps unstaggered (one barrier per step, next step's A and B DMA'd
 // under the current step's MFMAs).
-template <typename T, bool X2>
+//
+// WCO = channels per wave (tile = 2 WCO output channels x 256 pixels): 128 (the 256-channel tile
+// of layer5-8) or 64 (128-channel convs: D-22 layer4); GR = WCO / 32 MFMA groups per substep.
+template <typename T, bool X2, int WCO = 128>
 __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   using K = KT<T>;
   constexpr int BK = 128 / K::ESZ;                   // 128-B LDS rows (bf16 64, int8 128 channels)
-  using C = BigCfg<128, 2, 2, BK, 4, K::ESZ>;
-  static_assert(C::ROWB == 128 && C::A_INSTR == 4 && C::FN == 4 && C::FM == 8, "stag tile geometry");
+  using C = BigCfg<WCO, 2, 2, BK, 4, K::ESZ>;
+  constexpr int FM = C::FM, GR = FM / 2, AI = C::A_INSTR, BCO = 2 * WCO;
+  static_assert(C::ROWB == 128 && C::FN == 4 && (WCO == 128 || WCO == 64) && AI == WCO / 32, "stag tile geometry");
   constexpr int CE = 16 / K::ESZ;
   constexpr int AB = C::A_BYTES;                     // 32 KB per A stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -68,7 +72,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   const int wp = wave & 3;                           // 64-pixel slice
   const int M = p.n * p.ho * p.wo;
   const int hw_o = p.ho * p.wo;
-  const int nco = (p.cout + 255) / 256;
+  const int nco = (p.cout + BCO - 1) / BCO;
   const int ntiles = (M / kBPX) * nco;
   const int cin = p.cin;
   const int lc = 31 - __builtin_clz(cin);
@@ -86,7 +90,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
 
   const int tile = xcd_remap2(blockIdx.x, ntiles);
   const int px0 = (tile / nco) * kBPX;
-  const int co0 = (tile % nco) * 256;
+  const int co0 = (tile % nco) * BCO;
   const int s_n = px0 / hw_o;
   const int s_q = px0 - s_n * hw_o;
   const int s_oh = s_q / p.wo;
@@ -106,7 +110,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   uint32_t a_off[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int r = (wave * 4 + i) * 8 + lrow;
+    const int r = (wave * AI + i) * 8 + lrow;
     a_off[i] = ((co0 + r) * p.k_pad + swzb<128>(r, lslot) * CE) * K::ESZ;
   }
   constexpr uint32_t kOOB = 0x80000000u;             // beyond every buffer (sizes < 2^31)
@@ -116,7 +120,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     const int cb = kt / 9;
     const int tap = kt - cb * 9;
     const int k0 = (X2 && kt >= nk) ? 9 * cin + (kt - nk) * BK : (tap << lc) + cb * BK;
-    dma(rs_w, a_off[i & 1], ((i & ~1) * 8 * p.k_pad + k0) * K::ESZ, stage * AB + (wave * 4 + i) * 1024);
+    dma(rs_w, a_off[i & 1], ((i & ~1) * 8 * p.k_pad + k0) * K::ESZ, stage * AB + (wave * AI + i) * 1024);
   };
   // strip share sh of group g (channel block g / 3, tap row g % 3) into strip buffer `buf`
   auto issue_strip = [&](int g, int buf, int sh) {
@@ -158,7 +162,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   uint32_t a_base[2], b_base[3][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int r = wc * 128 + fr;
+    const int r = wc * WCO + fr;
     a_base[u] = r * 128 + (swzb<128>(r, u * 4 + fq) << 4);
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
@@ -167,7 +171,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     }
   }
 
-  typename K::acc acc[8][4];
+  typename K::acc acc[FM][4];
   typename K::frag af[2][2], bfr[2][4];
   auto rd = [&](typename K::frag& dst, uint32_t base, auto off_c) {
     constexpr int OFF = decltype(off_c)::value;
@@ -192,10 +196,10 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     rd(dst[3], b, std::integral_constant<int, BF * kStripBytes + 3 * 2048>{});
   };
 
-  if constexpr (K::ESZ == 2) init_tile<8, 128, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
+  if constexpr (K::ESZ == 2) init_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
   else zero_tile(acc);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) issue_a(0, 0, i);
+  for (int i = 0; i < AI; ++i) issue_a(0, 0, i);
 #pragma unroll
   for (int sh = 0; sh < 5; ++sh) issue_strip(0, 0, sh);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
@@ -228,7 +232,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     }
     auto group_reads = [&](auto qg_c) {
       constexpr int QG = decltype(qg_c)::value;
-      if constexpr (QG < 3) {
+      if constexpr (QG < GR - 1) {
         load_a(af[(QG + 1) & 1], IS{}, IU{}, std::integral_constant<int, QG + 1>{});
       } else if constexpr (U == 0) {                 // the second substep's first fragments, ahead of the barrier
         load_b(bfr[1], IG{}, IK{}, O{});
@@ -236,7 +240,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
       }
     };
 #pragma unroll
-    for (int qg = 0; qg < 4; ++qg) {
+    for (int qg = 0; qg < GR; ++qg) {
       if (qg == 0) group_reads(std::integral_constant<int, 0>{});
       if (qg == 1) group_reads(std::integral_constant<int, 1>{});
       if (qg == 2) group_reads(std::integral_constant<int, 2>{});
@@ -244,7 +248,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
 #if DRNMI_STAG_LGKM || DRNMI_STAG_ASM
       // this group's fragments: everything but the reads issued after them (the next group's
       // 2, or 6 when the second substep's B and first A went out)
-      if (qg < 3) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      if (qg < GR - 1) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
       else if (U == 0) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -254,21 +258,21 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
 #pragma unroll
         for (int fn = 0; fn < 4; ++fn)
           acc[qg * 2 + h][fn] = K::mma(af[qg & 1][h], bfr[U][fn], acc[qg * 2 + h][fn]);
-      if constexpr (U == 0) issue_a(ta, STAGE ^ 1, qg);
+      if constexpr (U == 0) { if (qg < AI) issue_a(ta, STAGE ^ 1, qg); }
       if constexpr (KW == 0 && U == 1) { if (qg < 2) issue_next_strip(g, GP ^ 1, qg); }
       if constexpr (KW == 1 && U == 0) { if (qg == 1) issue_next_strip(g, GP ^ 1, 2); }
       if constexpr (KW == 1 && U == 1) { if (qg < 2) issue_next_strip(g, GP ^ 1, 3 + qg); }
       __builtin_amdgcn_sched_barrier(0);
     }
     // retire every piece issued before this phase; this phase's own stay in flight
-    if constexpr (KW == 0 && U == 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if constexpr (KW == 0 && U == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(AI) : "memory");
     if constexpr (KW == 0 && U == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    if constexpr (KW == 1 && U == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    if constexpr (KW == 1 && U == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(AI + 1) : "memory");
     if constexpr (KW == 1 && U == 1) {
       if (wave == 0) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // shares 3 and 4 (piece 32)
       else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     }
-    if constexpr (KW == 2 && U == 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if constexpr (KW == 2 && U == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(AI) : "memory");
     if constexpr (KW == 2 && U == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (U == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else asm volatile("s_barrier" ::: "memory");
@@ -304,7 +308,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
       const int buf = (ngroups + e) & 1;
       if (e + 1 < nx2) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) issue_a(nk + e + 1, stage ^ 1, i);
+        for (int i = 0; i < AI; ++i) issue_a(nk + e + 1, stage ^ 1, i);
 #pragma unroll
         for (int sh = 0; sh < 5; ++sh) issue_x2(e + 1, buf ^ 1, sh);
       }
@@ -315,7 +319,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
         for (int fn = 0; fn < 4; ++fn)
           b4[fn] = *reinterpret_cast<const typename K::frag*>(smem + b_base[0][u] + buf * kStripBytes + fn * 2048);
 #pragma unroll
-        for (int qg = 0; qg < 4; ++qg) {
+        for (int qg = 0; qg < GR; ++qg) {
           typename K::frag a2[2];
 #pragma unroll
           for (int h = 0; h < 2; ++h)
@@ -331,8 +335,8 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped re-fetches
-  if constexpr (K::ESZ == 2) store_tile<8, 128, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
-  else store_tile_i8<8, 128, 4>(p, acc, px0, co0, wc, wp, fr, fq);
+  if constexpr (K::ESZ == 2) store_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
+  else store_tile_i8<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
 }
 
 __global__ void __launch_bounds__(512, 1)
@@ -347,6 +351,17 @@ conv_i8_stag_kernel(const drnmi_conv_args p) {
   conv_stag_body<int8_t, false>(p);
 }
 
+// the 128-channel tile (D-22 layer4: 128 -> 128, with the fused 1x1 stride-2 downsample in
+// layer4.0 conv2)
+__global__ void __launch_bounds__(512, 1)
+conv_stag128_kernel(const drnmi_conv_args p) {
+  conv_stag_body<uint16_t, false, 64>(p);
+}
+__global__ void __launch_bounds__(512, 1)
+conv_stag128_x2_kernel(const drnmi_conv_args p) {
+  conv_stag_body<uint16_t, true, 64>(p);
+}
+
 // + the fused 1x1 downsample (x2 != NULL; layer5.0 / layer6.0 conv2 of D-22)
 __global__ void __launch_bounds__(512, 1)
 conv_stag_x2_kernel(const drnmi_conv_args p) {
@@ -355,7 +370,8 @@ conv_stag_x2_kernel(const drnmi_conv_args p) {
 
 }  // namespace
 
-constexpr int kStagLds = 2 * 256 * 128 + 2 * kStripBytes;   // 2 A stages + 2 strips (130 KB)
+constexpr int kStagLds = 2 * 256 * 128 + 2 * kStripBytes;     // 2 A stages + 2 strips (130 KB)
+constexpr int kStag128Lds = 2 * 128 * 128 + 2 * kStripBytes;  // 128-channel tile (98 KB)
 
 hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s) {
   static bool attr_set = false;
@@ -365,16 +381,25 @@ hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kStagLds);
       if (e != hipSuccess) return e;
     }
+    for (const void* f : {reinterpret_cast<const void*>(&conv_stag128_kernel), reinterpret_cast<const void*>(&conv_stag128_x2_kernel)}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kStag128Lds);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
-  const int64_t blocks = (M / kBPX) * ((p.cout + 255) / 256);
-  if (p.dtype == DRNMI_I8)
-    hipLaunchKernelGGL(conv_i8_stag_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), kStagLds, s, p);
-  else if (p.x2 != nullptr)
-    hipLaunchKernelGGL(conv_stag_x2_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), kStagLds, s, p);
-  else
-    hipLaunchKernelGGL(conv_stag_kernel, dim3(static_cast<unsigned>(blocks)), dim3(512), kStagLds, s, p);
+  const dim3 grid(static_cast<unsigned>((M / kBPX) * ((p.cout + 255) / 256)));
+  if (p.dtype != DRNMI_I8 && p.cout <= 128) {
+    const dim3 g128(static_cast<unsigned>((M / kBPX) * ((p.cout + 127) / 128)));
+    if (p.x2 != nullptr) hipLaunchKernelGGL(conv_stag128_x2_kernel, g128, dim3(512), kStag128Lds, s, p);
+    else hipLaunchKernelGGL(conv_stag128_kernel, g128, dim3(512), kStag128Lds, s, p);
+  } else if (p.dtype == DRNMI_I8) {
+    hipLaunchKernelGGL(conv_i8_stag_kernel, grid, dim3(512), kStagLds, s, p);
+  } else if (p.x2 != nullptr) {
+    hipLaunchKernelGGL(conv_stag_x2_kernel, grid, dim3(512), kStagLds, s, p);
+  } else {
+    hipLaunchKernelGGL(conv_stag_kernel, grid, dim3(512), kStagLds, s, p);
+  }
   return hipGetLastError();
 }
 
