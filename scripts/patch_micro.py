@@ -22,6 +22,8 @@ only = os.environ.get("ONLY", "")
 cases = [
     ("stem u8 7x7 3->16", 2.0 * B * H * W * 16 * 147,
      lambda: ops.stem_u8(frames, w0, one16, zero16, (0.3, 0.3, 0.3), (0.2, 0.2, 0.2))),
+    ("stem+layer1 fused", 2.0 * B * H * W * 16 * (147 + 144),
+     lambda: ops.stem_layer1_u8(frames, w0, one16, zero16, w1, one16, zero16, (0.3, 0.3, 0.3), (0.2, 0.2, 0.2))),
     ("layer1 3x3 16->16", 2.0 * B * H * W * 16 * 144,
      lambda: ops.conv2d_bn_act(x1, w1, None, None, None, 1, 1, 1, True, algo=_lib.ALGO_PATCH)),
     ("layer2 3x3 s2 16->32", 2.0 * B * H * W / 4 * 32 * 144,
