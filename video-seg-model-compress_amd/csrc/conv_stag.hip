@@ -12,6 +12,10 @@
 #define DRNMI_STAG_ASM 1    // fragment reads as inline-asm ds_read_b128 with hand-counted lgkmcnt (hipcc's
                             // own waits drain every second group: 0.6-0.8 % slower, profiles/r4a_stag_ab)
 #endif
+#ifndef DRNMI_STAG_ABL
+#define DRNMI_STAG_ABL 0    // diagnostic builds only: bit 0 drops the in-loop DMA, bit 1 the MFMAs,
+                            // bit 2 the fragment reads (registers keep stale values)
+#endif
 #ifndef DRNMI_STAG_PRIO
 #define DRNMI_STAG_PRIO 0   // diagnostic: s_setprio 1 for the lagging half (waves 4-7)
 #endif
@@ -103,7 +107,9 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.wgt), 0, p.cout_pad * p.k_pad * K::ESZ, 0x00020000);
   typedef __attribute__((address_space(3))) void lds_t;
+  bool in_loop = false;                              // DRNMI_STAG_ABL bit 0: no DMA once the loop runs
   auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, int soff, int lds_byte) {
+    if ((DRNMI_STAG_ABL & 1) && in_loop) return;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, 0);
   };
   // weight rows (wave*4 + i)*8 + lrow: the swizzle depends on i only through its parity
@@ -175,6 +181,9 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   typename K::frag af[2][2], bfr[2][4];
   auto rd = [&](typename K::frag& dst, uint32_t base, auto off_c) {
     constexpr int OFF = decltype(off_c)::value;
+    if constexpr ((DRNMI_STAG_ABL & 4) != 0) {
+      if (in_loop) { asm volatile("" : "+v"(dst)); return; }
+    }
 #if DRNMI_STAG_ASM
     // base: a byte offset into smem, which is LDS address 0 (the kernel's only LDS object)
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(OFF));
@@ -204,6 +213,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   for (int sh = 0; sh < 5; ++sh) issue_strip(0, 0, sh);
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
+  in_loop = true;
   if (wc == 1) {                                     // the stagger: waves 4-7 sit out phase 0
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -257,7 +267,8 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int fn = 0; fn < 4; ++fn)
-          acc[qg * 2 + h][fn] = K::mma(af[qg & 1][h], bfr[U][fn], acc[qg * 2 + h][fn]);
+          if constexpr ((DRNMI_STAG_ABL & 2) != 0) asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
+          else acc[qg * 2 + h][fn] = K::mma(af[qg & 1][h], bfr[U][fn], acc[qg * 2 + h][fn]);
       if constexpr (U == 0) { if (qg < AI) issue_a(ta, STAGE ^ 1, qg); }
       if constexpr (KW == 0 && U == 1) { if (qg < 2) issue_next_strip(g, GP ^ 1, qg); }
       if constexpr (KW == 1 && U == 0) { if (qg == 1) issue_next_strip(g, GP ^ 1, 2); }
