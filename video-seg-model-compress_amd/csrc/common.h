@@ -88,6 +88,17 @@ template <> struct Vec8<float> {
   }
 };
 
+// 16-B row pieces of the MFMA accumulator layout (lane (fr, fq) holds channels 16 fm + 4 fq .. + 3
+// of pixel fr): row fq of the 16-lane groups moves chunk s(fq) = (0, 2, 1, 3)[fq] of a 32-channel
+// group, and one v_permlane16_swap per dword pair converts (lo: x y, hi: z w) <-> (fragment 2 f2,
+// fragment 2 f2 + 1) both ways (conv_tile.h load_residual / store_tile_x4)
+__device__ __forceinline__ int chunk_of_row(int fq) { return (fq & 1) * 2 + (fq >> 1); }
+__device__ __forceinline__ void swap_halves(uint4& v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(v.x, v.z, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(v.y, v.w, false, false);
+  v = make_uint4(a[0], b[0], a[1], b[1]);
+}
+
 inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
 
 }  // namespace drnmi

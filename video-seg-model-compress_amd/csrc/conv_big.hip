@@ -378,8 +378,18 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       }
     }
 
-    if constexpr (K::ESZ == 2) store_tile<C::FM, WCO, C::FN, DEFER>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
-    else store_tile_i8<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+    if constexpr (K::ESZ == 2) {
+      // whole tile inside a dense bf16 NHWC output: 16-B stores (conv_tile.h store_tile_x4)
+      bool x4 = false;
+      if constexpr (!DEFER && C::FM % 2 == 0)
+        x4 = p.scale == nullptr && p.out_dtype == DRNMI_BF16 && p.y_sc == 1 && p.y_sp == p.cout &&
+             p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout && cur_px0 + kBPX <= p.n * p.ho * p.wo &&
+             cur_co0 + C::BCO <= p.cout;
+      if (x4) store_tile_x4<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+      else store_tile<C::FM, WCO, C::FN, DEFER>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+    } else {
+      store_tile_i8<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+    }
     if (!more) break;
     if constexpr (K::ESZ == 2) init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);
     else zero_tile(acc);

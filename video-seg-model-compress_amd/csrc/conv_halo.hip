@@ -136,8 +136,22 @@ conv_halo_kernel(const drnmi_conv_args p) {
         }
       }
   }
-  if (p.scale == nullptr && res != nullptr && oh < p.ho) {
-    uint2 rv[4][FN];
+  // residual loads issued here, added after the patch and weight DMA went out (adding them here
+  // made the DMA wait for the residual: two latencies in series per tile)
+  const bool add_res = p.scale == nullptr && res != nullptr && oh < p.ho;
+  // full output row run (wave-uniform): residual and output as 16-B pieces (common.h swap_halves)
+  const bool full_row = oh < p.ho && ow0 + TC <= p.wo;
+  uint2 rv[4][FN];
+  uint4 rq[2][FN];
+  if (add_res && full_row) {
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow0 + fn * 16 + fr;
+#pragma unroll
+      for (int f2 = 0; f2 < 2; ++f2)
+        rq[f2][fn] = *reinterpret_cast<const uint4*>(res + m * p.cout + wc * 64 + f2 * 32 + chunk_of_row(fq) * 8);
+    }
+  } else if (add_res) {
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       const int ow = ow0 + fn * 16 + fr;
@@ -146,15 +160,6 @@ conv_halo_kernel(const drnmi_conv_args p) {
       for (int fm = 0; fm < 4; ++fm)
         rv[fm][fn] = *reinterpret_cast<const uint2*>(res + m * p.cout + wc * 64 + fm * 16 + fq * 4);
     }
-#pragma unroll
-    for (int fm = 0; fm < 4; ++fm)
-#pragma unroll
-      for (int fn = 0; fn < FN; ++fn) {
-        acc[fm][fn][0] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x & 0xffff));
-        acc[fm][fn][1] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x >> 16));
-        acc[fm][fn][2] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y & 0xffff));
-        acc[fm][fn][3] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y >> 16));
-      }
   }
 
   // --- patch: DMA once (pieces dealt round-robin over the waves)
@@ -194,6 +199,27 @@ conv_halo_kernel(const drnmi_conv_args p) {
   for (int t = 0; t < kNST - 1 && t < nk_all; ++t)
 #pragma unroll
     for (int i = 0; i < A_PIECES; ++i) issue_a(t, i);
+  if (add_res && full_row) {
+#pragma unroll
+    for (int f2 = 0; f2 < 2; ++f2)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        swap_halves(rq[f2][fn]);
+        rv[2 * f2][fn] = make_uint2(rq[f2][fn].x, rq[f2][fn].y);
+        rv[2 * f2 + 1][fn] = make_uint2(rq[f2][fn].z, rq[f2][fn].w);
+      }
+  }
+  if (add_res) {
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        acc[fm][fn][0] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x & 0xffff));
+        acc[fm][fn][1] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].x >> 16));
+        acc[fm][fn][2] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y & 0xffff));
+        acc[fm][fn][3] += bf16_to_f32(static_cast<uint16_t>(rv[fm][fn].y >> 16));
+      }
+  }
 
 
   for (int t = 0; t < nk; ++t) {
@@ -268,6 +294,31 @@ conv_halo_kernel(const drnmi_conv_args p) {
 
   // --- epilogue: lane owns channels co..co+3 of pixel (oh0 + wp, ow0 + fn*16 + fr)
   if (oh >= p.ho) return;
+  if (full_row && p.scale == nullptr) {   // shift (+ residual) already in the accumulators
+    uint16_t* __restrict__ y = reinterpret_cast<uint16_t*>(p.y);
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow0 + fn * 16 + fr;
+#pragma unroll
+      for (int f2 = 0; f2 < 2; ++f2) {
+        uint32_t w[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v[4] = {acc[2 * f2 + h][fn][0], acc[2 * f2 + h][fn][1], acc[2 * f2 + h][fn][2], acc[2 * f2 + h][fn][3]};
+          if (p.relu) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          }
+          w[2 * h] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+          w[2 * h + 1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+        }
+        uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
+        swap_halves(o);
+        *reinterpret_cast<uint4*>(y + m * p.cout + wc * 64 + f2 * 32 + chunk_of_row(fq) * 8) = o;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
     const int ow = ow0 + fn * 16 + fr;

@@ -16,6 +16,9 @@
 #define DRNMI_STAG_ABL 0    // diagnostic builds only: bit 0 drops the in-loop DMA, bit 1 the MFMAs,
                             // bit 2 the fragment reads (registers keep stale values)
 #endif
+#ifndef DRNMI_STAG_OLDINIT
+#define DRNMI_STAG_OLDINIT 0  // diagnostic: residual loaded and added before the prologue DMA (A/B)
+#endif
 #ifndef DRNMI_STAG_PRIO
 #define DRNMI_STAG_PRIO 0   // diagnostic: s_setprio 1 for the lagging half (waves 4-7)
 #endif
@@ -205,12 +208,48 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     rd(dst[3], b, std::integral_constant<int, BF * kStripBytes + 3 * 2048>{});
   };
 
-  if constexpr (K::ESZ == 2) init_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
-  else zero_tile(acc);
+  // accumulator start: shift (+ residual).  The residual loads go out before the prologue DMA
+  // and are added after it, so their latency and the DMA's overlap (init_tile waited for them
+  // before issuing the DMA).  Tiles cover whole 4-channel groups when cout % BCO == 0.
+  const bool split_init = K::ESZ == 2 && p.scale == nullptr && p.cout % BCO == 0;
+  const bool has_res = split_init && p.res != nullptr;
+  // dense bf16 NHWC output: the 16-B store epilogue (store_tile_x4)
+  const bool fast_epi = split_init && p.out_dtype == DRNMI_BF16 && p.y_sc == 1 && p.y_sp == p.cout &&
+                        p.y_sn == static_cast<int64_t>(hw_o) * p.cout;
+  uint4 rv[FM / 2][4];
+  float4 shv[FM];
+  if constexpr (K::ESZ == 2) {
+#if DRNMI_STAG_OLDINIT
+    init_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
+#else
+    if (split_init) {
+      // only loads here: a register written from a pending load before the DMA issue would make
+      // the compiler wait (vmcnt(0) at the join) ahead of it
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm) shv[fm] = *reinterpret_cast<const float4*>(p.shift + co0 + wc * WCO + fm * 16 + fq * 4);
+      if (has_res) load_residual<FM, WCO, 4>(p, rv, px0, co0, wc, wp, fr, fq);
+    } else {
+      init_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
+    }
+#endif
+  } else {
+    zero_tile(acc);
+  }
 #pragma unroll
   for (int i = 0; i < AI; ++i) issue_a(0, 0, i);
 #pragma unroll
   for (int sh = 0; sh < 5; ++sh) issue_strip(0, 0, sh);
+#if !DRNMI_STAG_OLDINIT
+  if constexpr (K::ESZ == 2) {
+    if (split_init) {
+#pragma unroll
+      for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = f32x4{shv[fm].x, shv[fm].y, shv[fm].z, shv[fm].w};
+      if (has_res) add_residual(acc, rv);
+    }
+  }
+#endif
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   in_loop = true;
@@ -346,8 +385,10 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped re-fetches
-  if constexpr (K::ESZ == 2) store_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
-  else store_tile_i8<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
+  if constexpr (K::ESZ == 2) {
+    if (fast_epi && !DRNMI_STAG_OLDINIT) store_tile_x4<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
+    else store_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
+  } else store_tile_i8<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
 }
 
 __global__ void __launch_bounds__(512, 1)

@@ -142,6 +142,75 @@ __device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)
   }
 }
 
+// Residual and output rows as 16-B pieces.  The accumulator layout gives lane (fr, fq) channels
+// 16 fm + 4 fq .. + 3 of pixel fr: as 8-B accesses every instruction touches 16 pixels x 32 B, and
+// each 128-B line is requested by four instructions.  Here row fq of the 16-lane groups moves the
+// 16-B chunk s(fq) = (0, 2, 1, 3)[fq] of a 32-channel group (channels 8 s .. 8 s + 7) and one
+// v_permlane16_swap per dword pair converts between the two layouts: swapping the odd rows of the
+// low halves with the even rows of the high halves leaves quad fq of the group (fragment 2 f2) in
+// the low halves and quad 4 + fq (fragment 2 f2 + 1) in the high halves, and back.  Half the
+// instructions, 64 contiguous bytes per pixel; the values are the same, so the sums are.
+// (chunk_of_row, swap_halves: common.h)
+template <int FM, int WCO, int FN>
+__device__ __forceinline__ void load_residual(const drnmi_conv_args& p, uint4 (&rq)[FM / 2][FN], int px0, int co0, int wc,
+                                              int wp, int fr, int fq) {
+  const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
+  const int c = co0 + wc * WCO + chunk_of_row(fq) * 8;
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    const int64_t m = px0 + wp * 16 * FN + fn * 16 + fr;
+#pragma unroll
+    for (int f2 = 0; f2 < FM / 2; ++f2) rq[f2][fn] = *reinterpret_cast<const uint4*>(res + m * p.cout + c + f2 * 32);
+  }
+}
+template <int FM, int FN>
+__device__ __forceinline__ void add_residual(f32x4 (&acc)[FM][FN], uint4 (&rq)[FM / 2][FN]) {
+#pragma unroll
+  for (int f2 = 0; f2 < FM / 2; ++f2)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      swap_halves(rq[f2][fn]);
+      const uint32_t w[4] = {rq[f2][fn].x, rq[f2][fn].y, rq[f2][fn].z, rq[f2][fn].w};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4& a = acc[2 * f2 + h][fn];
+        a[0] += bf16_to_f32(static_cast<uint16_t>(w[2 * h] & 0xffff));
+        a[1] += bf16_to_f32(static_cast<uint16_t>(w[2 * h] >> 16));
+        a[2] += bf16_to_f32(static_cast<uint16_t>(w[2 * h + 1] & 0xffff));
+        a[3] += bf16_to_f32(static_cast<uint16_t>(w[2 * h + 1] >> 16));
+      }
+    }
+}
+// dense bf16 NHWC output (y_sc 1, y_sp cout), shift and residual already in the accumulators:
+// ReLU, round, 16-B stores (the rounding and ReLU of store_tile, element for element)
+template <int FM, int WCO, int FN>
+__device__ __forceinline__ void store_tile_x4(const drnmi_conv_args& p, const f32x4 (&acc)[FM][FN], int px0, int co0,
+                                              int wc, int wp, int fr, int fq) {
+  uint16_t* __restrict__ y = reinterpret_cast<uint16_t*>(p.y);
+  const int c = co0 + wc * WCO + chunk_of_row(fq) * 8;
+  const bool relu = p.relu != 0;
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    const int64_t m = px0 + wp * 16 * FN + fn * 16 + fr;
+#pragma unroll
+    for (int f2 = 0; f2 < FM / 2; ++f2) {
+      uint32_t w[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float v[4] = {acc[2 * f2 + h][fn][0], acc[2 * f2 + h][fn][1], acc[2 * f2 + h][fn][2], acc[2 * f2 + h][fn][3]};
+        if (relu) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        w[2 * h] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+        w[2 * h + 1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+      }
+      uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
+      swap_halves(o);
+      *reinterpret_cast<uint4*>(y + m * p.cout + c + f2 * 32) = o;
+    }
+  }
+}
 template <int FM, int WCO, int FN = 4, bool DEFER = false>
 __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4 (&acc)[FM][FN], int cur_px0,
                                            int cur_co0, int wc, int wp, int fr, int fq) {
