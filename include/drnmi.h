@@ -301,6 +301,10 @@ typedef struct drnmi_wgrad_args {
 } drnmi_wgrad_args;
 int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* args);
 int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* args, void* stream);
+/* The same weight gradient in fp32-class split-bf16 arithmetic (the fp32x fine-tune: exact 3-way
+ * bf16 split of dy and x, the six products above 2^-24 on the bf16 MFMA, fp32 accumulation);
+ * same arguments, workspace and errors.  semantic_seg.py:166-230 backward. */
+int drnmi_conv_wgrad_f32x3(const drnmi_wgrad_args* args, void* stream);
 
 /* out[n][y][x][c] = dy[n][y/s][x/s][c] where y, x are multiples of s (and inside dy), else 0;
  * out is [n][hu][wu][c] (c % 4 == 0).  Input of the stride-1 dgrad conv of a stride-s conv. */

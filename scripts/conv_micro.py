@@ -28,6 +28,9 @@ SHAPES = [  # name, cin, cout, ks, stride, dil, H(in), W(in), residual
 ]
 dev = "cuda"
 ONLY = os.environ.get("ONLY")
+# scale folded into the weights (scale = NULL: the accumulators start from shift + residual), as the
+# engine launches the bf16 convs; FOLD=0 times the unfolded epilogue
+FOLD = os.environ.get("FOLD", "1") != "0"
 for name, cin, cout, ks, st, dil, h, w, has_res in SHAPES:
     if ONLY and not name.startswith(ONLY):
         continue
@@ -47,11 +50,11 @@ for name, cin, cout, ks, st, dil, h, w, has_res in SHAPES:
         for t in TILES:
             try:
                 for _ in range(2):
-                    ops.conv2d_bn_act(x, wt, None, None, res, st, pad, dil, True, tile=t, packed=packed)
+                    ops.conv2d_bn_act(x, wt, None, None, res, st, pad, dil, True, tile=t, packed=packed, fold_scale=FOLD)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(5):
-                    ops.conv2d_bn_act(x, wt, None, None, res, st, pad, dil, True, tile=t, packed=packed)
+                    ops.conv2d_bn_act(x, wt, None, None, res, st, pad, dil, True, tile=t, packed=packed, fold_scale=FOLD)
                 e1.record()
                 torch.cuda.synchronize()
                 times.setdefault(t, []).append(e0.elapsed_time(e1) / 5 * 1e3)

@@ -99,6 +99,20 @@ __device__ __forceinline__ void swap_halves(uint4& v) {
   v = make_uint4(a[0], b[0], a[1], b[1]);
 }
 
+// int8 rows: lane (fr, fq) holds byte quad fq (channels 4 fq .. + 3) of fragments 4 g + k in r[k];
+// this 4 x 4 transpose over (register, 16-lane row) leaves fragment 4 g + fq whole in row fq's four
+// registers (16 contiguous bytes), and back (it is its own inverse)
+__device__ __forceinline__ void transpose_rows4(uint32_t (&r)[4]) {
+  const auto a = __builtin_amdgcn_permlane32_swap(r[0], r[2], false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(r[1], r[3], false, false);
+  const auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+  const auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+  r[0] = c[0];
+  r[1] = c[1];
+  r[2] = d[0];
+  r[3] = d[1];
+}
+
 inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
 
 }  // namespace drnmi

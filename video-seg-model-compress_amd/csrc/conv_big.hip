@@ -388,7 +388,13 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       if (x4) store_tile_x4<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
       else store_tile<C::FM, WCO, C::FN, DEFER>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
     } else {
-      store_tile_i8<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+      bool x4 = false;
+      if constexpr (C::FM % 4 == 0)
+        x4 = p.out_dtype == DRNMI_I8 && p.y_sc == 1 && p.y_sp == p.cout &&
+             p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout && cur_px0 + kBPX <= p.n * p.ho * p.wo &&
+             cur_co0 + C::BCO <= p.cout && (p.res == nullptr || p.cout % 16 == 0);
+      if (x4) store_tile_i8_x4<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
+      else store_tile_i8<C::FM, WCO, C::FN>(p, acc, cur_px0, cur_co0, wc, wp, fr, fq);
     }
     if (!more) break;
     if constexpr (K::ESZ == 2) init_tile<C::FM, WCO, C::FN, DEFER>(p, acc, px0, co0, wc, wp, fr, fq);
@@ -755,7 +761,19 @@ constexpr int kPingPong = 12;
 constexpr int kHalo = 13;   // conv_halo.hip (tile id 17)
 constexpr int kStrip = 14;  // conv_strip_kernel (tile id 18); auto routes variant 1 there when strip_ok
 constexpr int kStag = 15;   // conv_stag_kernel (tile id 19): the strip tile with staggered SIMD partners
+constexpr int kSeg = 16;    // conv_seg_kernel (tile id 20): the seg classifier, 1x1 to <= 32 classes
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// auto-picked seg classifier launches (1x1, cout <= 32) run conv_seg_kernel (bit-identical to the
+// BK-32 tile); DRNMI_SEG=0 keeps them on conv_big (A/B runs)
+bool seg_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("DRNMI_SEG");
+    on = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
 
 template <int KS, bool PERSIST>
 hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
@@ -973,6 +991,7 @@ bool big_conv_supported(const drnmi_conv_args& p) {
 }
 
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
+  if (variant == kSeg || (variant < 0 && seg_enabled() && seg_conv_supported(p))) return seg_conv_dispatch(p, s);
   // the halo kernel (cin/cout 64-128) stays dense: it beats unit skipping on those shapes
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_dispatch(p, s);
   if (!big_conv_supported(p)) return DRNMI_ENOTSUP;
@@ -1019,6 +1038,8 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 }
 
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
+  if (variant == kSeg || (variant < 0 && seg_enabled() && seg_conv_supported(p)))
+    return seg_conv_supported(p) ? "conv_seg_kernel" : nullptr;
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_name(p);
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);

@@ -299,6 +299,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) {
       const int64_t m = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow0 + fn * 16 + fr;
+      uint4 o[2];
 #pragma unroll
       for (int f2 = 0; f2 < 2; ++f2) {
         uint32_t w[4];
@@ -312,10 +313,23 @@ conv_halo_kernel(const drnmi_conv_args p) {
           w[2 * h] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
           w[2 * h + 1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
         }
-        uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
-        swap_halves(o);
-        *reinterpret_cast<uint4*>(y + m * p.cout + wc * 64 + f2 * 32 + chunk_of_row(fq) * 8) = o;
+        o[f2] = make_uint4(w[0], w[1], w[2], w[3]);
+        swap_halves(o[f2]);
       }
+      // whole 128-B lines (the wave's 64 channels of 8 pixels per instruction): lanes fr and
+      // fr ^ 8 trade their second-group chunks (as conv_tile.h store_tile_x4)
+      const bool lo = fr < 8;
+      const int64_t m0 = m - (lo ? 0 : 8), m1 = m0 + 8;
+      uint4 r;
+      r.x = __builtin_amdgcn_update_dpp(0u, o[1].x, 0x128, 0xf, 0xf, false);
+      r.y = __builtin_amdgcn_update_dpp(0u, o[1].y, 0x128, 0xf, 0xf, false);
+      r.z = __builtin_amdgcn_update_dpp(0u, o[1].z, 0x128, 0xf, 0xf, false);
+      r.w = __builtin_amdgcn_update_dpp(0u, o[1].w, 0x128, 0xf, 0xf, false);
+      const uint4 d0 = make_uint4(lo ? o[0].x : r.x, lo ? o[0].y : r.y, lo ? o[0].z : r.z, lo ? o[0].w : r.w);
+      const uint4 d1 = make_uint4(lo ? r.x : o[0].x, lo ? r.y : o[0].y, lo ? r.z : o[0].z, lo ? r.w : o[0].w);
+      const int c = wc * 64 + chunk_of_row(fq) * 8;
+      *reinterpret_cast<uint4*>(y + m0 * p.cout + c + (lo ? 0 : 32)) = d0;
+      *reinterpret_cast<uint4*>(y + m1 * p.cout + c + (lo ? 32 : 0)) = d1;
     }
     return;
   }

@@ -246,7 +246,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
       for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
         for (int fn = 0; fn < 4; ++fn) acc[fm][fn] = f32x4{shv[fm].x, shv[fm].y, shv[fm].z, shv[fm].w};
-      if (has_res) add_residual(acc, rv);
+      if (has_res) add_residual(acc, rv, fr);
     }
   }
 #endif
@@ -388,7 +388,14 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   if constexpr (K::ESZ == 2) {
     if (fast_epi && !DRNMI_STAG_OLDINIT) store_tile_x4<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
     else store_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
-  } else store_tile_i8<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
+  } else {
+    // whole tile of a dense int8 NHWC output (M % 256 == 0 here): 16-B pieces
+    if (p.out_dtype == DRNMI_I8 && p.y_sc == 1 && p.y_sp == p.cout && p.y_sn == static_cast<int64_t>(hw_o) * p.cout &&
+        p.cout % BCO == 0 && (p.res == nullptr || p.cout % 16 == 0))
+      store_tile_i8_x4<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
+    else
+      store_tile_i8<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
+  }
 }
 
 __global__ void __launch_bounds__(512, 1)

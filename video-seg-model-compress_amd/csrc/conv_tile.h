@@ -151,6 +151,9 @@ __device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)
 // the low halves and quad 4 + fq (fragment 2 f2 + 1) in the high halves, and back.  Half the
 // instructions, 64 contiguous bytes per pixel; the values are the same, so the sums are.
 // (chunk_of_row, swap_halves: common.h)
+#ifndef DRNMI_EPI128
+#define DRNMI_EPI128 1   // store_tile_x4 writes whole 128-B lines (0: 64-B pieces, A/B)
+#endif
 template <int FM, int WCO, int FN>
 __device__ __forceinline__ void load_residual(const drnmi_conv_args& p, uint4 (&rq)[FM / 2][FN], int px0, int co0, int wc,
                                               int wp, int fr, int fq) {
@@ -159,12 +162,44 @@ __device__ __forceinline__ void load_residual(const drnmi_conv_args& p, uint4 (&
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
     const int64_t m = px0 + wp * 16 * FN + fn * 16 + fr;
+#if DRNMI_EPI128
+    // whole 128-B lines, the mirror of store_tile_x4: rq[2 L] / rq[2 L + 1] hold the pieces of
+    // pixels 0-7 / 8-15 of groups (2 L, 2 L + 1); add_residual trades them back (lanes fr ^ 8)
+    static_assert((FM / 2) % 2 == 0, "line pairs");
+    const bool lo = fr < 8;
+    const int64_t m0 = m - (lo ? 0 : 8), m1 = m0 + 8;
+#pragma unroll
+    for (int L = 0; L < FM / 4; ++L) {
+      const int ca = c + 2 * L * 32;
+      rq[2 * L][fn] = *reinterpret_cast<const uint4*>(res + m0 * p.cout + ca + (lo ? 0 : 32));
+      rq[2 * L + 1][fn] = *reinterpret_cast<const uint4*>(res + m1 * p.cout + ca + (lo ? 32 : 0));
+    }
+#else
 #pragma unroll
     for (int f2 = 0; f2 < FM / 2; ++f2) rq[f2][fn] = *reinterpret_cast<const uint4*>(res + m * p.cout + c + f2 * 32);
+#endif
   }
 }
 template <int FM, int FN>
-__device__ __forceinline__ void add_residual(f32x4 (&acc)[FM][FN], uint4 (&rq)[FM / 2][FN]) {
+__device__ __forceinline__ void add_residual(f32x4 (&acc)[FM][FN], uint4 (&rq)[FM / 2][FN], int fr) {
+#if DRNMI_EPI128
+  const bool lo = fr < 8;
+#pragma unroll
+  for (int L = 0; L < FM / 4; ++L)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      const uint4 d0 = rq[2 * L][fn], d1 = rq[2 * L + 1][fn];
+      const uint4 own = make_uint4(lo ? d0.x : d1.x, lo ? d0.y : d1.y, lo ? d0.z : d1.z, lo ? d0.w : d1.w);
+      const uint4 give = make_uint4(lo ? d1.x : d0.x, lo ? d1.y : d0.y, lo ? d1.z : d0.z, lo ? d1.w : d0.w);
+      uint4 r;
+      r.x = __builtin_amdgcn_update_dpp(0u, give.x, 0x128, 0xf, 0xf, false);
+      r.y = __builtin_amdgcn_update_dpp(0u, give.y, 0x128, 0xf, 0xf, false);
+      r.z = __builtin_amdgcn_update_dpp(0u, give.z, 0x128, 0xf, 0xf, false);
+      r.w = __builtin_amdgcn_update_dpp(0u, give.w, 0x128, 0xf, 0xf, false);
+      rq[2 * L][fn] = own;
+      rq[2 * L + 1][fn] = r;
+    }
+#endif
 #pragma unroll
   for (int f2 = 0; f2 < FM / 2; ++f2)
 #pragma unroll
@@ -192,6 +227,7 @@ __device__ __forceinline__ void store_tile_x4(const drnmi_conv_args& p, const f3
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
     const int64_t m = px0 + wp * 16 * FN + fn * 16 + fr;
+    uint4 o[FM / 2];
 #pragma unroll
     for (int f2 = 0; f2 < FM / 2; ++f2) {
       uint32_t w[4];
@@ -205,10 +241,35 @@ __device__ __forceinline__ void store_tile_x4(const drnmi_conv_args& p, const f3
         w[2 * h] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
         w[2 * h + 1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
       }
-      uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
-      swap_halves(o);
-      *reinterpret_cast<uint4*>(y + m * p.cout + c + f2 * 32) = o;
+      o[f2] = make_uint4(w[0], w[1], w[2], w[3]);
+      swap_halves(o[f2]);
     }
+#if DRNMI_EPI128
+    // whole 128-B lines: lanes fr and fr ^ 8 (DPP row_ror:8) trade their odd-group chunks, so one
+    // instruction writes groups (2 L, 2 L + 1) of pixels 0-7 and the next those of pixels 8-15
+    const bool lo = fr < 8;
+    const int64_t m0 = m - (lo ? 0 : 8), m1 = m0 + 8;
+#pragma unroll
+    for (int L = 0; L < FM / 4; ++L) {
+      const uint4 a = o[2 * L], b = o[2 * L + 1];
+      uint4 r;
+      r.x = __builtin_amdgcn_update_dpp(0u, b.x, 0x128, 0xf, 0xf, false);
+      r.y = __builtin_amdgcn_update_dpp(0u, b.y, 0x128, 0xf, 0xf, false);
+      r.z = __builtin_amdgcn_update_dpp(0u, b.z, 0x128, 0xf, 0xf, false);
+      r.w = __builtin_amdgcn_update_dpp(0u, b.w, 0x128, 0xf, 0xf, false);
+      const int ca = c + 2 * L * 32, cb = ca + 32;
+      const uint4 d0 = make_uint4(lo ? a.x : r.x, lo ? a.y : r.y, lo ? a.z : r.z, lo ? a.w : r.w);
+      const uint4 d1 = make_uint4(lo ? r.x : a.x, lo ? r.y : a.y, lo ? r.z : a.z, lo ? r.w : a.w);
+      uint16_t* y0 = y + m0 * p.cout + ca + (lo ? 0 : 32);
+      uint16_t* y1 = y + m1 * p.cout + ca + (lo ? 32 : 0);
+      *reinterpret_cast<uint4*>(y0) = d0;
+      *reinterpret_cast<uint4*>(y1) = d1;
+    }
+    if constexpr ((FM / 2) % 2 == 1) *reinterpret_cast<uint4*>(y + m * p.cout + c + (FM / 2 - 1) * 32) = o[FM / 2 - 1];
+#else
+#pragma unroll
+    for (int f2 = 0; f2 < FM / 2; ++f2) *reinterpret_cast<uint4*>(y + m * p.cout + c + f2 * 32) = o[f2];
+#endif
   }
 }
 template <int FM, int WCO, int FN = 4, bool DEFER = false>
@@ -366,6 +427,109 @@ __device__ __forceinline__ void store_tile_i8(const drnmi_conv_args& p, const i3
           else reinterpret_cast<float*>(p.y)[off] = v[j];
         }
       }
+    }
+  }
+}
+
+// store_tile_i8 for whole tiles of a dense int8 NHWC output (y_sc 1, y_sp cout): the same
+// per-element arithmetic, residual loads and output stores as 16-B pieces (common.h
+// transpose_rows4: row fq moves fragment 4 g + fq whole) instead of 4-B ones
+template <int FM, int WCO, int FN>
+__device__ __forceinline__ void store_tile_i8_x4(const drnmi_conv_args& p, const i32x4 (&acc)[FM][FN], int px0,
+                                                 int co0, int wc, int wp, int fr, int fq) {
+#pragma clang fp contract(off)
+  static_assert(FM % 4 == 0, "16-B int8 pieces");
+  constexpr int NG = FM / 4;                         // 64-B groups of the wave's channels per pixel
+  const int8_t* __restrict__ res = reinterpret_cast<const int8_t*>(p.res);
+  int8_t* __restrict__ y = reinterpret_cast<int8_t*>(p.y);
+  const int cbase = co0 + wc * WCO + fq * 16;
+  const bool lo = fr < 8;
+  // 128-B lines when the wave's channels span whole lines (NG even): groups (2 L, 2 L + 1) of
+  // pixels 0-7, then of pixels 8-15, lanes fr and fr ^ 8 trading the odd group (DPP row_ror:8)
+  constexpr bool LINES = DRNMI_EPI128 && NG % 2 == 0;
+  auto trade = [](uint4 v) {
+    uint4 r;
+    r.x = __builtin_amdgcn_update_dpp(0u, v.x, 0x128, 0xf, 0xf, false);
+    r.y = __builtin_amdgcn_update_dpp(0u, v.y, 0x128, 0xf, 0xf, false);
+    r.z = __builtin_amdgcn_update_dpp(0u, v.z, 0x128, 0xf, 0xf, false);
+    r.w = __builtin_amdgcn_update_dpp(0u, v.w, 0x128, 0xf, 0xf, false);
+    return r;
+  };
+  auto sel = [](bool c, uint4 a, uint4 b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+  };
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    const int64_t m = px0 + wp * 16 * FN + fn * 16 + fr;
+    const int64_t m0 = m - (lo ? 0 : 8), m1 = m0 + 8;
+    uint4 rq[NG];
+    if (res != nullptr) {
+      if constexpr (LINES) {
+#pragma unroll
+        for (int L = 0; L < NG / 2; ++L) {
+          const uint4 d0 = *reinterpret_cast<const uint4*>(res + m0 * p.cout + cbase + (2 * L + (lo ? 0 : 1)) * 64);
+          const uint4 d1 = *reinterpret_cast<const uint4*>(res + m1 * p.cout + cbase + (2 * L + (lo ? 1 : 0)) * 64);
+          rq[2 * L] = sel(lo, d0, d1);
+          rq[2 * L + 1] = trade(sel(lo, d1, d0));
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) rq[g] = *reinterpret_cast<const uint4*>(res + m * p.cout + cbase + g * 64);
+      }
+    }
+    uint4 out[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      uint32_t rr[4] = {0, 0, 0, 0};
+      if (res != nullptr) {
+        rr[0] = rq[g].x;
+        rr[1] = rq[g].y;
+        rr[2] = rq[g].z;
+        rr[3] = rq[g].w;
+        transpose_rows4(rr);
+      }
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int fm = 4 * g + k;
+        const int co = co0 + wc * WCO + fm * 16 + fq * 4;
+        const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);
+        const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+        float v[4];
+        v[0] = static_cast<float>(acc[fm][fn][0]) * sc.x + sh.x;
+        v[1] = static_cast<float>(acc[fm][fn][1]) * sc.y + sh.y;
+        v[2] = static_cast<float>(acc[fm][fn][2]) * sc.z + sh.z;
+        v[3] = static_cast<float>(acc[fm][fn][3]) * sc.w + sh.w;
+        if (res != nullptr) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v[j] = v[j] + static_cast<float>(static_cast<int8_t>((rr[k] >> (8 * j)) & 0xff)) * p.res_scale;
+        }
+        if (p.relu) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+        }
+        uint32_t w = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float t = fminf(fmaxf(rintf(v[j] * p.out_scale), -127.f), 127.f);
+          w |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(t)))) << (8 * j);
+        }
+        o[k] = w;
+      }
+      transpose_rows4(o);
+      out[g] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    if constexpr (LINES) {
+#pragma unroll
+      for (int L = 0; L < NG / 2; ++L) {
+        const uint4 r = trade(out[2 * L + 1]);
+        *reinterpret_cast<uint4*>(y + m0 * p.cout + cbase + (2 * L + (lo ? 0 : 1)) * 64) = sel(lo, out[2 * L], r);
+        *reinterpret_cast<uint4*>(y + m1 * p.cout + cbase + (2 * L + (lo ? 1 : 0)) * 64) = sel(lo, r, out[2 * L]);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) *reinterpret_cast<uint4*>(y + m * p.cout + cbase + g * 64) = out[g];
     }
   }
 }

@@ -29,4 +29,8 @@ const char* x6_conv_name(const drnmi_conv_args& p);
 // The strip tile with staggered SIMD partners (conv_stag.hip): 3x3 stride-1 bf16, wo % 256 == 0,
 // cin % 128 == 0 (conv_big.hip's dispatch checks the shape).
 hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s);
+// The seg classifier (1x1, cout <= 32, cin % 256 == 0; conv_seg.hip), bit-identical to conv_big's
+// BK-32 tile.
+bool seg_conv_supported(const drnmi_conv_args& p);
+int seg_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
 }  // namespace drnmi

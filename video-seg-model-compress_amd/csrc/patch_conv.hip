@@ -277,7 +277,7 @@ struct DmaCfg {
   static constexpr int NK = (K + 31) / 32;
   static constexpr int MF = COUT / 16;
   static constexpr int PFW = TR * TC / 16 / 4;                 // pixel fragments per wave
-  static constexpr int ST = PFW * MF;                          // stores per lane per tile
+  static constexpr int ST = PFW * (MF % 2 == 0 ? MF / 2 : MF);   // stores per lane per tile (16-B pieces for even MF)
   static constexpr int LDS = NB * PB;
   static_assert(TR * TC % 64 == 0, "tile must split over 4 waves");
 };
@@ -406,6 +406,7 @@ patch_dma_kernel(const drnmi_conv_args p) {
       const int oh = oh0 + idx / TC, ow = ow0 + idx % TC;
       const bool ok = oh < p.ho && ow < p.wo;
       const int64_t pix = (static_cast<int64_t>(n) * p.ho + oh) * p.wo + ow;
+      uint32_t w[C::MF][2];
 #pragma unroll
       for (int mf = 0; mf < C::MF; ++mf) {
         float v[4];
@@ -414,12 +415,30 @@ patch_dma_kernel(const drnmi_conv_args p) {
           v[j] = acc[mf][q][j] * sc[mf][j] + sh[mf][j];
           if (p.relu) v[j] = fmaxf(v[j], 0.f);
         }
-        u32x2_t o;
-        o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
-        o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
-        // every lane issues the store (out-of-range offset = dropped): constant vmcnt per tile
-        const unsigned yoff = ok ? static_cast<unsigned>((pix * COUT + mf * 16 + kq * 4) * 2) : 0xffffffffu;
-        __builtin_amdgcn_raw_buffer_store_b64(o, ys, yoff, 0, 0);
+        w[mf][0] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+        w[mf][1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+      }
+      // every lane issues the store (out-of-range offset = dropped): constant vmcnt per tile
+      if constexpr (C::MF % 2 == 0) {
+        // 16-B pieces: 64 contiguous bytes per pixel per instruction (common.h swap_halves)
+#pragma unroll
+        for (int f2 = 0; f2 < C::MF / 2; ++f2) {
+          uint4 o = make_uint4(w[2 * f2][0], w[2 * f2][1], w[2 * f2 + 1][0], w[2 * f2 + 1][1]);
+          swap_halves(o);
+          const unsigned yoff = ok ? static_cast<unsigned>((pix * COUT + f2 * 32 + chunk_of_row(kq) * 8) * 2) : 0xffffffffu;
+          typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+          const u32x4_t ov = {o.x, o.y, o.z, o.w};
+          __builtin_amdgcn_raw_buffer_store_b128(ov, ys, yoff, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int mf = 0; mf < C::MF; ++mf) {
+          u32x2_t o;
+          o.x = w[mf][0];
+          o.y = w[mf][1];
+          const unsigned yoff = ok ? static_cast<unsigned>((pix * COUT + mf * 16 + kq * 4) * 2) : 0xffffffffu;
+          __builtin_amdgcn_raw_buffer_store_b64(o, ys, yoff, 0, 0);
+        }
       }
     }
   }

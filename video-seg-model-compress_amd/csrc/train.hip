@@ -167,19 +167,51 @@ hipError_t launch_colred(RedArgs& r, hipStream_t s) {
   return hipGetLastError();
 }
 
-// finalize: one thread per channel, partials summed in split order.
+// finalize.  The G split partials of a channel were summed by one thread in split order: up to
+// 1024 dependent fp64 adds per channel on a handful of waves (120 us per BN layer in the
+// fine-tune profile, profiles/r2e_finetune_kernel_stats.csv).  Here a block owns 16 channels
+// (a 128-B row of partials per split, coalesced) and 16 threads per channel sum 16 contiguous
+// runs of splits, which are then added run by run: a fixed order, so the statistics stay
+// deterministic.
+constexpr int kFinCh = 16;
+__device__ __forceinline__ bool split_sums(const double* __restrict__ ws, int G, int C, int& c, double& s1,
+                                           double& s2) {
+  __shared__ double p1[kThreads], p2[kThreads];
+  const int t = threadIdx.x, tc = t % kFinCh, tg = t / kFinCh;
+  constexpr int NG = kThreads / kFinCh;
+  c = blockIdx.x * kFinCh + tc;
+  const int gs = (G + NG - 1) / NG;
+  const int g0 = tg * gs, g1 = g0 + gs < G ? g0 + gs : G;
+  double a1 = 0, a2 = 0;
+  if (c < C) {
+#pragma unroll 8
+    for (int g = g0; g < g1; ++g) {
+      a1 += ws[static_cast<int64_t>(g) * C + c];
+      a2 += ws[static_cast<int64_t>(G + g) * C + c];
+    }
+  }
+  p1[t] = a1;
+  p2[t] = a2;
+  __syncthreads();
+  if (t >= kFinCh || c >= C) return false;
+  s1 = 0;
+  s2 = 0;
+  for (int j = 0; j < NG; ++j) {
+    s1 += p1[j * kFinCh + tc];
+    s2 += p2[j * kFinCh + tc];
+  }
+  return true;
+}
+inline unsigned fin_grid(int C) { return static_cast<unsigned>((C + kFinCh - 1) / kFinCh); }
+
 __global__ void __launch_bounds__(kThreads)
 bn_stats_final_kernel(const double* __restrict__ ws, int G, int C, int64_t rows, float eps, float momentum,
                       float* __restrict__ mean, float* __restrict__ invstd, float* __restrict__ rmean,
                       float* __restrict__ rvar, int64_t* __restrict__ nbt) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt != nullptr) nbt[0] += 1;
-  if (c >= C) return;
-  double s1 = 0, s2 = 0;
-  for (int g = 0; g < G; ++g) {
-    s1 += ws[static_cast<int64_t>(g) * C + c];
-    s2 += ws[static_cast<int64_t>(G + g) * C + c];
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
+  int c;
+  double s1, s2;
+  if (!split_sums(ws, G, C, c, s1, s2)) return;
   const double m = s1 / static_cast<double>(rows);
   double var = s2 / static_cast<double>(rows) - m * m;
   if (var < 0) var = 0;
@@ -229,13 +261,9 @@ __global__ void __launch_bounds__(kThreads)
 bn_bwd_final_kernel(const double* __restrict__ ws, int G, int C, int64_t rows, const float* __restrict__ mean,
                     const float* __restrict__ invstd, const float* __restrict__ gamma, float* __restrict__ dgamma,
                     float* __restrict__ dbeta, int accumulate, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s1 = 0, s2 = 0;
-  for (int g = 0; g < G; ++g) {
-    s1 += ws[static_cast<int64_t>(g) * C + c];
-    s2 += ws[static_cast<int64_t>(G + g) * C + c];
-  }
+  int c;
+  double s1, s2;
+  if (!split_sums(ws, G, C, c, s1, s2)) return;
   const double is = invstd[c];
   const double sx = s2 - static_cast<double>(mean[c]) * s1;   // sum(dr * (y - mean))
   const float dg = static_cast<float>(is * sx);
@@ -313,6 +341,12 @@ constexpr int kWT = 64;      // tile rows / cols
 constexpr int kWM = 32;      // pixels per chunk
 constexpr int kWLD = kWM + 4;
 
+// X6 (fp32x fine-tune): the same tiles and chunks, each 32-pixel chunk one K step of
+// v_mfma_f32_16x16x32_bf16 on the exact 3-way bf16 splits of both operands (common.h split3),
+// the six products above 2^-24 in conv_x6's order -- fp32-class accuracy at the bf16 MFMA rate
+// (2.5 PF / 6 = 417 TF against the 157 TF of the f32 MFMA).  Lane (fr, fq) takes pixels
+// 8 fq .. 8 fq + 7 of the chunk for its A row and its B column alike, so the pairing over m holds.
+template <bool X6>
 __global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
   __shared__ __attribute__((aligned(16))) float As[2][kWT][kWLD];
   __shared__ __attribute__((aligned(16))) float Bs[2][kWT][kWLD];
@@ -393,6 +427,28 @@ __global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
   for (int64_t mc = m_begin; mc < m_end; mc += kWM) {
     const bool more = mc + kWM < m_end;
     if (more) load(mc + kWM);
+    if constexpr (X6) {
+      bf16x8 a[2][3], b[2][3];
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const float* ar = &As[buf][wr * 32 + f * 16 + fr][8 * fq];
+        const float* br = &Bs[buf][wcn * 32 + f * 16 + fr][8 * fq];
+        split3(*reinterpret_cast<const float4*>(ar), *reinterpret_cast<const float4*>(ar + 4), a[f][0], a[f][1], a[f][2]);
+        split3(*reinterpret_cast<const float4*>(br), *reinterpret_cast<const float4*>(br + 4), b[f][0], b[f][1], b[f][2]);
+      }
+#pragma unroll
+      for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+        for (int fj = 0; fj < 2; ++fj) {
+          f32x4& c = acc[fi][fj];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][2], b[fj][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][1], b[fj][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][0], b[fj][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][1], b[fj][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][0], b[fj][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][0], b[fj][0], c, 0, 0, 0);
+        }
+    } else {
 #pragma unroll
     for (int mm = 0; mm < kWM; mm += 16) {
       float4 a4[2], b4[2];
@@ -410,6 +466,7 @@ __global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
           acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].z, b4[fj].z, acc[fi][fj], 0, 0, 0);
           acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].w, b4[fj].w, acc[fi][fj], 0, 0, 0);
         }
+    }
     }
     if (more) store(buf ^ 1);
     __syncthreads();
@@ -771,7 +828,7 @@ extern "C" int drnmi_bn_stats_f32(const float* y, int64_t rows, int32_t C, float
   r.ws = reinterpret_cast<double*>(ws);
   hipError_t e = launch_colred<RED_STATS>(r, s);
   if (e != hipSuccess) return static_cast<int>(e);
-  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(grid_of(C)), dim3(kThreads), 0, s, r.ws, r.G, C, rows, eps,
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(fin_grid(C)), dim3(kThreads), 0, s, r.ws, r.G, C, rows, eps,
                      momentum, mean, invstd, running_mean, running_var, num_batches_tracked);
   return static_cast<int>(hipGetLastError());
 }
@@ -806,7 +863,7 @@ extern "C" int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float
   hipError_t e = launch_colred<RED_BNBWD>(r, s);
   if (e != hipSuccess) return static_cast<int>(e);
   float* coef = reinterpret_cast<float*>(r.ws + static_cast<int64_t>(2) * r.G * C);
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(grid_of(C)), dim3(kThreads), 0, s, r.ws, r.G, C, rows, mean, invstd,
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(fin_grid(C)), dim3(kThreads), 0, s, r.ws, r.G, C, rows, mean, invstd,
                      gamma, dgamma, dbeta, grad_accumulate, coef);
   e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
@@ -852,7 +909,7 @@ extern "C" int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* a) {
   return static_cast<int64_t>(splits) * a->cout * a->ks * a->ks * a->cin_stride * 4;
 }
 
-extern "C" int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* a, void* stream) {
+static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   const int rc = wgrad_check(a);
   if (rc != DRNMI_OK) return rc;
   if (a->dy == nullptr || a->x == nullptr || a->dw == nullptr || a->ws == nullptr) return DRNMI_EINVAL;
@@ -873,7 +930,8 @@ extern "C" int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* a, void* stream) {
   int splits;
   wgrad_plan(*a, &splits, &p.pix_per_split);
   const dim3 grid((p.K + kWT - 1) / kWT, (a->cout + kWT - 1) / kWT, splits);
-  hipLaunchKernelGGL(wgrad_kernel, grid, dim3(kThreads), 0, s, p);
+  if (x6) hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(kThreads), 0, s, p);
+  else hipLaunchKernelGGL(wgrad_kernel<false>, grid, dim3(kThreads), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
   const int64_t total = static_cast<int64_t>(a->cout) * a->cin * a->ks * a->ks;
@@ -881,6 +939,9 @@ extern "C" int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* a, void* stream) {
                      a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
   return static_cast<int>(hipGetLastError());
 }
+
+extern "C" int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* a, void* stream) { return wgrad_launch(a, false, stream); }
+extern "C" int drnmi_conv_wgrad_f32x3(const drnmi_wgrad_args* a, void* stream) { return wgrad_launch(a, true, stream); }
 
 extern "C" int drnmi_zero_insert_f32(const float* dy, int32_t n, int32_t ho, int32_t wo, int32_t c, int32_t stride,
                                      int32_t hu, int32_t wu, float* out, void* stream) {

@@ -92,6 +92,7 @@ SIGNATURES = {
     "drnmi_channel_sum_f32": (ctypes.c_int, [_VP, _I64, _I32, _I32, _VP, _I32, _VP, _VP]),
     "drnmi_conv_wgrad_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
     "drnmi_conv_wgrad_f32": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
+    "drnmi_conv_wgrad_f32x3": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
     "drnmi_zero_insert_f32": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     "drnmi_up8_lsm_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _F32, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
     "drnmi_up8_bilinear_lsm_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _F32, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),

@@ -22,7 +22,8 @@ Precision: fp32 (the reference trains in fp32; model.set_precision("fp32"), the 
 "fp32x": the forward and data-gradient convs with >= 32 input channels run on the fp32-accurate
 split-bf16 kernel (csrc/conv_x6.hip: exact 3-way bf16 split of weights and activations, the six
 products above 2^-24, fp32 accumulation, 2.5 PF / 6 peak) instead of the exact-f32 MFMA
-(157 TF); weight gradients, BN, the head and the small-channel convs stay exact fp32.
+(157 TF), and so do their weight gradients (drnmi_conv_wgrad_f32x3, the same split on dy and x);
+BN, the head and the small-channel convs stay exact fp32.
 Activations NHWC with a power-of-two channel stride, like the inference engine.  There is no
 CPU or ATen fallback.
 """
@@ -339,7 +340,11 @@ class TrainRunner:
                     raise RuntimeError(f"wgrad {nd.name}: bad geometry")
                 ws = self._ws("_wg_ws", nb, dev)
                 wa.ws, wa.ws_bytes = ws.data_ptr(), ws.numel()
-                _lib.check(lib.drnmi_conv_wgrad_f32(ctypes.byref(wa), sp), f"wgrad {nd.name}")
+                # fp32x: the convs with >= 32 input channels (those the forward runs on conv_x6)
+                # take the split-bf16 weight gradient too
+                wg = lib.drnmi_conv_wgrad_f32x3 if self.model.precision == "fp32x" and \
+                    self.cstride[nd.src] >= 32 else lib.drnmi_conv_wgrad_f32
+                _lib.check(wg(ctypes.byref(wa), sp), f"wgrad {nd.name}")
                 done.append(c.weight)
             if self.grad_ready is not None and done:
                 self.grad_ready(done)
