@@ -14,7 +14,9 @@
 #endif
 #ifndef DRNMI_STAG_ABL
 #define DRNMI_STAG_ABL 0    // diagnostic builds only: bit 0 drops the in-loop DMA, bit 1 the MFMAs,
-                            // bit 2 the fragment reads (registers keep stale values)
+                            // bit 2 the fragment reads (registers keep stale values), bit 3 the
+                            // MFMAs of 2 of the 8 16-row blocks per wave (the 25 % of 16 x 32
+                            // weight units a 16 x 16 BlockPruner mask at 50 % leaves all-zero)
 #endif
 #ifndef DRNMI_STAG_OLDINIT
 #define DRNMI_STAG_OLDINIT 0  // diagnostic: residual loaded and added before the prologue DMA (A/B)
@@ -307,6 +309,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
 #pragma unroll
         for (int fn = 0; fn < 4; ++fn)
           if constexpr ((DRNMI_STAG_ABL & 2) != 0) asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
+          else if ((DRNMI_STAG_ABL & 8) != 0 && h == 1 && (qg & 1) == 0) asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
           else acc[qg * 2 + h][fn] = K::mma(af[qg & 1][h], bfr[U][fn], acc[qg * 2 + h][fn]);
       if constexpr (U == 0) { if (qg < AI) issue_a(ta, STAGE ^ 1, qg); }
       if constexpr (KW == 0 && U == 1) { if (qg < 2) issue_next_strip(g, GP ^ 1, qg); }
