@@ -305,6 +305,9 @@ int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* args, void* stream);
  * bf16 split of dy and x, the six products above 2^-24 on the bf16 MFMA, fp32 accumulation);
  * same arguments, workspace and errors.  semantic_seg.py:166-230 backward. */
 int drnmi_conv_wgrad_f32x3(const drnmi_wgrad_args* args, void* stream);
+/* fp32 w[n] -> bf16 out[3][n] with w = out[0] + out[1] + out[2] exactly (round to nearest even at
+ * each step): the three weight planes of a DRNMI_F32X3 launch. */
+int drnmi_split3_bf16(const float* w, int64_t n, void* out, void* stream);
 
 /* out[n][y][x][c] = dy[n][y/s][x/s][c] where y, x are multiples of s (and inside dy), else 0;
  * out is [n][hu][wu][c] (c % 4 == 0).  Input of the stride-1 dgrad conv of a stride-s conv. */

@@ -764,13 +764,14 @@ constexpr int kStag = 15;   // conv_stag_kernel (tile id 19): the strip tile wit
 constexpr int kSeg = 16;    // conv_seg_kernel (tile id 20): the seg classifier, 1x1 to <= 32 classes
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-// auto-picked seg classifier launches (1x1, cout <= 32) run conv_seg_kernel (bit-identical to the
-// BK-32 tile); DRNMI_SEG=0 keeps them on conv_big (A/B runs)
+// the seg classifier (1x1, cout <= 32) stays on conv_big's BK-32 tile by default: conv_seg_kernel
+// (bit-identical) measured 80-84 vs 72 us on the D-22 batch-8 map (profiles/r5e_ab); DRNMI_SEG=1
+// routes it there (A/B runs)
 bool seg_enabled() {
   static int on = -1;
   if (on < 0) {
     const char* e = getenv("DRNMI_SEG");
-    on = (e != nullptr && e[0] == '0') ? 0 : 1;
+    on = (e != nullptr && e[0] == '1') ? 1 : 0;
   }
   return on == 1;
 }

@@ -16,7 +16,8 @@
 #define DRNMI_STAG_ABL 0    // diagnostic builds only: bit 0 drops the in-loop DMA, bit 1 the MFMAs,
                             // bit 2 the fragment reads (registers keep stale values), bit 3 the
                             // MFMAs of 2 of the 8 16-row blocks per wave (the 25 % of 16 x 32
-                            // weight units a 16 x 16 BlockPruner mask at 50 % leaves all-zero)
+                            // weight units a 16 x 16 BlockPruner mask at 50 % leaves all-zero),
+                            // bit 4 the MFMAs of a pseudo-random 25 % of those units
 #endif
 #ifndef DRNMI_STAG_OLDINIT
 #define DRNMI_STAG_OLDINIT 0  // diagnostic: residual loaded and added before the prologue DMA (A/B)
@@ -281,6 +282,10 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
       load_b(bfr[0], IG{}, IK{}, Z{});
       load_a(af[0], IS{}, Z{}, Z{});
     }
+    // DRNMI_STAG_ABL bit 4: a pseudo-random 25 % of the (16-row block, substep) units per wave
+    // skip their MFMAs (the dead-unit pattern of a random 50 % 16 x 16 BlockPruner mask)
+    const uint32_t abl_hash = __builtin_amdgcn_readfirstlane(
+        (static_cast<uint32_t>(wave + 1) * 2654435761u) ^ (static_cast<uint32_t>(t) * 40503u + U * 977u + 0x9e3779b9u) * 2246822519u);
     auto group_reads = [&](auto qg_c) {
       constexpr int QG = decltype(qg_c)::value;
       if constexpr (QG < GR - 1) {
@@ -310,6 +315,8 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
         for (int fn = 0; fn < 4; ++fn)
           if constexpr ((DRNMI_STAG_ABL & 2) != 0) asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
           else if ((DRNMI_STAG_ABL & 8) != 0 && h == 1 && (qg & 1) == 0) asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
+          else if ((DRNMI_STAG_ABL & 16) != 0 && ((abl_hash >> ((qg * 2 + h) * 2)) & 3u) == 0u)
+            asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
           else acc[qg * 2 + h][fn] = K::mma(af[qg & 1][h], bfr[U][fn], acc[qg * 2 + h][fn]);
       if constexpr (U == 0) { if (qg < AI) issue_a(ta, STAGE ^ 1, qg); }
       if constexpr (KW == 0 && U == 1) { if (qg < 2) issue_next_strip(g, GP ^ 1, qg); }

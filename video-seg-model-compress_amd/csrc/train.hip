@@ -940,6 +940,30 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   return static_cast<int>(hipGetLastError());
 }
 
+// fp32 [n] -> bf16 [3][n] planes, w = w1 + w2 + w3 (round to nearest even at each step): the weight
+// side of the fp32x arithmetic in one pass (drnmi/engine.py split3_bf16 took six ATen launches per
+// weight and step in the fp32x fine-tune)
+__global__ void __launch_bounds__(kThreads)
+split3_kernel(const float* __restrict__ w, int64_t n, bf16_t* __restrict__ out) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const float x = w[i];
+    const bf16_t a = f32_to_bf16(x);
+    const float r = x - bf16_to_f32(a);
+    const bf16_t b = f32_to_bf16(r);
+    out[i] = a;
+    out[n + i] = b;
+    out[2 * n + i] = f32_to_bf16(r - bf16_to_f32(b));
+  }
+}
+
+extern "C" int drnmi_split3_bf16(const float* w, int64_t n, void* out, void* stream) {
+  if (w == nullptr || out == nullptr || n <= 0) return DRNMI_EINVAL;
+  hipLaunchKernelGGL(split3_kernel, dim3(grid_of(n)), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream), w, n,
+                     reinterpret_cast<bf16_t*>(out));
+  return static_cast<int>(hipGetLastError());
+}
+
 extern "C" int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* a, void* stream) { return wgrad_launch(a, false, stream); }
 extern "C" int drnmi_conv_wgrad_f32x3(const drnmi_wgrad_args* a, void* stream) { return wgrad_launch(a, true, stream); }
 

@@ -93,6 +93,7 @@ SIGNATURES = {
     "drnmi_conv_wgrad_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
     "drnmi_conv_wgrad_f32": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
     "drnmi_conv_wgrad_f32x3": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
+    "drnmi_split3_bf16": (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP]),
     "drnmi_zero_insert_f32": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP]),
     "drnmi_up8_lsm_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _F32, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),
     "drnmi_up8_bilinear_lsm_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _F32, _I32, _I32, _I32, _I32, _VP, _VP, _VP]),

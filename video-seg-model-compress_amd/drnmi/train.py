@@ -159,8 +159,11 @@ class TrainRunner:
         (>= 32 input channels, k == k_pad); None keeps the launch on the exact-f32 kernel."""
         if self.model.precision != "fp32x" or cin_stride < 32 or k != k_pad:
             return None
-        from .engine import split3_bf16
-        return split3_bf16(wpk)
+        # one HIP pass (drnmi_split3_bf16), bit-identical to engine.split3_bf16
+        out = torch.empty((3,) + tuple(wpk.shape), dtype=torch.bfloat16, device=wpk.device)
+        _lib.check(_lib.load().drnmi_split3_bf16(_vp(wpk), wpk.numel(), _vp(out), _lib.stream_ptr(wpk.device)),
+                   "split3_bf16")
+        return out
 
     def _conv(self, x, cin_stride, h, w, wpk, k, k_pad, cout_pad, cout, ks, stride, pad, dil, y, y_strides,
               shift, res, n, ho, wo, stream, what, wx=None):
