@@ -337,6 +337,9 @@ struct WgradP {
   int64_t pix_per_split;
 };
 
+#ifndef DRNMI_WGRAD_MAP
+#define DRNMI_WGRAD_MAP 1    // 0: the 8-pixels-per-wave staging map (A/B)
+#endif
 constexpr int kWT = 64;      // tile rows / cols
 constexpr int kWM = 32;      // pixels per chunk
 constexpr int kWLD = kWM + 4;
@@ -359,8 +362,17 @@ __global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
   const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * p.pix_per_split;
   int64_t m_end = m_begin + p.pix_per_split;
   if (m_end > p.M) m_end = p.M;
+#if DRNMI_WGRAD_MAP
+  // the transposed LDS writes As[8 lv + j][lm] hit bank (4 j + lm) % 32 whatever lv is (rows are
+  // 36 floats, 8 rows = 288 = 0 mod 32): with 8 pixels x 8 column groups per wave every write was
+  // 8-way conflicted; 32 pixels per 32-lane half (lm = t % 32) makes them conflict-free, at 64 B
+  // per pixel per load instruction pair instead of 256 B
+  const int lm = t & 31;      // pixel row of the chunk this thread loads
+  const int lv = t >> 5;      // 8-column group
+#else
   const int lm = t >> 3;      // pixel row of the chunk this thread loads
   const int lv = t & 7;       // 8-column group
+#endif
   const int hw = p.ho * p.wo;
   // B column group: (tap, ci) fixed for the whole loop
   const int kcol = kc0 + 8 * lv;
