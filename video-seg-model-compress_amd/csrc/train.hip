@@ -350,7 +350,7 @@ constexpr int kWLD = kWM + 4;
 // (2.5 PF / 6 = 417 TF against the 157 TF of the f32 MFMA).  Lane (fr, fq) takes pixels
 // 8 fq .. 8 fq + 7 of the chunk for its A row and its B column alike, so the pairing over m holds.
 template <bool X6>
-__global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) wgrad_kernel(const WgradP p) {
   __shared__ __attribute__((aligned(16))) float As[2][kWT][kWLD];
   __shared__ __attribute__((aligned(16))) float Bs[2][kWT][kWLD];
   const int t = threadIdx.x;
@@ -383,9 +383,30 @@ __global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
   const int kw = kval ? tap - kh * p.ks : 0;
   const int co = co0 + 8 * lv;
 
-  float ra[8], rb[8];
-  auto load = [&](int64_t mc) {
-    const int64_t m = mc + lm;
+  // The thread's pixel advances by kWM per chunk: (n, oh, ow) are stepped, not divided out of m
+  // every chunk (an int64 division per chunk and thread), and two register sets keep two chunks
+  // of global loads in flight (chunk c + 2 loads while chunk c computes and chunk c + 1 is staged).
+  int64_t m_cur = m_begin + lm;
+  int p_n = 0, p_oh = 0, p_ow = 0;
+  {
+    const int mi = static_cast<int>(m_cur < p.M ? m_cur : 0);   // M < 2^31 (wgrad_check)
+    p_n = mi / hw;
+    const int q = mi - p_n * hw;
+    p_oh = q / p.wo;
+    p_ow = q - p_oh * p.wo;
+  }
+  auto load = [&](float (&ra)[8], float (&rb)[8]) {
+    const int64_t m = m_cur;
+    const int nn = p_n, oh = p_oh, ow = p_ow;
+    m_cur += kWM;
+    p_ow += kWM;
+    while (p_ow >= p.wo) {
+      p_ow -= p.wo;
+      if (++p_oh == p.ho) {
+        p_oh = 0;
+        ++p_n;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) { ra[j] = 0.f; rb[j] = 0.f; }
     if (m >= m_end) return;
@@ -401,10 +422,6 @@ __global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
         if (co + j < p.cout) ra[j] = dr[co + j];
     }
     if (kval) {
-      const int nn = static_cast<int>(m / hw);
-      const int q = static_cast<int>(m - static_cast<int64_t>(nn) * hw);
-      const int oh = q / p.wo;
-      const int ow = q - oh * p.wo;
       const int ih = oh * p.stride - p.pad + kh * p.dil;
       const int iw = ow * p.stride - p.pad + kw * p.dil;
       if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.w)) {
@@ -416,7 +433,7 @@ __global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
       }
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const float (&ra)[8], const float (&rb)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       As[buf][8 * lv + j][lm] = ra[j];
@@ -432,57 +449,71 @@ __global__ void __launch_bounds__(kThreads) wgrad_kernel(const WgradP p) {
 
   const int fr = lane & 15;
   const int fq = lane >> 4;
-  int buf = 0;
-  load(m_begin);
-  store(0);
-  __syncthreads();
-  for (int64_t mc = m_begin; mc < m_end; mc += kWM) {
-    const bool more = mc + kWM < m_end;
-    if (more) load(mc + kWM);
+  auto compute = [&](int buf) {
     if constexpr (X6) {
-      bf16x8 a[2][3], b[2][3];
+      // B splits first, then one A row block at a time (fewer live split registers: the kernel
+      // fits 128 VGPRs, four waves per SIMD, without spilling); same MFMA order per accumulator
+      bf16x8 b[2][3];
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
-        const float* ar = &As[buf][wr * 32 + f * 16 + fr][8 * fq];
         const float* br = &Bs[buf][wcn * 32 + f * 16 + fr][8 * fq];
-        split3(*reinterpret_cast<const float4*>(ar), *reinterpret_cast<const float4*>(ar + 4), a[f][0], a[f][1], a[f][2]);
         split3(*reinterpret_cast<const float4*>(br), *reinterpret_cast<const float4*>(br + 4), b[f][0], b[f][1], b[f][2]);
       }
 #pragma unroll
-      for (int fi = 0; fi < 2; ++fi)
+      for (int fi = 0; fi < 2; ++fi) {
+        bf16x8 a[3];
+        const float* ar = &As[buf][wr * 32 + fi * 16 + fr][8 * fq];
+        split3(*reinterpret_cast<const float4*>(ar), *reinterpret_cast<const float4*>(ar + 4), a[0], a[1], a[2]);
 #pragma unroll
         for (int fj = 0; fj < 2; ++fj) {
           f32x4& c = acc[fi][fj];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][2], b[fj][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][1], b[fj][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][0], b[fj][2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][1], b[fj][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][0], b[fj][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[fi][0], b[fj][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[fj][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[fj][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[fj][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][0], c, 0, 0, 0);
         }
+      }
     } else {
 #pragma unroll
-    for (int mm = 0; mm < kWM; mm += 16) {
-      float4 a4[2], b4[2];
+      for (int mm = 0; mm < kWM; mm += 16) {
+        float4 a4[2], b4[2];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        a4[f] = *reinterpret_cast<const float4*>(&As[buf][wr * 32 + f * 16 + fr][mm + 4 * fq]);
-        b4[f] = *reinterpret_cast<const float4*>(&Bs[buf][wcn * 32 + f * 16 + fr][mm + 4 * fq]);
-      }
-#pragma unroll
-      for (int fi = 0; fi < 2; ++fi)
-#pragma unroll
-        for (int fj = 0; fj < 2; ++fj) {
-          acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].x, b4[fj].x, acc[fi][fj], 0, 0, 0);
-          acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].y, b4[fj].y, acc[fi][fj], 0, 0, 0);
-          acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].z, b4[fj].z, acc[fi][fj], 0, 0, 0);
-          acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].w, b4[fj].w, acc[fi][fj], 0, 0, 0);
+        for (int f = 0; f < 2; ++f) {
+          a4[f] = *reinterpret_cast<const float4*>(&As[buf][wr * 32 + f * 16 + fr][mm + 4 * fq]);
+          b4[f] = *reinterpret_cast<const float4*>(&Bs[buf][wcn * 32 + f * 16 + fr][mm + 4 * fq]);
         }
+#pragma unroll
+        for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+          for (int fj = 0; fj < 2; ++fj) {
+            acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].x, b4[fj].x, acc[fi][fj], 0, 0, 0);
+            acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].y, b4[fj].y, acc[fi][fj], 0, 0, 0);
+            acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].z, b4[fj].z, acc[fi][fj], 0, 0, 0);
+            acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].w, b4[fj].w, acc[fi][fj], 0, 0, 0);
+          }
+      }
     }
-    }
-    if (more) store(buf ^ 1);
+  };
+
+  // chunk c computes from LDS buffer c & 1; set X holds chunk c + 1 (staged after the compute),
+  // set Y receives chunk c + 2 (its loads fly across the compute of c and the staging of c + 1)
+  float r0a[8], r0b[8], r1a[8], r1b[8];
+  load(r0a, r0b);
+  store(0, r0a, r0b);
+  load(r0a, r0b);                                   // chunk 1
+  __syncthreads();
+  for (int64_t mc = m_begin; mc < m_end; mc += 2 * kWM) {
+    load(r1a, r1b);                                 // chunk c + 2 (zeros past the end)
+    compute(0);
+    if (mc + kWM < m_end) store(1, r0a, r0b);
     __syncthreads();
-    buf ^= 1;
+    if (mc + kWM >= m_end) break;
+    load(r0a, r0b);                                 // chunk c + 3
+    compute(1);
+    if (mc + 2 * kWM < m_end) store(0, r1a, r1b);
+    __syncthreads();
   }
   // D[row = 4*(l/16) + r][col = l%16] of each 16x16 fragment; rows = co, cols = k
   float* out = p.ws + static_cast<int64_t>(blockIdx.z) * p.cout * p.K;

@@ -34,7 +34,7 @@ import ctypes
 import torch
 
 from . import _lib
-from .engine import COUT_ALIGN, K_ALIGN, _conv_out, _pow2_at_least, _round_up
+from .engine import COUT_ALIGN, K_ALIGN, X6_PATCH_SHAPES, _conv_out, _pow2_at_least, _round_up
 
 F32 = _lib.DRNMI_F32
 
@@ -46,10 +46,11 @@ def _vp(t):
 class _NodeState:
     """Per-node packed weights (forward / dgrad layouts) cached across steps."""
 
-    __slots__ = ("wf", "wd", "wfx", "wdx", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift")
+    __slots__ = ("wf", "wd", "wfx", "wdx", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift", "patch")
 
     def __init__(self):
         self.wf = self.wd = self.wfx = self.wdx = self.shift = None
+        self.patch = False
 
 
 class TrainRunner:
@@ -136,7 +137,11 @@ class TrainRunner:
             raise RuntimeError(f"{nd.name}: expected a contiguous fp32 weight")
         _lib.check(lib.drnmi_pack_conv_weight(_vp(w), cout, cin, ks, cs, st.cout_pad, st.k_pad, 0, None, F32,
                                               _vp(st.wf), stream), f"pack {nd.name}")
-        st.wfx = self._split(st.wf, cs, st.k, st.k_pad)
+        # fp32x: the full-resolution small-channel convs (stem, layer1, layer2 shapes) run on the
+        # split-bf16 patch kernels, as in the inference engine (engine.X6_PATCH_SHAPES)
+        st.patch = self.model.precision == "fp32x" and not nd.out_fp32_nchw and \
+            (cs, cout, ks, conv.stride[0], conv.dilation[0]) in X6_PATCH_SHAPES
+        st.wfx = self._split(st.wf, cs, st.k, st.k_pad, patch=st.patch)
         if conv.bias is not None:
             st.shift[:cout].copy_(conv.bias.detach())
 
@@ -154,10 +159,11 @@ class TrainRunner:
         st.wdx = self._split(st.wd, dys, st.kd, st.kd_pad)
         return dys
 
-    def _split(self, wpk, cin_stride, k, k_pad):
+    def _split(self, wpk, cin_stride, k, k_pad, patch=False):
         """fp32x: the three bf16 planes of a packed fp32 weight, for the convs conv_x6 takes
-        (>= 32 input channels, k == k_pad); None keeps the launch on the exact-f32 kernel."""
-        if self.model.precision != "fp32x" or cin_stride < 32 or k != k_pad:
+        (>= 32 input channels, k == k_pad) or the split-bf16 patch kernels take (`patch`); None
+        keeps the launch on the exact-f32 kernel."""
+        if self.model.precision != "fp32x" or (not patch and (cin_stride < 32 or k != k_pad)):
             return None
         # one HIP pass (drnmi_split3_bf16), bit-identical to engine.split3_bf16
         out = torch.empty((3,) + tuple(wpk.shape), dtype=torch.bfloat16, device=wpk.device)
@@ -166,7 +172,7 @@ class TrainRunner:
         return out
 
     def _conv(self, x, cin_stride, h, w, wpk, k, k_pad, cout_pad, cout, ks, stride, pad, dil, y, y_strides,
-              shift, res, n, ho, wo, stream, what, wx=None):
+              shift, res, n, ho, wo, stream, what, wx=None, algo=_lib.ALGO_IGEMM):
         a = _lib.ConvArgs()
         a.x, a.wgt, a.scale, a.shift = x.data_ptr(), (wx if wx is not None else wpk).data_ptr(), None, shift.data_ptr()
         a.res = res.data_ptr() if res is not None else None
@@ -180,7 +186,7 @@ class TrainRunner:
         a.dtype = a.out_dtype = F32
         if wx is not None:
             a.dtype = _lib.DRNMI_F32X3           # fp32x: conv_x6 (fp32 in/out, bf16 weight planes)
-        a.tile, a.algo = -1, _lib.ALGO_IGEMM
+        a.tile, a.algo = -1, algo
         _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), what)
 
     # ------------------------------------------------------------------ forward
@@ -220,7 +226,8 @@ class TrainRunner:
             rows = n * oh * ow
             y = torch.empty(rows, cs, dtype=torch.float32, device=dev)
             self._conv(vals[nd.src], cs_in, ih, iw, st.wf, st.k, st.k_pad, st.cout_pad, cout, ks, s, p, d,
-                       y, (oh * ow * cs, cs, 1), st.shift, None, n, oh, ow, stream, nd.name, st.wfx)
+                       y, (oh * ow * cs, cs, 1), st.shift, None, n, oh, ow, stream, nd.name, st.wfx,
+                       _lib.ALGO_PATCH if st.patch else _lib.ALGO_IGEMM)
             bn = nd.bn
             if bn.momentum is None or not bn.track_running_stats:
                 raise NotImplementedError("BatchNorm2d with momentum=None / no running stats")
