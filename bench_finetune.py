@@ -82,10 +82,11 @@ def train_flops(model, n, h, w):
 
 
 def step_t_star(model, n, h, w, precision):
-    """Roofline time of one step's convs at their kernels' MFMA peaks: forward and dgrad at the
-    fp32x rate (2.5 PF / 6) where conv_x6 runs them (>= 32 input channels), else the f32 MFMA
-    (157 TF); wgrad always f32."""
-    from drnmi.engine import _conv_out
+    """Roofline time of one step's convs at their kernels' MFMA peaks: in fp32x, forward, dgrad
+    and wgrad at the split-bf16 rate (2.5 PF / 6) where the HIP path runs them split (conv_x6 and
+    drnmi_conv_wgrad_f32x3 for >= 32 input channels, the X6 patch kernels for the stem / layer1 /
+    layer2 forward), else the f32 MFMA (157 TF)."""
+    from drnmi.engine import X6_PATCH_SHAPES, _conv_out, _pow2_at_least
     from drnmi.roofline import MFMA_PEAK  # noqa: F401
     shapes = {"input": (h, w)}
     t = 0.0
@@ -97,10 +98,13 @@ def step_t_star(model, n, h, w, precision):
         ow = _conv_out(iw, c.kernel_size[1], c.stride[1], c.padding[1], c.dilation[1])
         shapes[nd.dst] = (oh, ow)
         fl = 2.0 * n * oh * ow * c.out_channels * c.in_channels * c.kernel_size[0] * c.kernel_size[1]
-        t += fl / (x6 if precision == "fp32x" and c.in_channels >= 32 else f32)           # forward
+        cs = 8 if nd.src == "input" else _pow2_at_least(c.in_channels)
+        patch = (cs, c.out_channels, c.kernel_size[0], c.stride[0], c.dilation[0]) in X6_PATCH_SHAPES
+        fx = precision == "fp32x"
+        t += fl / (x6 if fx and (c.in_channels >= 32 or patch) else f32)                 # forward
         if nd.src != "input":
-            t += fl / (x6 if precision == "fp32x" and c.out_channels >= 32 else f32)      # dgrad
-        t += fl / f32                                                                      # wgrad
+            t += fl / (x6 if fx and c.out_channels >= 32 else f32)                        # dgrad
+        t += fl / (x6 if fx and cs >= 32 else f32)                                        # wgrad
     return t
 
 
@@ -215,7 +219,8 @@ def main():
                    "parallelism": f"dp{world} (bucketed SUM all-reduce overlapped with backward)"},
         "roofline": {"bound": "mfma", "kernel": "whole step (fwd + dgrad + wgrad convs, fp32 MFMA)"
                                                   if args.precision == "fp32" else
-                                                  "whole step (fwd + dgrad convs on conv_x6, wgrad fp32 MFMA)",
+                                                  "whole step (fwd, dgrad and wgrad convs split-bf16 where cin >= 32, "
+                                                  "small-channel fwd on the X6 patch kernels)",
                      "achieved": round(ach, 2), "peak": peak if args.precision == "fp32" else round(fl / t_star / 1e12, 2),
                      "unit": "TFLOP/s", "frac": round(t_star / (el / args.steps), 4),
                      "traffic": None, "step_tflop": round(fl / 1e12, 3),
