@@ -268,7 +268,8 @@ int drnmi_bn_stats_f32(const float* y, int64_t rows, int32_t C, float eps, float
                        int64_t* num_batches_tracked, void* ws, void* stream);
 
 /* z = relu?(((y - mean) * invstd) * gamma + beta [+ res]) over [rows][C]; gamma/beta/res NULL-able.
- * (BasicBlock / Bottleneck tail: lmodels/drn.py:49-65, :86-106.) */
+ * (BasicBlock / Bottleneck tail: lmodels/drn.py:49-65, :86-106.)  mean/invstd/gamma/beta must be
+ * 16-byte aligned (DRNMI_EINVAL otherwise). */
 int drnmi_bn_act_f32(const float* y, const float* mean, const float* invstd, const float* gamma,
                      const float* beta, const float* res, int32_t relu, int64_t rows, int32_t C,
                      float* z, void* stream);
@@ -276,7 +277,7 @@ int drnmi_bn_act_f32(const float* y, const float* mean, const float* invstd, con
 /* Backward of drnmi_bn_act_f32 (train-mode BN): dr = dz * (relu ? z > 0 : 1);
  * dbeta = sum dr, dgamma = sum dr * xhat; dy = gamma*invstd*(dr - mean(dr) - xhat*mean(dr*xhat));
  * dres (NULL-able) = dr (or += dr with dres_accumulate).  dy may alias dz.
- * grad_accumulate: dgamma/dbeta += instead of =. */
+ * grad_accumulate: dgamma/dbeta += instead of =.  mean must be 16-byte aligned. */
 int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float* y, const float* mean,
                          const float* invstd, const float* gamma, int32_t relu, int64_t rows,
                          int32_t C, float* dy, float* dres, int32_t dres_accumulate, float* dgamma,

@@ -172,7 +172,7 @@ def test_eval_after_train_uses_new_weights():
 
 
 # ------------------------------------------------------------------ kernel-level checks
-def _wgrad(dy_nhwc, x_nhwc, cin, cout, ks, stride, pad, dil, ho, wo, accumulate=None):
+def _wgrad(dy_nhwc, x_nhwc, cin, cout, ks, stride, pad, dil, ho, wo, accumulate=None, x6=False):
     from drnmi import _lib
     lib = _lib.load()
     n, h, w, cs = x_nhwc.shape
@@ -186,7 +186,8 @@ def _wgrad(dy_nhwc, x_nhwc, cin, cout, ks, stride, pad, dil, ho, wo, accumulate=
     nb = lib.drnmi_conv_wgrad_workspace_bytes(ctypes.byref(a))
     ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
     a.ws, a.ws_bytes = ws.data_ptr(), nb
-    _lib.check(lib.drnmi_conv_wgrad_f32(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "wgrad")
+    fn = lib.drnmi_conv_wgrad_f32x3 if x6 else lib.drnmi_conv_wgrad_f32
+    _lib.check(fn(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "wgrad")
     return dw
 
 
@@ -197,8 +198,12 @@ def _wgrad(dy_nhwc, x_nhwc, cin, cout, ks, stride, pad, dil, ho, wo, accumulate=
     (128, 128, 256, 256, 1, 2, 0, 1, 18, 16),
     (512, 512, 19, 32, 1, 1, 0, 1, 12, 10),
     (256, 256, 512, 512, 3, 1, 4, 4, 16, 16),
+    (96, 128, 200, 256, 3, 1, 1, 1, 13, 17),
 ])
-def test_wgrad_kernel_matches_torch(cin, cs, cout, dys, ks, stride, pad, dil, h, w):
+@pytest.mark.parametrize("x6", [False, True])
+def test_wgrad_kernel_matches_torch(cin, cs, cout, dys, ks, stride, pad, dil, h, w, x6):
+    """fp32 wgrad and the fp32x split-bf16 one (drnmi_conv_wgrad_f32x3: the 64 x 64 tile, and the
+    128 x 128 tile where cout and K >= 128, ragged cout / pixel counts included) vs torch autograd."""
     torch.manual_seed(cin + cout)
     n = 2
     x = torch.randn(n, cin, h, w)
@@ -211,11 +216,11 @@ def test_wgrad_kernel_matches_torch(cin, cs, cout, dys, ks, stride, pad, dil, h,
     xn[..., :cin] = x.permute(0, 2, 3, 1)
     gn = torch.zeros(n, ho, wo, dys)
     gn[..., :cout] = g.permute(0, 2, 3, 1)
-    dw = _wgrad(gn.to(DEV).contiguous(), xn.to(DEV).contiguous(), cin, cout, ks, stride, pad, dil, ho, wo)
+    dw = _wgrad(gn.to(DEV).contiguous(), xn.to(DEV).contiguous(), cin, cout, ks, stride, pad, dil, ho, wo, x6=x6)
     torch.cuda.synchronize()
     assert TC.rel_err(dw.cpu().numpy(), wt.grad.numpy()) <= 1e-4
     dw2 = _wgrad(gn.to(DEV).contiguous(), xn.to(DEV).contiguous(), cin, cout, ks, stride, pad, dil, ho, wo,
-                 accumulate=dw)
+                 accumulate=dw, x6=x6)
     assert TC.rel_err(dw2.cpu().numpy(), 2 * wt.grad.numpy()) <= 1e-4
 
 

@@ -236,12 +236,15 @@ bn_act_kernel(const float* __restrict__ y, const float* __restrict__ mean, const
     const int c = static_cast<int>((i * 4) & (C - 1));
     const float4 v = reinterpret_cast<const float4*>(y)[i];
     float o[4] = {v.x, v.y, v.z, v.w};
+    // per-channel terms as 16-B loads (c % 4 == 0)
+    const float4 m4 = *reinterpret_cast<const float4*>(mean + c);
+    const float4 s4 = *reinterpret_cast<const float4*>(invstd + c);
+    const float4 g4 = gamma != nullptr ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    const float4 b4 = beta != nullptr ? *reinterpret_cast<const float4*>(beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float cm[4] = {m4.x, m4.y, m4.z, m4.w}, cs[4] = {s4.x, s4.y, s4.z, s4.w};
+    const float cg[4] = {g4.x, g4.y, g4.z, g4.w}, cb[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float g = gamma != nullptr ? gamma[c + j] : 1.f;
-      const float b = beta != nullptr ? beta[c + j] : 0.f;
-      o[j] = ((o[j] - mean[c + j]) * invstd[c + j]) * g + b;
-    }
+    for (int j = 0; j < 4; ++j) o[j] = ((o[j] - cm[j]) * cs[j]) * cg[j] + cb[j];
     if (res != nullptr) {
       const float4 rv = reinterpret_cast<const float4*>(res)[i];
       o[0] += rv.x; o[1] += rv.y; o[2] += rv.z; o[3] += rv.w;
@@ -294,10 +297,16 @@ bn_bwd_apply_kernel(const float* dz, const float* __restrict__ z, const float* _
     }
     const float4 yv = reinterpret_cast<const float4*>(y)[i];
     const float yy[4] = {yv.x, yv.y, yv.z, yv.w};
+    // per-channel terms as 16-B loads (c % 4 == 0; coef's three rows are C floats each)
+    const float4 a4 = *reinterpret_cast<const float4*>(coef + c);
+    const float4 b4 = *reinterpret_cast<const float4*>(coef + C + c);
+    const float4 d4 = *reinterpret_cast<const float4*>(coef + 2 * C + c);
+    const float4 m4 = *reinterpret_cast<const float4*>(mean + c);
+    const float ca[4] = {a4.x, a4.y, a4.z, a4.w}, cb[4] = {b4.x, b4.y, b4.z, b4.w};
+    const float cd[4] = {d4.x, d4.y, d4.z, d4.w}, cm[4] = {m4.x, m4.y, m4.z, m4.w};
     float o[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      o[j] = coef[c + j] * (dr[j] - coef[C + c + j] - (yy[j] - mean[c + j]) * coef[2 * C + c + j]);
+    for (int j = 0; j < 4; ++j) o[j] = ca[j] * (dr[j] - cb[j] - (yy[j] - cm[j]) * cd[j]);
     if (dres != nullptr) {
       float4 rv = make_float4(dr[0], dr[1], dr[2], dr[3]);
       if (dres_acc) {
@@ -337,6 +346,9 @@ struct WgradP {
   int64_t pix_per_split;
 };
 
+#ifndef DRNMI_WGRAD_BIG
+#define DRNMI_WGRAD_BIG 1    // fp32x: the 128 x 128 wgrad tile where cout and K >= 128 (0: 64 x 64 only, A/B)
+#endif
 #ifndef DRNMI_WGRAD_MAP
 #define DRNMI_WGRAD_MAP 1    // 0: the 8-pixels-per-wave staging map (A/B)
 #endif
@@ -526,6 +538,160 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int c = co0 + wr * 32 + fi * 16 + 4 * fq + r;
+        if (c < p.cout) out[static_cast<int64_t>(c) * p.K + k] = acc[fi][fj][r];
+      }
+    }
+}
+
+// The fp32x weight gradient on a 128 co x 128 k tile (cout and K >= 128): four waves of 64 x 64
+// (4 x 4 fragments), so every staged byte feeds twice the MFMAs of the 64 x 64 tile.  Same chunks,
+// staging map (32 pixels per 32-lane half: conflict-free transposed writes), two register sets of
+// loads in flight, split order and MFMA order per accumulator as wgrad_kernel<true>; the split of a
+// B fragment is done once per chunk and reused by the wave's four row blocks.  Two workgroups per
+// CU (2 x 2 x 128 x 36 floats of LDS each).
+constexpr int kWT2 = 128;
+__global__ void __launch_bounds__(kThreads) wgrad_x6_big_kernel(const WgradP p) {
+  __shared__ __attribute__((aligned(16))) float As[2][kWT2][kWLD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kWT2][kWLD];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wr = wave >> 1, wcn = wave & 1;
+  const int co0 = blockIdx.y * kWT2;
+  const int kc0 = blockIdx.x * kWT2;
+  const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * p.pix_per_split;
+  int64_t m_end = m_begin + p.pix_per_split;
+  if (m_end > p.M) m_end = p.M;
+  const int lm = t & 31;      // pixel row of the chunk this thread loads
+  const int lv = t >> 5;      // 16-column group
+  const int hw = p.ho * p.wo;
+  const int kcol = kc0 + 16 * lv;                  // 16 consecutive k stay in one tap (cs % 16 == 0)
+  const int tap = kcol / p.cs;
+  const int ci = kcol - tap * p.cs;
+  const bool kval = kcol < p.K && tap < p.ks * p.ks;
+  const int kh = kval ? tap / p.ks : 0;
+  const int kw = kval ? tap - kh * p.ks : 0;
+  const int co = co0 + 16 * lv;
+
+  int64_t m_cur = m_begin + lm;
+  int p_n = 0, p_oh = 0, p_ow = 0;
+  {
+    const int mi = static_cast<int>(m_cur < p.M ? m_cur : 0);
+    p_n = mi / hw;
+    const int q = mi - p_n * hw;
+    p_oh = q / p.wo;
+    p_ow = q - p_oh * p.wo;
+  }
+  auto load = [&](float4 (&ra)[4], float4 (&rb)[4]) {
+    const int64_t m = m_cur;
+    const int nn = p_n, oh = p_oh, ow = p_ow;
+    m_cur += kWM;
+    p_ow += kWM;
+    while (p_ow >= p.wo) {
+      p_ow -= p.wo;
+      if (++p_oh == p.ho) {
+        p_oh = 0;
+        ++p_n;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ra[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      rb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (m >= m_end) return;
+    const float* dr = p.dy + m * p.dys;
+    if (co + 16 <= p.dys && co + 16 <= p.cout) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ra[j] = *reinterpret_cast<const float4*>(dr + co + 4 * j);
+    } else {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = co + j < p.cout ? dr[co + j] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ra[j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    }
+    if (kval) {
+      const int ih = oh * p.stride - p.pad + kh * p.dil;
+      const int iw = ow * p.stride - p.pad + kw * p.dil;
+      if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.w)) {
+        const float* xr = p.x + ((static_cast<int64_t>(nn) * p.h + ih) * p.w + iw) * p.cs + ci;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rb[j] = *reinterpret_cast<const float4*>(xr + 4 * j);
+      }
+    }
+  };
+  auto store = [&](int buf, const float4 (&ra)[4], const float4 (&rb)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float av[4] = {ra[j].x, ra[j].y, ra[j].z, ra[j].w};
+      const float bv[4] = {rb[j].x, rb[j].y, rb[j].z, rb[j].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        As[buf][16 * lv + 4 * j + e][lm] = av[e];
+        Bs[buf][16 * lv + 4 * j + e][lm] = bv[e];
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  auto compute = [&](int buf) {
+    bf16x8 b[4][3];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const float* br = &Bs[buf][wcn * 64 + f * 16 + fr][8 * fq];
+      split3(*reinterpret_cast<const float4*>(br), *reinterpret_cast<const float4*>(br + 4), b[f][0], b[f][1], b[f][2]);
+    }
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) {
+      bf16x8 a[3];
+      const float* ar = &As[buf][wr * 64 + fi * 16 + fr][8 * fq];
+      split3(*reinterpret_cast<const float4*>(ar), *reinterpret_cast<const float4*>(ar + 4), a[0], a[1], a[2]);
+#pragma unroll
+      for (int fj = 0; fj < 4; ++fj) {
+        f32x4& c = acc[fi][fj];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[fj][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[fj][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[fj][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][0], c, 0, 0, 0);
+      }
+    }
+  };
+
+  float4 r0a[4], r0b[4], r1a[4], r1b[4];
+  load(r0a, r0b);
+  store(0, r0a, r0b);
+  load(r0a, r0b);
+  __syncthreads();
+  for (int64_t mc = m_begin; mc < m_end; mc += 2 * kWM) {
+    load(r1a, r1b);
+    compute(0);
+    if (mc + kWM < m_end) store(1, r0a, r0b);
+    __syncthreads();
+    if (mc + kWM >= m_end) break;
+    load(r0a, r0b);
+    compute(1);
+    if (mc + 2 * kWM < m_end) store(0, r1a, r1b);
+    __syncthreads();
+  }
+  float* out = p.ws + static_cast<int64_t>(blockIdx.z) * p.cout * p.K;
+#pragma unroll
+  for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+    for (int fj = 0; fj < 4; ++fj) {
+      const int k = kc0 + wcn * 64 + fj * 16 + fr;
+      if (k >= p.K) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = co0 + wr * 64 + fi * 16 + 4 * fq + r;
         if (c < p.cout) out[static_cast<int64_t>(c) * p.K + k] = acc[fi][fj][r];
       }
     }
@@ -881,6 +1047,10 @@ extern "C" int drnmi_bn_act_f32(const float* y, const float* mean, const float* 
                                 float* z, void* stream) {
   if (y == nullptr || mean == nullptr || invstd == nullptr || z == nullptr || rows <= 0 || !pow2_ge4(C))
     return DRNMI_EINVAL;
+  // the per-channel vectors are read as 16-B pieces
+  if ((reinterpret_cast<uintptr_t>(mean) | reinterpret_cast<uintptr_t>(invstd) | reinterpret_cast<uintptr_t>(gamma) |
+       reinterpret_cast<uintptr_t>(beta)) & 15)
+    return DRNMI_EINVAL;
   const int64_t n4 = rows * C / 4;
   hipLaunchKernelGGL(bn_act_kernel, dim3(grid_of(n4)), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
                      y, mean, invstd, gamma, beta, res, relu, n4, C, z);
@@ -894,6 +1064,7 @@ extern "C" int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float
   if (dz == nullptr || y == nullptr || mean == nullptr || invstd == nullptr || dy == nullptr || ws == nullptr ||
       rows <= 0 || !pow2_ge4(C) || (relu && z == nullptr))
     return DRNMI_EINVAL;
+  if (reinterpret_cast<uintptr_t>(mean) & 15) return DRNMI_EINVAL;   // read as 16-B pieces
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   RedArgs r{};
   r.a = dz;
@@ -973,8 +1144,14 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   int splits;
   wgrad_plan(*a, &splits, &p.pix_per_split);
   const dim3 grid((p.K + kWT - 1) / kWT, (a->cout + kWT - 1) / kWT, splits);
-  if (x6) hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(kThreads), 0, s, p);
-  else hipLaunchKernelGGL(wgrad_kernel<false>, grid, dim3(kThreads), 0, s, p);
+  if (x6 && DRNMI_WGRAD_BIG && a->cout >= kWT2 && p.K >= kWT2 && p.cs % 16 == 0) {
+    const dim3 g2((p.K + kWT2 - 1) / kWT2, (a->cout + kWT2 - 1) / kWT2, splits);   // same splits: same workspace
+    hipLaunchKernelGGL(wgrad_x6_big_kernel, g2, dim3(kThreads), 0, s, p);
+  } else if (x6) {
+    hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(kThreads), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(wgrad_kernel<false>, grid, dim3(kThreads), 0, s, p);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
   const int64_t total = static_cast<int64_t>(a->cout) * a->cin * a->ks * a->ks;
