@@ -701,17 +701,20 @@ __global__ void __launch_bounds__(kThreads) wgrad_x6_big_kernel(const WgradP p) 
 __global__ void __launch_bounds__(kThreads)
 wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin, int cs, int ks, int K,
                     float* __restrict__ dw, int acc) {
-  const int64_t total = static_cast<int64_t>(cout) * cin * ks * ks;
+  // threads walk the partials' own [co][k] order (k = tap * cs + ci), so each of the `splits`
+  // reads is coalesced (walking dw's OIHW order read them ks*ks*... apart); dw is written once
+  const int64_t total = static_cast<int64_t>(cout) * K;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int kw = static_cast<int>(i % ks);
-    const int kh = static_cast<int>((i / ks) % ks);
-    const int ci = static_cast<int>((i / (ks * ks)) % cin);
-    const int co = static_cast<int>(i / (static_cast<int64_t>(ks) * ks * cin));
-    const int64_t off = static_cast<int64_t>(co) * K + (kh * ks + kw) * cs + ci;
+    const int co = static_cast<int>(i / K);
+    const int k = static_cast<int>(i - static_cast<int64_t>(co) * K);
+    const int tap = k / cs;
+    const int ci = k - tap * cs;
+    if (ci >= cin) continue;
     float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += ws[static_cast<int64_t>(z) * cout * K + off];
-    dw[i] = acc ? dw[i] + s : s;
+    for (int z = 0; z < splits; ++z) s += ws[static_cast<int64_t>(z) * cout * K + i];
+    const int64_t o = (static_cast<int64_t>(co) * cin + ci) * ks * ks + tap;   // tap = kh * ks + kw
+    dw[o] = acc ? dw[o] + s : s;
   }
 }
 
@@ -1154,7 +1157,7 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
-  const int64_t total = static_cast<int64_t>(a->cout) * a->cin * a->ks * a->ks;
+  const int64_t total = static_cast<int64_t>(a->cout) * p.K;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_of(total)), dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin,
                      a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
   return static_cast<int>(hipGetLastError());
