@@ -39,8 +39,8 @@ def parse():
     ap.add_argument("--width", type=int, default=768)
     ap.add_argument("--no-prune", action="store_true")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32x"],
-                    help="fp32x: forward and data-gradient convs with >= 32 input channels on the "
-                         "fp32-accurate split-bf16 kernel (conv_x6); wgrad, BN and the head stay exact fp32")
+                    help="fp32x: the convs (forward, data and weight gradients) on the fp32-accurate "
+                         "split-bf16 kernels (conv_x6, X6 patch kernels, wgrad_f32x3); BN and the head stay exact fp32")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -84,8 +84,8 @@ def train_flops(model, n, h, w):
 def step_t_star(model, n, h, w, precision):
     """Roofline time of one step's convs at their kernels' MFMA peaks: in fp32x, forward, dgrad
     and wgrad at the split-bf16 rate (2.5 PF / 6) where the HIP path runs them split (conv_x6 and
-    drnmi_conv_wgrad_f32x3 for >= 32 input channels, the X6 patch kernels for the stem / layer1 /
-    layer2 forward), else the f32 MFMA (157 TF)."""
+    every drnmi_conv_wgrad_f32x3, the X6 patch kernels for the stem / layer1 / layer2 forward and
+    the layer1 data gradient), else the f32 MFMA (157 TF)."""
     from drnmi.engine import X6_PATCH_SHAPES, _conv_out, _pow2_at_least
     from drnmi.roofline import MFMA_PEAK  # noqa: F401
     shapes = {"input": (h, w)}
@@ -103,8 +103,10 @@ def step_t_star(model, n, h, w, precision):
         fx = precision == "fp32x"
         t += fl / (x6 if fx and (c.in_channels >= 32 or patch) else f32)                 # forward
         if nd.src != "input":
-            t += fl / (x6 if fx and c.out_channels >= 32 else f32)                        # dgrad
-        t += fl / (x6 if fx and cs >= 32 else f32)                                        # wgrad
+            dpatch = (_pow2_at_least(c.out_channels), c.in_channels, c.kernel_size[0], 1,
+                      c.dilation[0]) in X6_PATCH_SHAPES
+            t += fl / (x6 if fx and (c.out_channels >= 32 or dpatch) else f32)            # dgrad
+        t += fl / (x6 if fx else f32)                                                     # wgrad
     return t
 
 
@@ -219,8 +221,8 @@ def main():
                    "parallelism": f"dp{world} (bucketed SUM all-reduce overlapped with backward)"},
         "roofline": {"bound": "mfma", "kernel": "whole step (fwd + dgrad + wgrad convs, fp32 MFMA)"
                                                   if args.precision == "fp32" else
-                                                  "whole step (fwd, dgrad and wgrad convs split-bf16 where cin >= 32, "
-                                                  "small-channel fwd on the X6 patch kernels)",
+                                                  "whole step (fwd and dgrad convs split-bf16 where cin >= 32 or on "
+                                                  "the X6 patch kernels, every wgrad split-bf16)",
                      "achieved": round(ach, 2), "peak": peak if args.precision == "fp32" else round(fl / t_star / 1e12, 2),
                      "unit": "TFLOP/s", "frac": round(t_star / (el / args.steps), 4),
                      "traffic": None, "step_tflop": round(fl / 1e12, 3),

@@ -473,6 +473,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
       }
 #pragma unroll
       for (int fi = 0; fi < 2; ++fi) {
+        if (co0 + wr * 32 + fi * 16 >= p.cout) continue;   // rows past cout (16- and 32-channel layers)
         bf16x8 a[3];
         const float* ar = &As[buf][wr * 32 + fi * 16 + fr][8 * fq];
         split3(*reinterpret_cast<const float4*>(ar), *reinterpret_cast<const float4*>(ar + 4), a[0], a[1], a[2]);
@@ -497,7 +498,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
           b4[f] = *reinterpret_cast<const float4*>(&Bs[buf][wcn * 32 + f * 16 + fr][mm + 4 * fq]);
         }
 #pragma unroll
-        for (int fi = 0; fi < 2; ++fi)
+        for (int fi = 0; fi < 2; ++fi) {
+          if (co0 + wr * 32 + fi * 16 >= p.cout) continue;
 #pragma unroll
           for (int fj = 0; fj < 2; ++fj) {
             acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].x, b4[fj].x, acc[fi][fj], 0, 0, 0);
@@ -505,6 +507,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
             acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].z, b4[fj].z, acc[fi][fj], 0, 0, 0);
             acc[fi][fj] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[fi].w, b4[fj].w, acc[fi][fj], 0, 0, 0);
           }
+        }
       }
     }
   };
@@ -718,21 +721,44 @@ wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin,
   }
 }
 
-void wgrad_plan(const drnmi_wgrad_args& a, int* splits, int64_t* per) {
+// The pixel range is split so that the launch fills the chip: at least two rounds of the resident
+// workgroup slots, and among lo .. 4 lo splits the count whose last round is fullest (the first
+// rule alone put D-54 layer7.0's 576 big tiles on 512 slots at one split: 1.125 rounds, the
+// second round 1/8 full, 4.6 ms of a 52.8 ms fine-tune step).  Every split holds >= 512 pixels.
+static bool wgrad_big_ok(const drnmi_wgrad_args& a) {
   const int K = a.ks * a.ks * a.cin_stride;
+  return DRNMI_WGRAD_BIG && a.cout >= kWT2 && K >= kWT2 && a.cin_stride % 16 == 0;
+}
+
+static void wgrad_plan(const drnmi_wgrad_args& a, bool big, int* splits, int64_t* per) {
+  const int K = a.ks * a.ks * a.cin_stride;
+  const int tile = big ? kWT2 : kWT;
+  const int64_t slots = big ? 2 * 256 : 4 * 256;     // resident workgroups: LDS 73.7 KB / 36.9 KB each
   const int64_t M = static_cast<int64_t>(a.n) * a.ho * a.wo;
-  const int64_t tiles = static_cast<int64_t>((a.cout + kWT - 1) / kWT) * ((K + kWT - 1) / kWT);
-  int64_t s = 2048 / tiles;
-  const int64_t by_pix = (M + 511) / 512;
-  if (s > by_pix) s = by_pix;
-  if (s > 512) s = 512;
-  if (s < 1) s = 1;
-  int64_t pp = (M + s - 1) / s;
-  pp = (pp + kWM - 1) / kWM * kWM;
-  s = (M + pp - 1) / pp;
-  if (s < 1) s = 1;
-  *splits = static_cast<int>(s);
-  *per = pp;
+  const int64_t tiles = static_cast<int64_t>((a.cout + tile - 1) / tile) * ((K + tile - 1) / tile);
+  int64_t smax = (M + 511) / 512;
+  if (smax > 512) smax = 512;
+  if (smax < 1) smax = 1;
+  int64_t lo = (2 * slots + tiles - 1) / tiles;
+  if (lo > smax) lo = smax;
+  int64_t hi = 4 * lo < smax ? 4 * lo : smax;
+  int64_t best_s = 0, best_pp = 0;
+  double best_eff = -1.0;
+  for (int64_t s = lo; s <= hi; ++s) {
+    int64_t pp = (M + s - 1) / s;
+    pp = (pp + kWM - 1) / kWM * kWM;
+    const int64_t sa = (M + pp - 1) / pp;
+    const int64_t wgs = tiles * sa;
+    const int64_t rounds = (wgs + slots - 1) / slots;
+    const double eff = static_cast<double>(wgs) / static_cast<double>(rounds * slots);
+    if (eff > best_eff + 0.02) {     // a larger split count only for a clearly fuller last round
+      best_eff = eff;
+      best_s = sa;
+      best_pp = pp;
+    }
+  }
+  *splits = static_cast<int>(best_s);
+  *per = best_pp;
 }
 
 // ------------------------------------------------------------------ zero insert (stride-s dgrad)
@@ -1120,9 +1146,15 @@ static int wgrad_check(const drnmi_wgrad_args* a) {
 
 extern "C" int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* a) {
   if (wgrad_check(a) != DRNMI_OK) return -1;
+  // the caller does not say which kernel will run (f32 or f32x3): room for either plan
   int splits;
   int64_t per;
-  wgrad_plan(*a, &splits, &per);
+  wgrad_plan(*a, false, &splits, &per);
+  if (wgrad_big_ok(*a)) {
+    int s2;
+    wgrad_plan(*a, true, &s2, &per);
+    if (s2 > splits) splits = s2;
+  }
   return static_cast<int64_t>(splits) * a->cout * a->ks * a->ks * a->cin_stride * 4;
 }
 
@@ -1144,11 +1176,12 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   p.ho = a->ho; p.wo = a->wo; p.ks = a->ks; p.stride = a->stride; p.pad = a->pad; p.dil = a->dil;
   p.K = a->ks * a->ks * a->cin_stride;
   p.M = static_cast<int64_t>(a->n) * a->ho * a->wo;
+  const bool big = x6 && wgrad_big_ok(*a);
   int splits;
-  wgrad_plan(*a, &splits, &p.pix_per_split);
+  wgrad_plan(*a, big, &splits, &p.pix_per_split);
   const dim3 grid((p.K + kWT - 1) / kWT, (a->cout + kWT - 1) / kWT, splits);
-  if (x6 && DRNMI_WGRAD_BIG && a->cout >= kWT2 && p.K >= kWT2 && p.cs % 16 == 0) {
-    const dim3 g2((p.K + kWT2 - 1) / kWT2, (a->cout + kWT2 - 1) / kWT2, splits);   // same splits: same workspace
+  if (big) {
+    const dim3 g2((p.K + kWT2 - 1) / kWT2, (a->cout + kWT2 - 1) / kWT2, splits);
     hipLaunchKernelGGL(wgrad_x6_big_kernel, g2, dim3(kThreads), 0, s, p);
   } else if (x6) {
     hipLaunchKernelGGL(wgrad_kernel<true>, grid, dim3(kThreads), 0, s, p);

@@ -46,11 +46,12 @@ def _vp(t):
 class _NodeState:
     """Per-node packed weights (forward / dgrad layouts) cached across steps."""
 
-    __slots__ = ("wf", "wd", "wfx", "wdx", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift", "patch")
+    __slots__ = ("wf", "wd", "wfx", "wdx", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift", "patch",
+                 "dpatch")
 
     def __init__(self):
         self.wf = self.wd = self.wfx = self.wdx = self.shift = None
-        self.patch = False
+        self.patch = self.dpatch = False
 
 
 class TrainRunner:
@@ -156,7 +157,11 @@ class TrainRunner:
             st.wd = torch.empty(st.rows_d, st.kd_pad, dtype=torch.float32, device=device)
         _lib.check(lib.drnmi_pack_conv_weight(_vp(nd.conv.weight.detach()), cout, cin, ks, dys, st.rows_d,
                                               st.kd_pad, 1, None, F32, _vp(st.wd), stream), f"pack dgrad {nd.name}")
-        st.wdx = self._split(st.wd, dys, st.kd, st.kd_pad)
+        # fp32x: a data gradient whose (stride-1) conv is a patch-kernel shape (layer1's 16 -> 16
+        # at full resolution) runs split-bf16 on the patch kernel, not on the f32 igemm
+        st.dpatch = self.model.precision == "fp32x" and \
+            (dys, cin, ks, 1, nd.conv.dilation[0]) in X6_PATCH_SHAPES
+        st.wdx = self._split(st.wd, dys, st.kd, st.kd_pad, patch=st.dpatch)
         return dys
 
     def _split(self, wpk, cin_stride, k, k_pad, patch=False):
@@ -350,10 +355,9 @@ class TrainRunner:
                     raise RuntimeError(f"wgrad {nd.name}: bad geometry")
                 ws = self._ws("_wg_ws", nb, dev)
                 wa.ws, wa.ws_bytes = ws.data_ptr(), ws.numel()
-                # fp32x: the convs with >= 32 input channels (those the forward runs on conv_x6)
-                # take the split-bf16 weight gradient too
-                wg = lib.drnmi_conv_wgrad_f32x3 if self.model.precision == "fp32x" and \
-                    self.cstride[nd.src] >= 32 else lib.drnmi_conv_wgrad_f32
+                # fp32x: every weight gradient is split-bf16 (the forward's small-channel layers
+                # run split on the patch kernels as well)
+                wg = lib.drnmi_conv_wgrad_f32x3 if self.model.precision == "fp32x" else lib.drnmi_conv_wgrad_f32
                 _lib.check(wg(ctypes.byref(wa), sp), f"wgrad {nd.name}")
                 done.append(c.weight)
             if self.grad_ready is not None and done:
@@ -373,9 +377,11 @@ class TrainRunner:
                                f"zero_insert {nd.name}")
                 prev = grads.get(nd.src)
                 out = prev if prev is not None else torch.empty(n * ih * iw, cs_src, dtype=torch.float32, device=dev)
+                patch = st.dpatch and prev is None       # the patch kernels take no residual
                 self._conv(src, dys, hu, wu, st.wd, st.kd, st.kd_pad, st.rows_d, cin, ks, 1, pad_d, d, out,
                            (ih * iw * cs_src, cs_src, 1), self._zeros_f32(st.rows_d, dev), prev, n, ih, iw,
-                           stream, f"dgrad {nd.name}", st.wdx)
+                           stream, f"dgrad {nd.name}", st.wdx if (patch or not st.dpatch) else None,
+                           _lib.ALGO_PATCH if patch else _lib.ALGO_IGEMM)
                 grads[nd.src] = out
             del dy
 
