@@ -458,6 +458,17 @@ X6_CASES = [
 @pytest.mark.parametrize("case", X6_CASES)
 def test_conv_x6_fp32_accuracy(case):
     """DRNMI_F32X3 (split-bf16, 6 products) vs an fp64 conv: as close as the exact-f32 kernel."""
+    _x6_case(case, split=False)
+
+
+@pytest.mark.parametrize("case", [X6_CASES[0], X6_CASES[1], X6_CASES[2]])
+def test_conv_x6_split_k(case):
+    """The split-K launch (caller workspace, grids of few tiles): partial sums + the epilogue
+    kernel, as accurate as the unsplit kernel (fp64 reference, same bound)."""
+    _x6_case(case, split=True)
+
+
+def _x6_case(case, split):
     import torch.nn.functional as F
     from drnmi import ops
     from drnmi.engine import split3_bf16
@@ -498,6 +509,12 @@ def test_conv_x6_fp32_accuracy(case):
     a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_F32X3, _lib.DRNMI_F32, -1, _lib.ALGO_IGEMM
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
     assert name.startswith("conv_x6_kernel")
+    if split:
+        nb = _lib.load().drnmi_conv_workspace_bytes(ctypes.byref(a))
+        assert nb > 0, "these geometries leave most CUs idle: the launch must split"
+        ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
+        a.ws, a.ws_bytes = ws.data_ptr(), nb
+        name += f" split-K {nb // (4 * n * ho * wo * cout)}"
     _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "x6")
     torch.cuda.synchronize()
     ref = y64.permute(0, 2, 3, 1).numpy()

@@ -365,6 +365,11 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   return static_cast<int>(e);
 }
 
+extern "C" int64_t drnmi_conv_workspace_bytes(const drnmi_conv_args* a) {
+  if (a == nullptr) return -1;
+  return a->dtype == DRNMI_F32X3 && a->algo == DRNMI_ALGO_IGEMM ? x6_conv_workspace_bytes(*a) : 0;
+}
+
 extern "C" int drnmi_stem_layer1(const drnmi_conv_args* stem, const drnmi_conv_args* next, void* stream) {
   if (stem == nullptr || next == nullptr) return DRNMI_EINVAL;
   return stem_l1_dispatch(*stem, *next, reinterpret_cast<hipStream_t>(stream));

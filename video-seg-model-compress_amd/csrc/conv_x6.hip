@@ -102,7 +102,10 @@ conv_x6_kernel(const drnmi_conv_args p) {
   const float* __restrict__ x = reinterpret_cast<const float*>(p.x);
   const uint16_t* __restrict__ wt = reinterpret_cast<const uint16_t*>(p.wgt);
   const int64_t plane_stride = static_cast<int64_t>(p.cout_pad) * p.k_pad;
-  const int nk = p.k_pad / kBK;
+  // split-K (gridDim.y > 1, drnmi_conv_args.ws): this workgroup runs K steps [kt0, kt0 + nk)
+  const int nk_all = p.k_pad / kBK;
+  const int kt0 = static_cast<int>(static_cast<int64_t>(nk_all) * blockIdx.y / gridDim.y);
+  const int nk = static_cast<int>(static_cast<int64_t>(nk_all) * (blockIdx.y + 1) / gridDim.y) - kt0;
   const char* zero_src = reinterpret_cast<const char*>(g_x6_zero) + lane * 16;
 
   // --- A pieces: 16 rows of 64 B each; linear row R = plane * BCO + r
@@ -136,7 +139,8 @@ conv_x6_kernel(const drnmi_conv_args p) {
 
   // one DMA piece ("instruction") of K step kt: pieces [0, A_PW) weights, then pixel rows
   struct StepP { int k0, dh, dw, toff; };
-  auto step_params = [&](int kt) {
+  auto step_params = [&](int u) {
+    const int kt = kt0 + u;
     StepP sp;
     const int cb = kt / (KS * KS);
     const int tap = kt - cb * (KS * KS);
@@ -251,6 +255,30 @@ conv_x6_kernel(const drnmi_conv_args p) {
     }
   }
 
+  // --- split-K: raw fp32 partial sums [split][m][cout]; x6_splitk_epilogue_kernel finishes
+  if (gridDim.y > 1) {
+    float* __restrict__ part = reinterpret_cast<float*>(p.ws) + static_cast<int64_t>(blockIdx.y) * M * p.cout;
+#pragma unroll
+    for (int fn = 0; fn < C::FN; ++fn) {
+      const int m = px0 + wp * 64 + fn * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int fm = 0; fm < C::FM; ++fm) {
+        const int co = co0 + wc * WCO + fm * 16 + fq * 4;
+        if (co >= p.cout) continue;
+        float* q = part + static_cast<int64_t>(m) * p.cout + co;
+        if (co + 3 < p.cout) {
+          *reinterpret_cast<float4*>(q) = make_float4(acc[fm][fn][0], acc[fm][fn][1], acc[fm][fn][2], acc[fm][fn][3]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (co + j < p.cout) q[j] = acc[fm][fn][j];
+        }
+      }
+    }
+    return;
+  }
+
   // --- epilogue: lane owns channels co..co+3 of pixel m, fp32
   const float* __restrict__ res = reinterpret_cast<const float*>(p.res);
   const bool nhwc = p.y_sc == 1;
@@ -310,8 +338,67 @@ conv_x6_kernel(const drnmi_conv_args p) {
   }
 }
 
+// split-K finish: v = sum of the partials in split order, then conv_x6's epilogue (scale / shift,
+// residual, ReLU, NHWC or strided store); one thread per 4 channels of a pixel
+__global__ void __launch_bounds__(256) x6_splitk_epilogue_kernel(const drnmi_conv_args p, int splits) {
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const int c4 = (p.cout + 3) / 4;
+  const int64_t total = M * c4;
+  const float* __restrict__ part = reinterpret_cast<const float*>(p.ws);
+  const float* __restrict__ res = reinterpret_cast<const float*>(p.res);
+  float* __restrict__ y = reinterpret_cast<float*>(p.y);
+  const int hw_o = p.ho * p.wo;
+  const int64_t pstride = M * p.cout;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t m = i / c4;
+    const int co = static_cast<int>(i - m * c4) * 4;
+    const bool full = co + 3 < p.cout;
+    const int64_t o = m * p.cout + co;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < splits; ++z) {
+      if (full) {
+        const float4 a = *reinterpret_cast<const float4*>(part + z * pstride + o);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      } else {
+        for (int j = 0; j < 4; ++j)
+          if (co + j < p.cout) v[j] += part[z * pstride + o + j];
+      }
+    }
+    const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+    const float shv[4] = {sh.x, sh.y, sh.z, sh.w};
+    if (p.scale != nullptr) {
+      const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);
+      const float scv[4] = {sc.x, sc.y, sc.z, sc.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = v[j] * scv[j] + shv[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += shv[j];
+    }
+    if (res != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (co + j < p.cout) v[j] += res[o + j];
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    const int n = static_cast<int>(m / hw_o);
+    const int q = static_cast<int>(m - static_cast<int64_t>(n) * hw_o);
+    const int64_t ybase = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp;
+    if (p.y_sc == 1 && full) {
+      *reinterpret_cast<float4*>(y + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (co + j < p.cout) y[ybase + static_cast<int64_t>(co + j) * p.y_sc] = v[j];
+    }
+  }
+}
+
 template <int KS, int WCO, int WC>
-hipError_t launch_x6(const drnmi_conv_args& p, hipStream_t s) {
+hipError_t launch_x6(const drnmi_conv_args& p, int splits, hipStream_t s) {
   using C = X6Cfg<WCO, WC>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -322,14 +409,56 @@ hipError_t launch_x6(const drnmi_conv_args& p, hipStream_t s) {
   }
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const int64_t blocks = ((M + kBPX - 1) / kBPX) * ((p.cout + C::BCO - 1) / C::BCO);
-  hipLaunchKernelGGL((conv_x6_kernel<KS, WCO, WC>), dim3(static_cast<unsigned>(blocks)), dim3(C::THREADS), C::LDS,
-                     s, p);
+  hipLaunchKernelGGL((conv_x6_kernel<KS, WCO, WC>), dim3(static_cast<unsigned>(blocks), splits), dim3(C::THREADS),
+                     C::LDS, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || splits == 1) return e;
+  const int64_t total = M * ((p.cout + 3) / 4);
+  int64_t g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(x6_splitk_epilogue_kernel, dim3(static_cast<unsigned>(g)), dim3(256), 0, s, p, splits);
   return hipGetLastError();
 }
 
 // 0: 256-channel tile (8 waves), 1: 128 (4 waves), 2: 64 (4 waves)
 int x6_variant(const drnmi_conv_args& p) { return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 1 : 2; }
 constexpr int kX6Bco[3] = {256, 128, 64};
+
+// Split-K count for a launch whose tiles leave CUs idle (one workgroup per CU: 96 tiles of the
+// fine-tune's 2 x 128 x 96 layer5 convs used 96 of 256 CUs).  Cost model per split count S:
+// MFMA time at the fraction of CUs busy in each round plus the partials' HBM round trip
+// (S x M x cout fp32 written and read); S = 1 unless that is >= 10 % faster.  Only with a
+// caller workspace (the fp32x training path): inference launches never split.
+int x6_splits(const drnmi_conv_args& p) {
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const int64_t tiles = ((M + kBPX - 1) / kBPX) * ((p.cout + kX6Bco[x6_variant(p)] - 1) / kX6Bco[x6_variant(p)]);
+  const int nk = p.k_pad / kBK;
+  const double flops = 2.0 * static_cast<double>(M) * p.cout * p.k;
+  auto cost = [&](int S) {
+    const int64_t wgs = tiles * S;
+    const int64_t rounds = (wgs + 255) / 256;
+    const double busy = static_cast<double>(wgs) / static_cast<double>(rounds * 256);
+    double t = flops / (250e12 * busy);
+    if (S > 1) t += 2.0 * S * static_cast<double>(M) * p.cout * 4.0 / 4e12 + 4e-6;
+    return t;
+  };
+  const double c1 = cost(1);
+  int best = 1;
+  double bc = c1;
+  for (int S = 2; S <= 4 && nk / S >= 8; ++S) {
+    const double c = cost(S);
+    if (c < 0.9 * c1 && c < bc) {
+      best = S;
+      bc = c;
+    }
+  }
+  return best;
+}
+
+int64_t x6_workspace_bytes(const drnmi_conv_args& p) {
+  const int S = x6_splits(p);
+  return S > 1 ? static_cast<int64_t>(S) * p.n * p.ho * p.wo * p.cout * 4 : 0;
+}
 
 }  // namespace
 
@@ -340,14 +469,26 @@ bool x6_conv_supported(const drnmi_conv_args& p) {
          (p.y_sc != 1 || p.y_sp == p.cout);
 }
 
+int64_t x6_conv_workspace_bytes(const drnmi_conv_args& p) {
+  return x6_conv_supported(p) ? x6_workspace_bytes(p) : 0;
+}
+
 int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!x6_conv_supported(p)) return DRNMI_ENOTSUP;
   const int v = x6_variant(p);
   // every weight row a tile's DMA reads must exist in each plane
   if ((p.cout + kX6Bco[v] - 1) / kX6Bco[v] * kX6Bco[v] > p.cout_pad) return DRNMI_EINVAL;
+  int S = 1;
+  if (p.ws != nullptr) {
+    S = x6_splits(p);
+    if (S > 1 && p.ws_bytes < x6_workspace_bytes(p)) return DRNMI_EINVAL;
+    if (S > 1 && (reinterpret_cast<uintptr_t>(p.ws) & 15) != 0) return DRNMI_EINVAL;
+  }
   hipError_t e;
-  if (p.ks == 3) e = v == 0 ? launch_x6<3, 128, 2>(p, s) : v == 1 ? launch_x6<3, 128, 1>(p, s) : launch_x6<3, 64, 1>(p, s);
-  else e = v == 0 ? launch_x6<1, 128, 2>(p, s) : v == 1 ? launch_x6<1, 128, 1>(p, s) : launch_x6<1, 64, 1>(p, s);
+  if (p.ks == 3)
+    e = v == 0 ? launch_x6<3, 128, 2>(p, S, s) : v == 1 ? launch_x6<3, 128, 1>(p, S, s) : launch_x6<3, 64, 1>(p, S, s);
+  else
+    e = v == 0 ? launch_x6<1, 128, 2>(p, S, s) : v == 1 ? launch_x6<1, 128, 1>(p, S, s) : launch_x6<1, 64, 1>(p, S, s);
   return static_cast<int>(e);
 }
 

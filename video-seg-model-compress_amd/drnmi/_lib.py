@@ -43,6 +43,7 @@ class ConvArgs(ctypes.Structure):
         ("out_scale", ctypes.c_float),
         ("x2", ctypes.c_void_p),
         ("cin2", ctypes.c_int32), ("h2", ctypes.c_int32), ("w2", ctypes.c_int32), ("stride2", ctypes.c_int32),
+        ("ws", ctypes.c_void_p), ("ws_bytes", ctypes.c_int64),
     ]
 
 
@@ -91,6 +92,7 @@ SIGNATURES = {
                                             _VP, _VP, _I32, _VP, _VP]),
     "drnmi_channel_sum_f32": (ctypes.c_int, [_VP, _I64, _I32, _I32, _VP, _I32, _VP, _VP]),
     "drnmi_conv_wgrad_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
+    "drnmi_conv_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(ConvArgs)]),
     "drnmi_conv_wgrad_f32": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
     "drnmi_conv_wgrad_f32x3": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
     "drnmi_split3_bf16": (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP]),

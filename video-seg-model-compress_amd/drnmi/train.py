@@ -68,6 +68,7 @@ class TrainRunner:
         self.state = [_NodeState() for _ in self.nodes]
         self._red_ws = None
         self._wg_ws = None
+        self._cv_ws = None
         self._zeros = None
         self.grad_ready = None          # callback(list[Parameter]) after each node's grads land
         self.grad_scale = 1.0           # multiplies dL/dlogprobs (DDP averaging: 1 / world_size)
@@ -192,7 +193,14 @@ class TrainRunner:
         if wx is not None:
             a.dtype = _lib.DRNMI_F32X3           # fp32x: conv_x6 (fp32 in/out, bf16 weight planes)
         a.tile, a.algo = -1, algo
-        _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), what)
+        lib = _lib.load()
+        if wx is not None and algo == _lib.ALGO_IGEMM:
+            # split-K scratch for the launches whose tiles would leave CUs idle (the 1/8-res layers)
+            nb = lib.drnmi_conv_workspace_bytes(ctypes.byref(a))
+            if nb > 0:
+                ws = self._ws("_cv_ws", nb, y.device)
+                a.ws, a.ws_bytes = ws.data_ptr(), ws.numel()
+        _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), what)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, save: bool):
