@@ -23,7 +23,7 @@ for (name, _), v in acc.items():
     if "End_Timestamp" in v:
         per[name]["dur_us"].append((v["End_Timestamp"] - v["Start_Timestamp"]) * 1e-3)
 for name, d in per.items():
-    if not name.startswith(("conv", "stem", "patch", "up8")):
+    if not name.startswith(("conv", "stem", "patch", "up8", "wgrad")):
         continue
     avg = {k: sum(x) / len(x) for k, x in d.items() if k not in ("Start_Timestamp", "End_Timestamp")}
     line = f"{name[:60]:60s} n={len(d.get('dur_us', [0]))}"
