@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
 // B fragment is done once per chunk and reused by the wave's four row blocks.  Two workgroups per
 // CU (2 x 2 x 128 x 36 floats of LDS each).
 constexpr int kWT2 = 128;
-__global__ void __launch_bounds__(kThreads) wgrad_x6_big_kernel(const WgradP p) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) wgrad_x6_big_kernel(const WgradP p) {
   __shared__ __attribute__((aligned(16))) float As[2][kWT2][kWLD];
   __shared__ __attribute__((aligned(16))) float Bs[2][kWT2][kWLD];
   const int t = threadIdx.x;
@@ -683,6 +683,221 @@ __global__ void __launch_bounds__(kThreads) wgrad_x6_big_kernel(const WgradP p) 
     load(r0a, r0b);
     compute(1);
     if (mc + 2 * kWM < m_end) store(0, r1a, r1b);
+    __syncthreads();
+  }
+  float* out = p.ws + static_cast<int64_t>(blockIdx.z) * p.cout * p.K;
+#pragma unroll
+  for (int fi = 0; fi < 4; ++fi)
+#pragma unroll
+    for (int fj = 0; fj < 4; ++fj) {
+      const int k = kc0 + wcn * 64 + fj * 16 + fr;
+      if (k >= p.K) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = co0 + wr * 64 + fi * 16 + 4 * fq + r;
+        if (c < p.cout) out[static_cast<int64_t>(c) * p.K + k] = acc[fi][fj][r];
+      }
+    }
+}
+
+// ---- fp32x weight gradient, dy pre-split (DRNMI_WGRAD_PRE) ---------------------------------
+// The 128 x 128 tile above splits every dy and x value in each of the two waves that read it
+// (~4.4 VALU instructions per MFMA: VALU-bound, MFMA busy 0.31, profiles/r5r_wgrad_pmc).  Here dy
+// is split once per launch into three transposed bf16 planes [plane][co][m] (one HBM pass,
+// wgrad_dy_split_kernel) that the tile stages with LDS-DMA like conv_x6's weight planes: the
+// kernel splits only x.  Same split3 (RNE) of the same values and the same MFMA order per
+// accumulator as wgrad_x6_big_kernel, so the partial sums are bit-identical to it.
+#ifndef DRNMI_WGRAD_PRE
+#define DRNMI_WGRAD_PRE 1
+#endif
+constexpr int kPreRows = kWT2;   // dyT rows padded to a multiple of the tile (zero rows)
+
+__global__ void __launch_bounds__(kThreads)
+wgrad_dy_split_kernel(const float* __restrict__ dy, int dys, int cout, int64_t M, int64_t Mp, int Cp,
+                      bf16_t* __restrict__ out) {
+  // thread: channel co = 64-channel block + t / 4, pixels 8 (t % 4) .. +7 of a 32-pixel group:
+  // four lanes write one channel's 64-B row piece per plane; each read instruction is 16
+  // consecutive channels (64 B) of 4 pixels
+  const int t = threadIdx.x;
+  const int64_t ngroups = Mp / 32;
+  const int cblocks = Cp / 64;
+  const int64_t total = ngroups * cblocks;
+  const int64_t pstride = static_cast<int64_t>(Cp) * Mp;
+  for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
+    const int cb = static_cast<int>(b % cblocks);
+    const int64_t g = b / cblocks;
+    const int co = cb * 64 + (t >> 2);
+    const int64_t m0 = g * 32 + 8 * (t & 3);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = (co < cout && m0 + j < M) ? dy[(m0 + j) * dys + co] : 0.f;
+    bf16x8 h1, h2, h3;
+    split3(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), h1, h2, h3);
+    bf16_t* o = out + static_cast<int64_t>(co) * Mp + m0;
+    *reinterpret_cast<bf16x8*>(o) = h1;
+    *reinterpret_cast<bf16x8*>(o + pstride) = h2;
+    *reinterpret_cast<bf16x8*>(o + 2 * pstride) = h3;
+  }
+}
+
+__device__ __forceinline__ int pre_swz_a(int row) { return ((row >> 3) & 1) * 3; }          // 64-B bf16 rows
+__device__ __forceinline__ int pre_swz_b(int row) { return ((row >> 1) & 1) | (row & 4); }  // 128-B fp32 rows
+
+struct WgradPreP {
+  WgradP p;
+  const bf16_t* dyt;   // [3][Cp][Mp]
+  int64_t Mp;
+  int Cp;
+};
+
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2))) wgrad_x6_pre_kernel(const WgradPreP q) {
+  const WgradP& p = q.p;
+  // A: [buf][plane][128 rows][64 B] bf16 (16-B chunks swizzled), B: [buf][128 rows][32 floats]
+  // (16-B chunks swizzled): 2 x (24 + 16) KB, two workgroups per CU
+  __shared__ __attribute__((aligned(16))) char Ab[2][3 * kWT2 * 64];
+  __shared__ __attribute__((aligned(16))) float Bs[2][kWT2 * 32];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wr = wave >> 1, wcn = wave & 1;
+  const int co0 = blockIdx.y * kWT2;
+  const int kc0 = blockIdx.x * kWT2;
+  const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * p.pix_per_split;
+  int64_t m_end = m_begin + p.pix_per_split;
+  if (m_end > p.M) m_end = p.M;
+  const int lm = t & 31;
+  const int lv = t >> 5;
+  const int hw = p.ho * p.wo;
+  const int kcol = kc0 + 16 * lv;
+  const int tap = kcol / p.cs;
+  const int ci = kcol - tap * p.cs;
+  const bool kval = kcol < p.K && tap < p.ks * p.ks;
+  const int kh = kval ? tap / p.ks : 0;
+  const int kw = kval ? tap - kh * p.ks : 0;
+
+  // A DMA: 24 pieces of 1 KB per chunk, 6 per wave; piece gi = plane * 8 + 16-row block
+  const int64_t plane_stride = static_cast<int64_t>(q.Cp) * q.Mp;
+  const bf16_t* a_src[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int gi = wave * 6 + i;
+    const int pl = gi >> 3;
+    const int r = (gi & 7) * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ pre_swz_a(r);
+    a_src[i] = q.dyt + pl * plane_stride + static_cast<int64_t>(co0 + r) * q.Mp + 8 * c;
+  }
+  auto dma_a = [&](int buf, int64_t m) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(a_src[i] + m),
+                                       (__attribute__((address_space(3))) void*)(&Ab[buf][(wave * 6 + i) * 1024]),
+                                       16, 0, 0);
+  };
+
+  int64_t m_cur = m_begin + lm;
+  int p_n = 0, p_oh = 0, p_ow = 0;
+  {
+    const int mi = static_cast<int>(m_cur < p.M ? m_cur : 0);
+    p_n = mi / hw;
+    const int qq = mi - p_n * hw;
+    p_oh = qq / p.wo;
+    p_ow = qq - p_oh * p.wo;
+  }
+  auto load = [&](float4 (&rb)[4]) {
+    const int64_t m = m_cur;
+    const int nn = p_n, oh = p_oh, ow = p_ow;
+    m_cur += kWM;
+    p_ow += kWM;
+    while (p_ow >= p.wo) {
+      p_ow -= p.wo;
+      if (++p_oh == p.ho) {
+        p_oh = 0;
+        ++p_n;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m >= m_end || !kval) return;
+    const int ih = oh * p.stride - p.pad + kh * p.dil;
+    const int iw = ow * p.stride - p.pad + kw * p.dil;
+    if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.w)) {
+      const float* xr = p.x + ((static_cast<int64_t>(nn) * p.h + ih) * p.w + iw) * p.cs + ci;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rb[j] = *reinterpret_cast<const float4*>(xr + 4 * j);
+    }
+  };
+  auto store = [&](int buf, const float4 (&rb)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float bv[4] = {rb[j].x, rb[j].y, rb[j].z, rb[j].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 16 * lv + 4 * j + e;
+        Bs[buf][row * 32 + 4 * ((lm >> 2) ^ pre_swz_b(row)) + (lm & 3)] = bv[e];
+      }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  auto compute = [&](int buf) {
+    bf16x8 b[4][3];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int r = wcn * 64 + f * 16 + fr;
+      const float* br = &Bs[buf][r * 32];
+      split3(*reinterpret_cast<const float4*>(br + 4 * ((2 * fq) ^ pre_swz_b(r))),
+             *reinterpret_cast<const float4*>(br + 4 * ((2 * fq + 1) ^ pre_swz_b(r))), b[f][0], b[f][1], b[f][2]);
+    }
+#pragma unroll
+    for (int fi = 0; fi < 4; ++fi) {
+      const int r = wr * 64 + fi * 16 + fr;
+      const char* ar = &Ab[buf][r * 64 + ((fq ^ pre_swz_a(r)) * 16)];
+      bf16x8 a[3];
+      a[0] = *reinterpret_cast<const bf16x8*>(ar);
+      a[1] = *reinterpret_cast<const bf16x8*>(ar + kWT2 * 64);
+      a[2] = *reinterpret_cast<const bf16x8*>(ar + 2 * kWT2 * 64);
+#pragma unroll
+      for (int fj = 0; fj < 4; ++fj) {
+        f32x4& c = acc[fi][fj];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[fj][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[fj][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[fj][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][0], c, 0, 0, 0);
+      }
+    }
+  };
+
+  // chunk c: A by DMA into buffer c & 1 (issued one chunk ahead), B through registers as in
+  // wgrad_x6_big_kernel (two register sets); every chunk ends with vmcnt(0) + barrier
+  float4 r0[4], r1[4];
+  dma_a(0, m_begin);
+  load(r0);
+  store(0, r0);
+  load(r0);                                        // chunk 1
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int64_t mc = m_begin; mc < m_end; mc += 2 * kWM) {
+    if (mc + kWM < m_end) dma_a(1, mc + kWM);
+    load(r1);                                      // chunk c + 2
+    compute(0);
+    if (mc + kWM < m_end) store(1, r0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (mc + kWM >= m_end) break;
+    if (mc + 2 * kWM < m_end) dma_a(0, mc + 2 * kWM);
+    load(r0);                                      // chunk c + 3
+    compute(1);
+    if (mc + 2 * kWM < m_end) store(0, r1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   float* out = p.ws + static_cast<int64_t>(blockIdx.z) * p.cout * p.K;
@@ -1144,18 +1359,37 @@ static int wgrad_check(const drnmi_wgrad_args* a) {
   return DRNMI_OK;
 }
 
+// the partials [splits][cout][K] fp32, then (fp32x, 128-tile geometries) the dy planes [3][Cp][Mp]
+static int64_t wgrad_partials_bytes(const drnmi_wgrad_args& a, int splits) {
+  return (static_cast<int64_t>(splits) * a.cout * a.ks * a.ks * a.cin_stride * 4 + 255) / 256 * 256;
+}
+// the dy split pass costs ~10 B of HBM per dy element against 2 K flops per element of the tile:
+// it pays where K >= 1024 (layer7.0: 3.78 -> 2.72 ms; a 1x1 256 -> 1024 wgrad: 128 -> 234 us)
+static bool wgrad_pre_ok(const drnmi_wgrad_args& a) {
+  return DRNMI_WGRAD_PRE && wgrad_big_ok(a) && a.ks * a.ks * a.cin_stride >= 1024;
+}
+static int64_t wgrad_pre_bytes(const drnmi_wgrad_args& a) {
+  if (!wgrad_pre_ok(a)) return 0;
+  const int64_t M = static_cast<int64_t>(a.n) * a.ho * a.wo;
+  const int64_t Mp = (M + kWM - 1) / kWM * kWM;
+  const int64_t Cp = (a.cout + kPreRows - 1) / kPreRows * kPreRows;
+  return 3 * Cp * Mp * 2;
+}
+
 extern "C" int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* a) {
   if (wgrad_check(a) != DRNMI_OK) return -1;
   // the caller does not say which kernel will run (f32 or f32x3): room for either plan
   int splits;
   int64_t per;
   wgrad_plan(*a, false, &splits, &per);
+  int64_t pre = 0;
   if (wgrad_big_ok(*a)) {
     int s2;
     wgrad_plan(*a, true, &s2, &per);
     if (s2 > splits) splits = s2;
+    pre = wgrad_pre_bytes(*a);
   }
-  return static_cast<int64_t>(splits) * a->cout * a->ks * a->ks * a->cin_stride * 4;
+  return wgrad_partials_bytes(*a, splits) + pre;
 }
 
 static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
@@ -1180,7 +1414,25 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   int splits;
   wgrad_plan(*a, big, &splits, &p.pix_per_split);
   const dim3 grid((p.K + kWT - 1) / kWT, (a->cout + kWT - 1) / kWT, splits);
-  if (big) {
+  if (big && wgrad_pre_ok(*a)) {
+    WgradPreP q{};
+    q.p = p;
+    q.Mp = (p.M + kWM - 1) / kWM * kWM;
+    q.Cp = (a->cout + kPreRows - 1) / kPreRows * kPreRows;
+    int full_splits;
+    int64_t per;
+    wgrad_plan(*a, false, &full_splits, &per);
+    int s2;
+    wgrad_plan(*a, true, &s2, &per);
+    if (s2 > full_splits) full_splits = s2;
+    bf16_t* dyt = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(a->ws) + wgrad_partials_bytes(*a, full_splits));
+    q.dyt = dyt;
+    const int64_t blocks = (q.Mp / 32) * (q.Cp / 64);
+    hipLaunchKernelGGL(wgrad_dy_split_kernel, dim3(static_cast<unsigned>(blocks < 8192 ? blocks : 8192)), dim3(kThreads),
+                       0, s, a->dy, a->dy_stride, a->cout, p.M, q.Mp, q.Cp, dyt);
+    const dim3 g2((p.K + kWT2 - 1) / kWT2, (a->cout + kWT2 - 1) / kWT2, splits);
+    hipLaunchKernelGGL(wgrad_x6_pre_kernel, g2, dim3(kThreads), 0, s, q);
+  } else if (big) {
     const dim3 g2((p.K + kWT2 - 1) / kWT2, (a->cout + kWT2 - 1) / kWT2, splits);
     hipLaunchKernelGGL(wgrad_x6_big_kernel, g2, dim3(kThreads), 0, s, p);
   } else if (x6) {
