@@ -328,9 +328,12 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
     B, H, W = frames.shape[0], frames.shape[1], frames.shape[2]
     plan = model.plan(B, H, W, device=dev)     # the plan model.segment() runs (same key)
     lib = _lib.load()
-    fused_stem = getattr(plan, "stem_fused", False)
+    front = getattr(plan, "front_fused", False)
+    fused_stem = getattr(plan, "stem_fused", False) and not front
 
     def launched_name(i):
+        if front and i <= 2:                 # layer0..layer2 in one launch (drnmi_video_front_u8)
+            return "" if i else "front_kernel"
         if fused_stem and i <= 1:            # stem + layer1 in one launch (drnmi_stem_layer1)
             return "" if i == 1 else lib.drnmi_stem_layer1_kernel_name(
                 ctypes.byref(plan.stem_u8), ctypes.byref(plan.args[1])).decode()
@@ -346,9 +349,11 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
     #  = dense FLOPs x the density of its weights, on dense and sparse kernels alike
     works = launch_work(plan)
     density = [float((nd.conv.weight != 0).sum()) / nd.conv.weight.numel() for nd in nodes]
-    if fused_stem:
-        density[0] = density[1] = float(sum((nd.conv.weight != 0).sum() for nd in nodes[:2])) / \
-            sum(nd.conv.weight.numel() for nd in nodes[:2])
+    for k, on in ((3, front), (2, fused_stem)):
+        if on:
+            density[:k] = [float(sum((nd.conv.weight != 0).sum() for nd in nodes[:k])) /
+                           sum(nd.conv.weight.numel() for nd in nodes[:k])] * k
+            break
     dense_flops = {i: w[1] for i, w in enumerate(works)}
     works = [(w[0], w[1] * density[i], w[2]) if i < len(nodes) else w for i, w in enumerate(works)]
     events = []

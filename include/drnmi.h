@@ -142,6 +142,33 @@ int64_t drnmi_conv_workspace_bytes(const drnmi_conv_args* args);
 int drnmi_stem_layer1(const drnmi_conv_args* stem, const drnmi_conv_args* next, void* stream);
 const char* drnmi_stem_layer1_kernel_name(const drnmi_conv_args* stem, const drnmi_conv_args* next);
 
+/* Fused video front (bf16 perf mode, csrc/front.hip front_kernel): uint8 HWC3 frames -> layer0
+ * (7x7 3->16 + BN + ReLU, lmodels/drn.py:132-137, on the normalised frame of data_transforms.py:
+ * 109-125, 256-281) -> layer1 (3x3 16->16 + BN + ReLU, drn.py:201-211) -> layer2 (3x3 stride 2
+ * 16->32 + BN + ReLU) in one launch: neither the 16-channel full-resolution stem output nor
+ * layer1's is ever written; the layer2 output y is NHWC bf16 [n][(h+1)/2][(w+1)/2][32].
+ * Arithmetic: the stem runs f16 MFMAs on the exact frame bytes (1024 + u8 is exact in f16) with the
+ * normalisation and the stem's BN scale folded into f16 weights w * scale / (255 std[c]); the
+ * offset 1024 and the mean term are subtracted through a per-border-case shift (the reference
+ * zero-pads in normalised space, so the shift depends on which taps fall inside the image);
+ * layer1 / layer2 are bf16 MFMAs (BN scale folded into bf16 weights) on bf16 activations.
+ *   drnmi_front_pack: HOST function, no GPU: packs the three convs' OIHW fp32 weights (w0
+ *     [16][3][7][7], w1 [16][16][3][3], w2 [32][16][3][3]), their folded BN scale/shift
+ *     (scale*: NULL = 1), mean/std (3 each, per model channel) and bgr into a host buffer of
+ *     drnmi_front_pack_bytes() bytes that the caller copies to the device once.
+ *   drnmi_video_front_u8: frames [n][h][w][3] uint8 (bgr as packed), pack = the device copy;
+ *     requires w % 4 == 0, h >= 8, w >= 8, n*h*w*3 < 2^31 (DRNMI_EINVAL otherwise).
+ *   drnmi_front_supported: 1 if drnmi_video_front_u8 takes (n, h, w).
+ * Replaces ToTensorVideoImage + Normalize + layer0 + layer1 + layer2 of the seg_video loop
+ * (seg_video_old_no_plot.py:157-169 -> lmodels/drnseg.py:295-299 -> drn.py:213-259). */
+int64_t drnmi_front_pack_bytes(void);
+int drnmi_front_pack(const float* w0, const float* scale0, const float* shift0, const float* w1, const float* scale1,
+                     const float* shift1, const float* w2, const float* scale2, const float* shift2,
+                     const float* mean3, const float* std3, int32_t bgr, void* out_host);
+int drnmi_front_supported(int32_t n, int32_t h, int32_t w);
+int drnmi_video_front_u8(const uint8_t* frames, const void* pack, void* y, int32_t n, int32_t h, int32_t w,
+                         void* stream);
+
 /* Block-sparsity map of packed weights [rows_pad][k_pad] (dtype F32 or BF16): one bit per
  * 16-row x 32-column unit, bit = 1 iff any element of the unit is nonzero (+-0 count as zero);
  * layout: row-block rb owns words [rb*W, rb*W + W), W = ceil(k_pad / 32 / 32), unit ku at bit

@@ -648,22 +648,27 @@ def test_stem_layer1_fused_bit_identical(shape):
 
 
 def test_stem_fused_network_matches_two_launch():
-    """The bf16 video path with the stem fused (default) gives the same labels as with the
-    stem and layer1 as two launches (bit-identical layer1 output => identical network)."""
+    """The bf16 video path with the stem fused gives the same labels as with the stem and layer1
+    as two launches (bit-identical layer1 output => identical network); the fused front
+    (layer0..layer2 in one launch, test_front.py) is switched off for both."""
     from drnmi import engine
     from drnmi.drnseg import build
     from drnmi.weights import synth_frames
-    m = build("drn_d_22", 19, seed=3, device=DEV, precision="bf16")
-    frames = torch.from_numpy(synth_frames(11, 2, 136, 200)).to(DEV)
-    assert m.plan(2, 136, 200).stem_fused
-    fused = m.segment(frames)
-    engine.FUSE_STEM = False
+    engine.FUSE_FRONT = False
     try:
-        m2 = build("drn_d_22", 19, seed=3, device=DEV, precision="bf16")
-        assert not m2.plan(2, 136, 200).stem_fused
-        two = m2.segment(frames)
+        m = build("drn_d_22", 19, seed=3, device=DEV, precision="bf16")
+        frames = torch.from_numpy(synth_frames(11, 2, 136, 200)).to(DEV)
+        assert m.plan(2, 136, 200).stem_fused and not m.plan(2, 136, 200).front_fused
+        fused = m.segment(frames)
+        engine.FUSE_STEM = False
+        try:
+            m2 = build("drn_d_22", 19, seed=3, device=DEV, precision="bf16")
+            assert not m2.plan(2, 136, 200).stem_fused
+            two = m2.segment(frames)
+        finally:
+            engine.FUSE_STEM = True
     finally:
-        engine.FUSE_STEM = True
+        engine.FUSE_FRONT = True
     assert torch.equal(fused, two)
 
 

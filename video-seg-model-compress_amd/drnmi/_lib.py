@@ -72,6 +72,10 @@ SIGNATURES = {
     "drnmi_stem_layer1": (ctypes.c_int, [ctypes.POINTER(ConvArgs), ctypes.POINTER(ConvArgs), _VP]),
     "drnmi_stem_layer1_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(ConvArgs), ctypes.POINTER(ConvArgs)]),
     "drnmi_conv_num_tiles": (ctypes.c_int, []),
+    "drnmi_front_pack_bytes": (ctypes.c_int64, []),
+    "drnmi_front_pack": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _I32, _VP]),
+    "drnmi_front_supported": (ctypes.c_int, [_I32, _I32, _I32]),
+    "drnmi_video_front_u8": (ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _VP]),
     "drnmi_frame_ingest_u8": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _VP, _VP, _I32, _I32, _VP]),
     "drnmi_nchw_to_nhwc": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_nhwc_to_nchw": (ctypes.c_int, [_VP, _VP, _I32, _I32, _I32, _I32, _I32, _I32, _VP]),

@@ -301,6 +301,44 @@ class PackedNet:
                 full = torch.zeros(stem.cout_pad, STEM_U8_K, device=self.device, dtype=torch.float32)
                 full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
                 self.stem_u8_w = split3_bf16(full) if self.base == "fp32x" else full.to(self.tdtype).contiguous()
+            self._front_packs = {}
+            self.front_eligible = self._front_shapes_ok()
+
+    def _front_shapes_ok(self) -> bool:
+        """The fused video front (drnmi_video_front_u8: layer0 + layer1 + layer2 of every DRN-D,
+        lmodels/drn.py:132-137, :201-211) takes exactly 7x7 3->16 s1, 3x3 16->16 s1, 3x3 16->32 s2,
+        bf16 activations (also in int8 nets, whose small-channel layers stay bf16)."""
+        nodes = self.graph.nodes
+        if self.base != "bf16" or len(nodes) < 4 or not FUSE_FRONT:
+            return False
+        want = [(3, 16, 7, 1, 3, 1), (16, 16, 3, 1, 1, 1), (16, 32, 3, 2, 1, 1)]
+        for nd, (ci, co, k, st, pd, dl) in zip(nodes[:3], want):
+            c = nd.conv
+            if (c.in_channels, c.out_channels, c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0]) != \
+                    (ci, co, k, st, pd, dl) or c.groups != 1 or nd.bn is None or nd.res is not None or \
+                    not nd.relu or nd.i8 or nd.out_fp32_nchw:
+                return False
+        return nodes[1].src == nodes[0].dst and nodes[2].src == nodes[1].dst and self.cstride[nodes[2].dst] == 32
+
+    def front_pack(self, mean, std, bgr: bool) -> torch.Tensor:
+        """Device copy of drnmi_front_pack for these weights and this normalisation (cached per
+        (mean, std, bgr); cleared by every repack)."""
+        key = (tuple(float(v) for v in mean), tuple(float(v) for v in std), bool(bgr))
+        t = self._front_packs.get(key)
+        if t is None:
+            import numpy as np
+            lib = _lib.load()
+            arrs = []
+            for nd in self.graph.nodes[:3]:
+                arrs += [nd.conv.weight.detach().float().cpu().contiguous().numpy(),
+                         nd.scale.float().cpu().contiguous().numpy(), nd.shift.float().cpu().contiguous().numpy()]
+            arrs += [np.asarray(key[0], dtype=np.float32), np.asarray(key[1], dtype=np.float32)]
+            out = np.zeros(int(lib.drnmi_front_pack_bytes()), dtype=np.uint8)
+            _lib.check(lib.drnmi_front_pack(*[a.ctypes.data_as(ctypes.c_void_p) for a in arrs], 1 if bgr else 0,
+                                            out.ctypes.data_as(ctypes.c_void_p)), "front_pack")
+            t = torch.from_numpy(out).to(self.device)
+            self._front_packs[key] = t
+        return t
 
 
     def _fuse_downsamples(self):
@@ -421,6 +459,9 @@ FUSE_DOWNSAMPLE = True
 # bf16 video path: the uint8 stem and the 3x3 16->16 layer1 conv run as one kernel
 # (drnmi_stem_layer1); the stem output is never written.  Plans with keep_all keep two launches.
 FUSE_STEM = True
+# bf16 video path: layer0 + layer1 + layer2 as one launch from the uint8 frames (drnmi_video_front_u8);
+# neither 16-channel full-resolution activation is written.  Plans with keep_all keep separate launches.
+FUSE_FRONT = True
 
 
 def _route_name(nd: ConvNode, cin_stride: int, cin2: int = 0, k_pad: int | None = None) -> str:
@@ -537,7 +578,23 @@ class Plan:
         self.args = [None if i in self.skip else self._conv_args(nd) for i, nd in enumerate(g.nodes)]
         self.stem_u8 = self._stem_u8_args()
         self.stem_fused = self._stem_fusable(reads_of)
+        self.front_fused = self._front_fusable(reads_of)
+        self.front_pack_t = None
         self.src = "nchw"
+
+    def _front_fusable(self, reads_of) -> bool:
+        """layer0..layer2 run as one drnmi_video_front_u8 launch on the u8 path when the packed net
+        takes it, each intermediate has exactly one reader and the frame shape is supported."""
+        pk = self.packed
+        nodes = pk.graph.nodes
+        if not (self.fuse and getattr(pk, "front_eligible", False)):
+            return False
+        for i in (0, 1):
+            if any(nodes[i].dst in reads_of[j] for j in range(len(nodes)) if j != i + 1) or pk.quant_after.get(i):
+                return False
+        if pk.quant_after.get(2):
+            return False
+        return bool(_lib.load().drnmi_front_supported(self.n, self.h, self.w))
 
     def _stem_fusable(self, reads_of) -> bool:
         """The u8 stem and layer1 can run as one launch (drnmi_stem_layer1) when layer1 is the
@@ -619,6 +676,7 @@ class Plan:
             if i in self.skip:
                 continue
             self.args[i] = self._conv_args(nd)
+        self.front_pack_t = None                  # re-fetched (repacked) at the next ingest_u8
         if self.stem_u8 is not None:
             nd = self.packed.graph.nodes[0]
             self.stem_u8.wgt = self.packed.stem_u8_w.data_ptr()
@@ -628,10 +686,20 @@ class Plan:
     # ------------------------------------------------------------------ execution
     def run_backbone(self, stream: int, timing_hook=None):
         lib = _lib.load()
-        fused_stem = self.src == "u8" and self.stem_fused
+        front = self.src == "u8" and self.front_fused
+        fused_stem = self.src == "u8" and self.stem_fused and not front
         for i, (a, nd) in enumerate(zip(self.args, self.packed.graph.nodes)):
-            if a is None or (i == 1 and fused_stem):
+            if a is None or (i == 1 and fused_stem) or (front and i in (1, 2)):
                 continue                          # folded into another launch
+            if front and i == 0:
+                if timing_hook is not None:
+                    timing_hook(0, nd, True)
+                _lib.check(lib.drnmi_video_front_u8(self.stem_u8.x, self.front_pack_t.data_ptr(),
+                                                    self.bufs[self.packed.graph.nodes[2].dst].data_ptr(),
+                                                    self.n, self.h, self.w, ctypes.c_void_p(stream)), "video_front_u8")
+                if timing_hook is not None:
+                    timing_hook(0, nd, False)
+                continue
             if i == 0 and self.src == "u8":
                 a = self.stem_u8
             if timing_hook is not None:
@@ -673,6 +741,8 @@ class Plan:
             for i in range(3):
                 a.mean[i] = float(mean[i])
                 a.std[i] = float(std[i])
+            if self.front_fused:
+                self.front_pack_t = self.packed.front_pack(mean, std, bgr)
             self.src = "u8"
             return
         self.src = "nchw"

@@ -69,9 +69,10 @@ def launch_work(plan, video: bool = True):
       * a 1x1 downsample folded into its block's last conv (plan.skip, lmodels/drn.py:181-186):
         its FLOPs and its input + weight bytes move into that launch, and the residual tensor
         is neither written by the downsample nor read by the conv;
-      * the fused stem + layer1 launch (plan.stem_fused, drn.py:132-137 + :201-211; video=True:
-        the uint8-frame segment() path): the 16-channel stem output is neither written nor read
-        back."""
+      * the fused front launch (plan.front_fused: layer0 + layer1 + layer2) or else the fused
+        stem + layer1 launch (plan.stem_fused, drn.py:132-137 + :201-211; video=True: the
+        uint8-frame segment() path): the 16-channel full-resolution intermediates are neither
+        written nor read back."""
     rows = list(node_work(plan))
     nodes = plan.packed.graph.nodes
     esz = 2 if plan.packed.base == "bf16" else 4
@@ -83,7 +84,17 @@ def launch_work(plan, video: bool = True):
         fi, bi = rows[i][1], rows[i][2]
         rows[j] = (n_, fj + fi, bj - res_b + (bi - res_b))
         rows[i] = (rows[i][0], 0.0, 0.0)
-    if video and getattr(plan, "stem_fused", False):
+    if video and getattr(plan, "front_fused", False):
+        # layer0 + layer1 + layer2 in one launch (drnmi_video_front_u8): neither full-resolution
+        # 16-channel intermediate is written or read back
+        mid = 0.0
+        for k in (0, 1):
+            hk, wk = plan.shapes[nodes[k].dst]
+            mid += plan.n * hk * wk * nodes[k].conv.out_channels * esz
+        rows[0] = (rows[0][0], rows[0][1] + rows[1][1] + rows[2][1], rows[0][2] + rows[1][2] + rows[2][2] - 2 * mid)
+        rows[1] = (rows[1][0], 0.0, 0.0)
+        rows[2] = (rows[2][0], 0.0, 0.0)
+    elif video and getattr(plan, "stem_fused", False):
         h0, w0 = plan.shapes[nodes[0].dst]
         mid = plan.n * h0 * w0 * nodes[0].conv.out_channels * esz
         rows[0] = (rows[0][0], rows[0][1] + rows[1][1], rows[0][2] + rows[1][2] - 2 * mid)
