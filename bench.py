@@ -67,11 +67,12 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def spawn_ranks(n: int, argv) -> int:
-    """`python bench.py --gpus N` outside torchrun: start N rank processes of this script (one
-    per GPU, LOCAL_RANK = RANK = r) with a 127.0.0.1 rendezvous, before this process touches the
-    GPU, and return the worst exit code.  The reference's multi-GPU entry does the same through
-    torch.multiprocessing + init_process_group (semantic_seg_multigpu.py:467-468)."""
+def spawn_ranks(n: int, argv, script: str | None = None) -> int:
+    """`python bench.py --gpus N` outside torchrun: start N rank processes of this script (or of
+    `script`: bench_finetune.py uses the same launcher; one per GPU, LOCAL_RANK = RANK = r) with a
+    127.0.0.1 rendezvous, before this process touches the GPU, and return the worst exit code.
+    The reference's multi-GPU entry does the same through torch.multiprocessing +
+    init_process_group (semantic_seg_multigpu.py:467-468)."""
     import socket
     import subprocess
     with socket.socket() as s_:
@@ -81,7 +82,7 @@ def spawn_ranks(n: int, argv) -> int:
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__), *argv], env=env))
     rcs = [None] * n
     try:
         while any(rc is None for rc in rcs):
@@ -100,7 +101,7 @@ def spawn_ranks(n: int, argv) -> int:
     return max(abs(rc) for rc in rcs)
 
 
-def resolve_world(args, environ=os.environ):
+def resolve_world(args, environ=os.environ, prog: str = "bench.py"):
     """(world, rank, local_rank) of this process, or None when it must spawn the ranks itself.
     A torchrun environment whose WORLD_SIZE differs from --gpus is refused."""
     if environ.get("WORLD_SIZE") is None:
@@ -109,7 +110,7 @@ def resolve_world(args, environ=os.environ):
         return 1, 0, 0
     world = int(environ["WORLD_SIZE"])
     if world != args.gpus:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch with matching values)")
+        raise SystemExit(f"{prog}: --gpus {args.gpus} but WORLD_SIZE={world} (launch with matching values)")
     return world, int(environ.get("RANK", "0")), int(environ.get("LOCAL_RANK", "0"))
 
 

@@ -9,8 +9,12 @@ momentum 0.9, wd 1e-4) with the pruner's masks applied in the same pass (:213-21
 throughout (the reference's arithmetic).  Synthetic normalised inputs and labels (10 % ignore)
 resident in HBM; hash-initialised weights.
 
-    python bench_finetune.py [--steps K] [--warmup W] [--batch B]
+    python bench_finetune.py [--steps K] [--warmup W] [--batch B] [--gpus N]
     torchrun --nproc-per-node N bench_finetune.py --gpus N
+
+`--gpus N` outside torchrun spawns the N rank processes itself (bench.py's launcher); under
+torchrun a WORLD_SIZE different from --gpus is refused.  `--stub-step` (test hook, no GPU) runs
+a CPU stand-in step over gloo through the same launcher, seeding and max-over-ranks timing.
 
 Prints ONE JSON line (rank 0).  Not the driver's headline bench (bench.py is).
 """
@@ -28,7 +32,7 @@ sys.path.insert(0, os.path.join(REPO, "video-seg-model-compress_amd"))
 sys.path.insert(0, REPO)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -43,7 +47,10 @@ def parse():
                          "split-bf16 kernels (conv_x6, X6 patch kernels, wgrad_f32x3); BN and the head stay exact fp32")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    ap.add_argument("--stub-step", action="store_true",
+                    help="test hook: no GPU; gloo ranks run a CPU stand-in step (a gradient all-reduce of a "
+                         "rank-seeded tensor) through the same launcher and timing code")
+    return ap.parse_args(argv)
 
 
 def rmb_pruner(model, on_gpu):
@@ -137,14 +144,57 @@ def cpu_baseline(args, seconds):
                       f"at {h}x{w}, scaled x{ratio:.2f} to {args.height}x{args.width} images/s ({threads} threads)"}
 
 
-def main():
-    args = parse()
+def stub_main(args, world, rank):
+    """CPU stand-in of the fine-tune step (no GPU): each rank sums a rank-seeded "gradient" over
+    gloo (the DDP all-reduce's role), timed like the real step: barrier, max over ranks."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    g = torch.Generator().manual_seed(2000 + rank)
+    grad = torch.randn(4096, generator=g)
+
+    def step():
+        buf = grad.clone()
+        if world > 1:
+            dist.all_reduce(buf)
+        return buf
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        red = step()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    out = {"metric": "fine-tune images/s (stub)", "value": world * args.batch * args.steps / el, "unit": "images/s",
+           "n_gpus": world, "steps": args.steps, "ms_per_step": el / args.steps * 1e3, "scaling": "weak",
+           "reduced_sum": float(red.sum()), "rank_seed": 2000 + rank}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main(argv=None):
+    args = parse(argv)
+    import bench
+    wr = bench.resolve_world(args, prog="bench_finetune.py")
+    if wr is None:                            # --gpus N outside torchrun: spawn the ranks
+        sys.exit(bench.spawn_ranks(args.gpus, sys.argv[1:] if argv is None else argv, os.path.abspath(__file__)))
+    world, rank, local = wr
+    if args.stub_step:
+        return stub_main(args, world, rank)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

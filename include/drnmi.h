@@ -25,6 +25,15 @@
 extern "C" {
 #endif
 
+/* ABI version of the argument structs below (drnmi_conv_args, drnmi_wgrad_args).  The structs
+ * have grown by appended fields (x2.. in version 2, ws / ws_bytes in version 3); a caller built
+ * against another header must not pass them: check drnmi_abi_version() == DRNMI_ABI_VERSION and
+ * drnmi_conv_args_size() == sizeof(drnmi_conv_args) once after loading the library (drnmi/_lib.py
+ * does, and refuses a mismatched library). */
+#define DRNMI_ABI_VERSION 4
+int32_t drnmi_abi_version(void);
+int64_t drnmi_conv_args_size(void);
+
 enum drnmi_dtype { DRNMI_F32 = 0, DRNMI_BF16 = 1, DRNMI_U8 = 2, DRNMI_I64 = 3, DRNMI_I8 = 4, DRNMI_F32X3 = 5 };
 /* DRNMI_F32X3 (conv dtype only, the "fp32x" precision mode): x, res and y are fp32 NHWC as in
  * DRNMI_F32, wgt is three bf16 planes [3][cout_pad][k_pad] with w = w1 + w2 + w3 (an exact split
@@ -164,7 +173,7 @@ const char* drnmi_stem_layer1_kernel_name(const drnmi_conv_args* stem, const drn
 int64_t drnmi_front_pack_bytes(void);
 int drnmi_front_pack(const float* w0, const float* scale0, const float* shift0, const float* w1, const float* scale1,
                      const float* shift1, const float* w2, const float* scale2, const float* shift2,
-                     const float* mean3, const float* std3, int32_t bgr, void* out_host);
+                                      const float* mean3, const float* std3, int32_t bgr, void* out_host);
 int drnmi_front_supported(int32_t n, int32_t h, int32_t w);
 int drnmi_video_front_u8(const uint8_t* frames, const void* pack, void* y, int32_t n, int32_t h, int32_t w,
                          void* stream);
@@ -340,7 +349,8 @@ typedef struct drnmi_wgrad_args {
   int32_t ks, stride, pad, dil;
   int32_t accumulate;    /* 1: dw += ; 0: dw =                                            */
 } drnmi_wgrad_args;
-int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* args);
+int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* args);    /* room for either kernel */
+int64_t drnmi_conv_wgrad_f32_workspace_bytes(const drnmi_wgrad_args* args);/* drnmi_conv_wgrad_f32 only */
 int drnmi_conv_wgrad_f32(const drnmi_wgrad_args* args, void* stream);
 /* The same weight gradient in fp32-class split-bf16 arithmetic (the fp32x fine-tune: exact 3-way
  * bf16 split of dy and x, the six products above 2^-24 on the bf16 MFMA, fp32 accumulation);

@@ -66,3 +66,31 @@ def test_single_rank_stub():
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["n_gpus"] == 1 and len(d["per_rank"]) == 1
+
+
+FT_SMALL = ["--stub-step", "--steps", "3", "--warmup", "1", "--batch", "2"]
+
+
+def test_finetune_gpus2_spawns_two_ranks():
+    """bench_finetune.py --gpus 2 (config C4's launcher, semantic_seg_multigpu.py:467-468) starts
+    two ranks that all-reduce over the process group: the reduced sum is the sum of both ranks'
+    rank-seeded tensors, and rank 0 prints one line with n_gpus = 2."""
+    import torch
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench_finetune.py"), "--gpus", "2", *FT_SMALL],
+                       capture_output=True, text=True, timeout=240, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    want = sum(float(torch.randn(4096, generator=torch.Generator().manual_seed(2000 + k)).sum()) for k in (0, 1))
+    assert d["reduced_sum"] == pytest.approx(want, rel=1e-5, abs=1e-3)
+    assert d["value"] == pytest.approx(2 * 2 * 3 / (d["ms_per_step"] * 3 / 1e3), rel=1e-6)
+
+
+def test_finetune_world_mismatch_refused():
+    env = _env()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_PORT="29998")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench_finetune.py"), "--gpus", "1", *FT_SMALL],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

@@ -339,14 +339,16 @@ conv_x6_kernel(const drnmi_conv_args p) {
 }
 
 // split-K finish: v = sum of the partials in split order, then conv_x6's epilogue (scale / shift,
-// residual, ReLU, NHWC or strided store); one thread per 4 channels of a pixel
+// residual, ReLU, NHWC or strided store); one thread per 4 channels of a pixel.  y and res may
+// alias (the fp32x data gradient accumulates the residual gradient in place: out = res = prev):
+// every element is read and then written by the same thread, so neither pointer is __restrict__.
 __global__ void __launch_bounds__(256) x6_splitk_epilogue_kernel(const drnmi_conv_args p, int splits) {
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const int c4 = (p.cout + 3) / 4;
   const int64_t total = M * c4;
   const float* __restrict__ part = reinterpret_cast<const float*>(p.ws);
-  const float* __restrict__ res = reinterpret_cast<const float*>(p.res);
-  float* __restrict__ y = reinterpret_cast<float*>(p.y);
+  const float* res = reinterpret_cast<const float*>(p.res);
+  float* y = reinterpret_cast<float*>(p.y);
   const int hw_o = p.ho * p.wo;
   const int64_t pstride = M * p.cout;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
@@ -429,15 +431,29 @@ constexpr int kX6Bco[3] = {256, 128, 64};
 // MFMA time at the fraction of CUs busy in each round plus the partials' HBM round trip
 // (S x M x cout fp32 written and read); S = 1 unless that is >= 10 % faster.  Only with a
 // caller workspace (the fp32x training path): inference launches never split.
+int x6_num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
 int x6_splits(const drnmi_conv_args& p) {
+  // the partials are [split][m][cout] rows written as float4: only cout % 4 == 0 splits
+  if (p.cout % 4 != 0) return 1;
+  const int cus = x6_num_cus();
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const int64_t tiles = ((M + kBPX - 1) / kBPX) * ((p.cout + kX6Bco[x6_variant(p)] - 1) / kX6Bco[x6_variant(p)]);
   const int nk = p.k_pad / kBK;
   const double flops = 2.0 * static_cast<double>(M) * p.cout * p.k;
   auto cost = [&](int S) {
     const int64_t wgs = tiles * S;
-    const int64_t rounds = (wgs + 255) / 256;
-    const double busy = static_cast<double>(wgs) / static_cast<double>(rounds * 256);
+    const int64_t rounds = (wgs + cus - 1) / cus;
+    const double busy = static_cast<double>(wgs) / static_cast<double>(rounds * cus);
     double t = flops / (250e12 * busy);
     if (S > 1) t += 2.0 * S * static_cast<double>(M) * p.cout * 4.0 / 4e12 + 4e-6;
     return t;

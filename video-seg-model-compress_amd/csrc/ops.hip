@@ -697,6 +697,8 @@ extern "C" int drnmi_mask_apply_bits_f32(int32_t ntensors, float* const* weights
 }
 
 extern "C" const char* drnmi_version(void) { return "drnmi 0.1.0 gfx950"; }
+extern "C" int32_t drnmi_abi_version(void) { return DRNMI_ABI_VERSION; }
+extern "C" int64_t drnmi_conv_args_size(void) { return static_cast<int64_t>(sizeof(drnmi_conv_args)); }
 
 extern "C" int drnmi_confusion_matrix(const void* pred, int32_t pred_dtype, const void* label,
                                       int32_t label_dtype, int64_t npix, int32_t nclass, int64_t* hist,

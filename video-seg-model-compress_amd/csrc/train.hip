@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
   int64_t m_cur = m_begin + lm;
   int p_n = 0, p_oh = 0, p_ow = 0;
   {
-    const int mi = static_cast<int>(m_cur < p.M ? m_cur : 0);   // M < 2^31 (wgrad_check)
+    const int mi = static_cast<int>(m_cur < p.M ? m_cur : 0);   // M < 2^31 (wgrad_check rejects larger)
     p_n = mi / hw;
     const int q = mi - p_n * hw;
     p_oh = q / p.wo;
@@ -948,7 +948,14 @@ static bool wgrad_big_ok(const drnmi_wgrad_args& a) {
 static void wgrad_plan(const drnmi_wgrad_args& a, bool big, int* splits, int64_t* per) {
   const int K = a.ks * a.ks * a.cin_stride;
   const int tile = big ? kWT2 : kWT;
-  const int64_t slots = big ? 2 * 256 : 4 * 256;     // resident workgroups: LDS 73.7 KB / 36.9 KB each
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int64_t slots = (big ? 2 : 4) * static_cast<int64_t>(cus);   // resident workgroups: LDS 73.7 / 36.9 KB
   const int64_t M = static_cast<int64_t>(a.n) * a.ho * a.wo;
   const int64_t tiles = static_cast<int64_t>((a.cout + tile - 1) / tile) * ((K + tile - 1) / tile);
   int64_t smax = (M + 511) / 512;
@@ -1356,6 +1363,8 @@ static int wgrad_check(const drnmi_wgrad_args* a) {
   if (a->ho != (a->h + 2 * a->pad - a->dil * (a->ks - 1) - 1) / a->stride + 1 ||
       a->wo != (a->w + 2 * a->pad - a->dil * (a->ks - 1) - 1) / a->stride + 1)
     return DRNMI_EINVAL;
+  // pixel indices are int32 inside the tiles (wgrad_kernel / wgrad_x6_*: m_cur, m / hw)
+  if (static_cast<int64_t>(a->n) * a->ho * a->wo >= (int64_t(1) << 31)) return DRNMI_EINVAL;
   return DRNMI_OK;
 }
 
@@ -1376,9 +1385,19 @@ static int64_t wgrad_pre_bytes(const drnmi_wgrad_args& a) {
   return 3 * Cp * Mp * 2;
 }
 
+// the exact-f32 kernel's own partials (the f32x3 query below also holds the split-bf16 plan and
+// its dy planes)
+extern "C" int64_t drnmi_conv_wgrad_f32_workspace_bytes(const drnmi_wgrad_args* a) {
+  if (wgrad_check(a) != DRNMI_OK) return -1;
+  int splits;
+  int64_t per;
+  wgrad_plan(*a, false, &splits, &per);
+  return wgrad_partials_bytes(*a, splits);
+}
+
 extern "C" int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* a) {
   if (wgrad_check(a) != DRNMI_OK) return -1;
-  // the caller does not say which kernel will run (f32 or f32x3): room for either plan
+  // room for either kernel (f32 or f32x3): enough for both plans
   int splits;
   int64_t per;
   wgrad_plan(*a, false, &splits, &per);
@@ -1396,8 +1415,11 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   const int rc = wgrad_check(a);
   if (rc != DRNMI_OK) return rc;
   if (a->dy == nullptr || a->x == nullptr || a->dw == nullptr || a->ws == nullptr) return DRNMI_EINVAL;
-  if (a->ws_bytes < drnmi_conv_wgrad_workspace_bytes(a)) return DRNMI_EINVAL;
-  if ((reinterpret_cast<uintptr_t>(a->dy) | reinterpret_cast<uintptr_t>(a->x)) & 15) return DRNMI_EINVAL;
+  if (a->ws_bytes < (x6 ? drnmi_conv_wgrad_workspace_bytes(a) : drnmi_conv_wgrad_f32_workspace_bytes(a)))
+    return DRNMI_EINVAL;
+  // 16-B loads of dy / x; the dy bf16 planes in ws are LDS-DMA'd and stored as 16-B pieces
+  if ((reinterpret_cast<uintptr_t>(a->dy) | reinterpret_cast<uintptr_t>(a->x) | reinterpret_cast<uintptr_t>(a->ws)) & 15)
+    return DRNMI_EINVAL;
   if (a->dy_stride % 4 != 0) return DRNMI_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   WgradP p{};

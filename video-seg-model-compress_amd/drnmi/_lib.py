@@ -111,7 +111,11 @@ SIGNATURES = {
     "drnmi_quantize_i8": (ctypes.c_int, [_VP, _I32, _VP, _I64, _F32, _VP]),
     "drnmi_absmax": (ctypes.c_int, [_VP, _I32, _I64, _VP, _VP]),
     "drnmi_version": (ctypes.c_char_p, []),
+    "drnmi_abi_version": (ctypes.c_int32, []),
+    "drnmi_conv_args_size": (ctypes.c_int64, []),
+    "drnmi_conv_wgrad_f32_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
 }
+ABI_VERSION = 4          # include/drnmi.h DRNMI_ABI_VERSION
 
 _lib = None
 
@@ -132,6 +136,10 @@ def load(path: str | None = None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.drnmi_abi_version() != ABI_VERSION or lib.drnmi_conv_args_size() != ctypes.sizeof(ConvArgs):
+        raise RuntimeError(f"drnmi: {path} has ABI {lib.drnmi_abi_version()} / drnmi_conv_args of "
+                           f"{lib.drnmi_conv_args_size()} B; this binding expects {ABI_VERSION} / "
+                           f"{ctypes.sizeof(ConvArgs)} B (rebuild the library)")
     _lib = lib
     return lib
 

@@ -358,14 +358,16 @@ class TrainRunner:
                 wa.ho, wa.wo, wa.cout, wa.dy_stride = oh, ow, cout, dys
                 wa.ks, wa.stride, wa.pad, wa.dil = ks, s, p, d
                 wa.accumulate = 1 if acc[id(c.weight)] else 0
-                nb = lib.drnmi_conv_wgrad_workspace_bytes(ctypes.byref(wa))
+                # fp32x: every weight gradient is split-bf16 (the forward's small-channel layers
+                # run split on the patch kernels as well); fp32 sizes only its own partials
+                x3 = self.model.precision == "fp32x"
+                nb = (lib.drnmi_conv_wgrad_workspace_bytes if x3 else lib.drnmi_conv_wgrad_f32_workspace_bytes)(
+                    ctypes.byref(wa))
                 if nb < 0:
                     raise RuntimeError(f"wgrad {nd.name}: bad geometry")
                 ws = self._ws("_wg_ws", nb, dev)
                 wa.ws, wa.ws_bytes = ws.data_ptr(), ws.numel()
-                # fp32x: every weight gradient is split-bf16 (the forward's small-channel layers
-                # run split on the patch kernels as well)
-                wg = lib.drnmi_conv_wgrad_f32x3 if self.model.precision == "fp32x" else lib.drnmi_conv_wgrad_f32
+                wg = lib.drnmi_conv_wgrad_f32x3 if x3 else lib.drnmi_conv_wgrad_f32
                 _lib.check(wg(ctypes.byref(wa), sp), f"wgrad {nd.name}")
                 done.append(c.weight)
             if self.grad_ready is not None and done:
