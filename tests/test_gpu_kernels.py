@@ -74,8 +74,15 @@ def test_conv_bn_act(case, prec):
     got = y.float().permute(0, 3, 1, 2).cpu()
     err = (got - ref).abs().max().item()
     scale = ref.abs().max().item()
-    tol = (2e-5 * scale + 1e-6) if prec == "fp32" else 1.5e-2 * scale
-    assert err <= tol, f"max err {err} (scale {scale})"
+    if prec == "fp32":
+        assert err <= 2e-5 * scale + 1e-6, f"max err {err} (scale {scale})"
+    else:
+        # bf16 operands are exact inputs here (pre-rounded), products exact, fp32 accumulation and
+        # epilogue: the only errors are the output's bf16 rounding (<= 2^-9 |v|) and the fp32
+        # summation order, so elementwise |got - ref| <= 2^-8 |ref| + 1e-3 max|ref|
+        bound = 2.0 ** -8 * ref.abs() + 1e-3 * scale
+        worst = ((got - ref).abs() - bound).max().item()
+        assert worst <= 0, f"max err {err} (scale {scale}), bound exceeded by {worst}"
 
 
 @pytest.mark.parametrize("tile", [0, 1, 2, 3])
