@@ -6,6 +6,7 @@ tag=$1; src=$2; shift 2
 cd "$(dirname "$0")/../video-seg-model-compress_amd"
 python -c "import drnmi.build as b; b.build(verbose=False)"
 base=$(basename $src .hip)
-/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -I ../include "$@" -c csrc/$src -o build/${base}_$tag.o
+extra=$(python -c "import drnmi.build as b; print(' '.join(b.EXTRA.get('$src', [])))")
+/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -I ../include $extra "$@" -c csrc/$src -o build/${base}_$tag.o
 others=$(ls build/*.hip.o | grep -v "/$base.hip.o")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 build/${base}_$tag.o $others -o drnmi/libdrnmi_$tag.so

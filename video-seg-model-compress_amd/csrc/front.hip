@@ -27,9 +27,16 @@
 //    Layer1 is 12 MFMAs per pair row (own pixels, and the left/right neighbours in one B operand:
 //    lane half 0 takes pixel 2r-1, half 1 pixel 2r+2); layer2 (stride 2, 32 output channels on the
 //    rows, output pixel x = pair r) is 9 MFMAs per output row, all A rows useful.
+//  * Skewed, branch-free steps: step j computes stem rows 2j+3, 2j+4, layer1 rows 2j, 2j+1 and
+//    layer2 row j-1, each only from rows that EARLIER steps left in LDS, so the step's three MFMA
+//    chains are independent and the stem / layer1 epilogues (bf16 pack, ReLU, border masks, LDS
+//    writes) run under the later chains' MFMAs.  Border rows / columns are data (zero frame rows,
+//    per-lane masks, a per-lane row-case shift read from LDS), not branches, and frame rows are
+//    prefetched a step ahead into registers, so the loop waits only for those loads (vmcnt(4):
+//    the layer2 stores stay in flight).
 //  * Persistent waves: one 64-thread workgroup per SIMD (512 VGPRs: all 32 weight fragments live in
 //    registers), each walking a contiguous range of (frame, strip, layer2 row) work; a range start
-//    re-primes the walk with two warm-up steps.
+//    re-primes the walk with three extra steps.
 #include <math.h>
 #include <string.h>
 
@@ -42,6 +49,8 @@ namespace {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 // ---- packed parameters (drnmi_front_pack): A fragments [frag][lane][8 x 16 bit], then shifts
 constexpr int kFS = 11, kF1 = 12, kF2 = 9;             // MFMA A fragments: stem, layer1, layer2
@@ -60,8 +69,19 @@ constexpr int kRowB = 1040;              // ring row: image byte o at o (copy A)
 constexpr int kCopyB = 516;              //   (copy B: 8-B aligned where o % 8 == 4)
 constexpr int kXSp = 34 * 16;            // exchange: [plane 2][sp 2][pair slot 34][16 B], pair r at r + 1
 constexpr int kXSlot = 4 * kXSp;
-constexpr int kLds = kRing * kRowB + 8 * kXSlot;       // 4 stem + 4 layer1 exchange slots
-constexpr uint32_t kF16Hi = 0x64646464u;               // v_perm source of the f16 exponent byte 0x64
+constexpr int kXSlots = 6;               // exchange rows per activation (row mod 6)
+constexpr int kLdsZero = kRing * kRowB + 2 * kXSlots * kXSlot;
+constexpr int kLds = kLdsZero + 49 * 16 * 4;            // + the stem shift table
+constexpr uint32_t kF16Hi = 0x64646464u;
+#ifndef DRNMI_FR_PIN
+#define DRNMI_FR_PIN 0          // 1: keep the step's LDS operand reads ahead of its MFMAs (measured slower: 360 vs 342 us)
+#endif
+#ifndef DRNMI_FR_AGPRW
+#define DRNMI_FR_AGPRW 1        // weight fragments pinned to AGPRs
+#endif
+#ifndef DRNMI_FR_ABL
+#define DRNMI_FR_ABL 0          // diagnostic builds only: bit 0/1/2 skip the stem/layer1/layer2 MFMAs
+#endif                          // (operands still read), bit 3 the output stores               // v_perm source of the f16 exponent byte 0x64
 
 struct FrontParams {
   const uint8_t* x;
@@ -86,18 +106,32 @@ __device__ __forceinline__ f16x8 ld_frag_f16(const char* row, int off) {
 __device__ __forceinline__ bf16x8 ld_frag_bf16(const char* p) {
   return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
 }
+template <int ABL = 0>
 __device__ __forceinline__ f32x16 mfma_f16(const uint4& a, const f16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), b, c, 0, 0, 0);
+  if constexpr ((DRNMI_FR_ABL & ABL) != 0) {
+    asm volatile("" :: "v"(__builtin_bit_cast(u32x4_t, a)), "v"(__builtin_bit_cast(u32x4_t, b)));
+    return c;
+  } else {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), b, c, 0, 0, 0);
+  }
 }
+template <int ABL = 0>
 __device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
+  if constexpr ((DRNMI_FR_ABL & ABL) != 0) {
+    asm volatile("" :: "v"(__builtin_bit_cast(u32x4_t, a)), "v"(__builtin_bit_cast(u32x4_t, b)));
+    return c;
+  } else {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
+  }
 }
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 front_kernel(const FrontParams a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const ring = smem;
-  char* const xs = smem + kRing * kRowB;
+  char* const xs0 = smem + kRing * kRowB;                 // stem rows (slot = row mod 6)
+  char* const xs1 = xs0 + kXSlots * kXSlot;               // layer1 rows (slot = row mod 6)
+  float* const ctab = reinterpret_cast<float*>(xs1 + kXSlots * kXSlot);   // [7][7][16] stem shifts
   const int lane = threadIdx.x;
   const int r = lane & 31, hh = lane >> 5;
 
@@ -109,22 +143,36 @@ front_kernel(const FrontParams a) {
   for (int m = 0; m < kF1; ++m) a1[m] = pk[(kFS + m) * 64 + lane];
 #pragma unroll
   for (int m = 0; m < kF2; ++m) a2[m] = pk[(kFS + kF1 + m) * 64 + lane];
-  const float* c0t = reinterpret_cast<const float*>(a.pack + kOffC0);
+  if constexpr (DRNMI_FR_AGPRW) {
+    // keep the 32 weight fragments in AGPRs (MFMA A operands may be AGPRs): the VGPRs are left to
+    // the operand fragments and the accumulators, whose epilogue VALU would otherwise copy them out
+#pragma unroll
+    for (int m = 0; m < kFS; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, as[m]); asm volatile("" : "+a"(t)); as[m] = __builtin_bit_cast(uint4, t); }
+#pragma unroll
+    for (int m = 0; m < kF1; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, a1[m]); asm volatile("" : "+a"(t)); a1[m] = __builtin_bit_cast(uint4, t); }
+#pragma unroll
+    for (int m = 0; m < kF2; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, a2[m]); asm volatile("" : "+a"(t)); a2[m] = __builtin_bit_cast(uint4, t); }
+  }
   const float* c1t = reinterpret_cast<const float*>(a.pack + kOffC1);
   const float* c2t = reinterpret_cast<const float*>(a.pack + kOffC2);
-  f32x16 cs, c1, c2;
+  f32x16 c1, c2;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    cs[j] = c0t[(3 * 7 + 3) * 16 + j];                 // interior stem shift, reg j = channel j
     c1[j] = c1t[j];
     c2[j] = c2t[(j & 3) + 8 * (j >> 2) + 4 * hh];      // 32x32 D row (j&3) + 8(j>>2) + 4h = channel
   }
-  for (int i = lane * 16; i < kLds; i += 64 * 16) *reinterpret_cast<uint4*>(smem + i) = make_uint4(0, 0, 0, 0);
+  for (int i = lane * 16; i < kLdsZero; i += 64 * 16) *reinterpret_cast<uint4*>(smem + i) = make_uint4(0, 0, 0, 0);
+  for (int i = lane * 4; i < 49 * 16 * 4; i += 64 * 4)
+    *reinterpret_cast<float*>(reinterpret_cast<char*>(ctab) + i) =
+        *reinterpret_cast<const float*>(a.pack + kOffC0 + i);
 
   const int H = a.h, W = a.w;
   const int rowb = 3 * W;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.x), 0, a.n * H * rowb, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ys =
+      __builtin_amdgcn_make_buffer_rsrc(a.y, 0, a.n * a.h2 * a.w2 * 64, 0x00020000);
+  constexpr unsigned kOob = 0x80000000u;                 // buffer offset past num_records: loads 0, stores dropped
 
   int idx = blockIdx.x * a.per_wave;
   const int end = min(idx + a.per_wave, a.total);
@@ -139,7 +187,6 @@ front_kernel(const FrontParams a) {
     const int S0 = 2 * X0 - 3;                       // stem / layer1 column of pair 0, sub-pixel 0
     const int col = S0 + 2 * r + hh;                 // this lane's stem / layer1 pixel
     const uint32_t cmask = static_cast<unsigned>(col) < static_cast<unsigned>(W) ? 0xffffffffu : 0u;
-    const bool edge = S0 < 3 || S0 + 66 >= W;        // strip meets a left / right border
     const int ccl = col < 3 ? col : (col >= W - 3 ? 6 - (W - 1 - col) : 3);
     const int cc = ccl < 0 ? 0 : (ccl > 6 ? 6 : ccl);
     // frame bytes: image byte t <-> row byte fb0 + t (fb0 % 4 == 0); lane l converts t = 4l .. 4l+3
@@ -152,7 +199,7 @@ front_kernel(const FrontParams a) {
     const int oP = 4 + 12 * r + 16 * hh;             // P fragments: chunk j = lane half
     const int oX = 36 + 12 * r;                      // X fragments: chunk 2 of rows fr + lane half
     const int rdP = (r & 1) ? oP : kCopyB + oP;
-    const int rdX = (r & 1) ? oX : kCopyB + oX;
+    const int rdX = ((r & 1) ? oX : kCopyB + oX) + hh * kRowB;     // lane half h reads row fr + h
     // exchange offsets (plane 1 = +2 kXSp)
     const int xo_own = hh * kXSp + (r + 1) * 16;
     const int xo_lr = hh ? (r + 2) * 16 : kXSp + r * 16;     // half 0: pixel 2r-1, half 1: 2r+2
@@ -160,29 +207,31 @@ front_kernel(const FrontParams a) {
     const int x2 = X0 - 1 + r;
     const bool st_ok = r >= 1 && r <= kCols && x2 < a.w2;
     const int frame_row0 = n * H;
+    const float* ctl = ctab + cc * 16;               // this lane's column case
 
-    auto load_row = [&](int fr) -> uint32_t {
-      if (static_cast<unsigned>(fr) >= static_cast<unsigned>(H)) return 0u;
-      return __builtin_amdgcn_raw_buffer_load_b32(rs, (frame_row0 + fr) * rowb + cb, 0, 0);
+    auto row_ok = [&](int q) { return static_cast<unsigned>(q) < static_cast<unsigned>(H); };
+    auto load_row = [&](int fr) -> uint32_t {        // OOB offset for rows outside the frame: 0
+      const unsigned off = row_ok(fr) ? static_cast<unsigned>((frame_row0 + fr) * rowb + cb) : kOob;
+      return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
     };
     auto ring_put = [&](int fr, uint32_t raw) {
-      const bool ok = static_cast<unsigned>(fr) < static_cast<unsigned>(H);
-      const uint32_t f0 = ok ? (__builtin_amdgcn_perm(kF16Hi, raw, 0x04010400u) & fm0) : 0u;
-      const uint32_t f1 = ok ? (__builtin_amdgcn_perm(kF16Hi, raw, 0x04030402u) & fm1) : 0u;
+      const bool ok = row_ok(fr);
+      const uint32_t f0 = __builtin_amdgcn_perm(kF16Hi, raw, 0x04010400u) & (ok ? fm0 : 0u);
+      const uint32_t f1 = __builtin_amdgcn_perm(kF16Hi, raw, 0x04030402u) & (ok ? fm1 : 0u);
       char* row = ring + (fr & (kRing - 1)) * kRowB;
       *reinterpret_cast<uint2*>(row + 8 * lane) = make_uint2(f0, f1);
       *reinterpret_cast<uint32_t*>(row + kCopyB + 8 * lane) = f0;
       *reinterpret_cast<uint32_t*>(row + kCopyB + 8 * lane + 4) = f1;
     };
-    auto put_x = [&](int slot, const uint32_t (&v)[8]) {
-      char* p = xs + slot * kXSlot + xo_own;
+    auto slot6 = [](int row) { return (row + 12) % 6; };   // rows >= -12
+    auto put_x = [&](char* base, int row, const uint32_t (&v)[8]) {
+      char* p = base + slot6(row) * kXSlot + xo_own;
       *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<uint4*>(p + 2 * kXSp) = make_uint4(v[4], v[5], v[6], v[7]);
     };
-    auto stem_init = [&](int q) -> f32x16 {
-      const int rc = q < 3 ? q : (q >= H - 3 ? 6 - (H - 1 - q) : 3);
-      if (rc == 3 && !edge) return cs;
-      const float4* ct = reinterpret_cast<const float4*>(c0t + (rc * 7 + cc) * 16);
+    auto row_case = [&](int q) { const int v = q < 3 ? q : (q >= H - 3 ? 6 - (H - 1 - q) : 3); return v < 0 ? 0 : (v > 6 ? 6 : v); };
+    auto cinit = [&](int q) -> f32x16 {
+      const float4* ct = reinterpret_cast<const float4*>(ctl + row_case(q) * 7 * 16);
       f32x16 c;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -191,118 +240,129 @@ front_kernel(const FrontParams a) {
       }
       return c;
     };
-    // two stem rows q, q + 1 (frame rows q-3 .. q+4; X of the last pair row pairs with a zero kh)
-    auto stem_rows = [&](int q) {
-      // P: chunk (lane half) of frame row q-3+i; X term t of stem row q: chunk 2 of rows q-3+2t+h
-      // (kh = 2t, 2t+1; the kh = 7 half of t = 3 has zero weights), of stem row q+1: rows q-2+2t+h
+
+    // Skewed walk: step j computes stem rows 2j+3, 2j+4, layer1 rows 2j, 2j+1 and layer2 row j-1,
+    // each from rows the PREVIOUS steps wrote, so the three MFMA chains of a step are independent
+    // and the stem / layer1 epilogues run under the later chains' MFMAs.  Steps ya-3 .. yb cover
+    // layer2 rows ya .. yb-1 (edge steps compute rows nobody stores).  The frame rows step j reads
+    // (2j .. 2j+7) were converted by the end of step j-1.
+    const int j0 = ya - 3;
+    {
+      uint32_t raw[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) raw[i] = load_row(2 * j0 + i);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ring_put(2 * j0 + i, raw[i]);
+    }
+    uint32_t raw0 = load_row(2 * j0 + 8), raw1 = load_row(2 * j0 + 9);
+    for (int j = j0; j <= yb; ++j) {
+      const int q = 2 * j + 3;                       // stem rows q, q+1
+      // ---- operand reads (all from rows written by earlier steps)
       f16x8 bp[8], bx[4], bx2[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) bp[i] = ld_frag_f16(ring + ((q - 3 + i) & (kRing - 1)) * kRowB, rdP);
+      for (int i = 0; i < 8; ++i) bp[i] = ld_frag_f16(ring + ((2 * j + i) & (kRing - 1)) * kRowB, rdP);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        bx[t] = ld_frag_f16(ring + ((q - 3 + 2 * t + hh) & (kRing - 1)) * kRowB, rdX);
-        bx2[t] = ld_frag_f16(ring + ((q - 2 + 2 * t + hh) & (kRing - 1)) * kRowB, rdX);
+        // X term t of stem row q: chunk 2 of rows q-3+2t+h = 2j+2t+h; of row q+1: 2j+1+2t+h
+        // (the kh = 7 half of t = 3 has zero weights; its row aliases a live ring slot)
+        bx[t] = ld_frag_f16(ring + ((2 * j + 2 * t) & (kRing - 1)) * kRowB, rdX - ((((2 * j + 2 * t) & (kRing - 1)) == kRing - 1) ? hh * kRing * kRowB : 0));
+        bx2[t] = ld_frag_f16(ring + ((2 * j + 1 + 2 * t) & (kRing - 1)) * kRowB, rdX - ((((2 * j + 1 + 2 * t) & (kRing - 1)) == kRing - 1) ? hh * kRing * kRowB : 0));
       }
-      const bool ok0 = static_cast<unsigned>(q) < static_cast<unsigned>(H);
-      const bool ok1 = static_cast<unsigned>(q + 1) < static_cast<unsigned>(H);
-      f32x16 acc0 = stem_init(q), acc1 = stem_init(q + 1);
-#pragma unroll
-      for (int kh = 0; kh < 7; ++kh) {
-        acc0 = mfma_f16(as[kh], bp[kh], acc0);
-        acc1 = mfma_f16(as[kh], bp[kh + 1], acc1);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc0 = mfma_f16(as[7 + t], bx[t], acc0);
-        acc1 = mfma_f16(as[7 + t], bx2[t], acc1);
-      }
-      const uint32_t m0 = ok0 ? (edge ? cmask : 0xffffffffu) : 0u;
-      const uint32_t m1 = ok1 ? (edge ? cmask : 0xffffffffu) : 0u;
-      uint32_t v0[8], v1[8];
-#pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        v0[d] = relu_pk(acc0[2 * d], acc0[2 * d + 1]) & m0;
-        v1[d] = relu_pk(acc1[2 * d], acc1[2 * d + 1]) & m1;
-      }
-      put_x(q & 3, v0);
-      put_x((q + 1) & 3, v1);
-    };
-    // two layer1 rows p, p + 1 (stem rows p-1 .. p+2)
-    auto l1_rows = [&](int p) {
-      bf16x8 own_a[4], own_b[4], lr_a[4], lr_b[4];
+      const f32x16 ci0 = cinit(q), ci1 = cinit(q + 1);
+      bf16x8 o1a[4], o1b[4], lr1a[4], lr1b[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const char* sl = xs + ((p - 1 + i) & 3) * kXSlot;
-        own_a[i] = ld_frag_bf16(sl + xo_own);
-        own_b[i] = ld_frag_bf16(sl + 2 * kXSp + xo_own);
-        lr_a[i] = ld_frag_bf16(sl + xo_lr);
-        lr_b[i] = ld_frag_bf16(sl + 2 * kXSp + xo_lr);
+        const char* sl = xs0 + slot6(2 * j - 1 + i) * kXSlot;
+        o1a[i] = ld_frag_bf16(sl + xo_own);
+        o1b[i] = ld_frag_bf16(sl + 2 * kXSp + xo_own);
+        lr1a[i] = ld_frag_bf16(sl + xo_lr);
+        lr1b[i] = ld_frag_bf16(sl + 2 * kXSp + xo_lr);
       }
-      f32x16 acc0 = c1, acc1 = c1;
+      bf16x8 o2a[3], o2b[3], rr2[3];
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
-        acc0 = mfma_bf16(a1[4 * kh + 0], own_a[kh], acc0);
-        acc1 = mfma_bf16(a1[4 * kh + 0], own_a[kh + 1], acc1);
-        acc0 = mfma_bf16(a1[4 * kh + 1], own_b[kh], acc0);
-        acc1 = mfma_bf16(a1[4 * kh + 1], own_b[kh + 1], acc1);
-        acc0 = mfma_bf16(a1[4 * kh + 2], lr_a[kh], acc0);
-        acc1 = mfma_bf16(a1[4 * kh + 2], lr_a[kh + 1], acc1);
-        acc0 = mfma_bf16(a1[4 * kh + 3], lr_b[kh], acc0);
-        acc1 = mfma_bf16(a1[4 * kh + 3], lr_b[kh + 1], acc1);
+        const char* sl = xs1 + slot6(2 * j - 3 + kh) * kXSlot;
+        o2a[kh] = ld_frag_bf16(sl + xo_own);
+        o2b[kh] = ld_frag_bf16(sl + 2 * kXSp + xo_own);
+        rr2[kh] = ld_frag_bf16(sl + xo_r);
       }
-      const bool ok0 = static_cast<unsigned>(p) < static_cast<unsigned>(H);
-      const bool ok1 = static_cast<unsigned>(p + 1) < static_cast<unsigned>(H);
-      const uint32_t m0 = ok0 ? (edge ? cmask : 0xffffffffu) : 0u;
-      const uint32_t m1 = ok1 ? (edge ? cmask : 0xffffffffu) : 0u;
-      uint32_t v0[8], v1[8];
+      // every operand of the step is in flight before the first MFMA waits on one
+      if constexpr (DRNMI_FR_PIN) __builtin_amdgcn_sched_barrier(0);
+      // ---- stem (2 x 11 MFMAs)
+      f32x16 s0 = ci0, s1 = ci1;
 #pragma unroll
-      for (int d = 0; d < 8; ++d) {
-        v0[d] = relu_pk(acc0[2 * d], acc0[2 * d + 1]) & m0;
-        v1[d] = relu_pk(acc1[2 * d], acc1[2 * d + 1]) & m1;
+      for (int kh = 0; kh < 7; ++kh) {
+        s0 = mfma_f16<1>(as[kh], bp[kh], s0);
+        s1 = mfma_f16<1>(as[kh], bp[kh + 1], s1);
       }
-      put_x(4 + (p & 3), v0);
-      put_x(4 + ((p + 1) & 3), v1);
-    };
-    auto l2_row = [&](int y) {
-      bf16x8 own_a[3], own_b[3], rr[3];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s0 = mfma_f16<1>(as[7 + t], bx[t], s0);
+        s1 = mfma_f16<1>(as[7 + t], bx2[t], s1);
+      }
+      // ---- layer1 (2 x 12 MFMAs)
+      f32x16 l0 = c1, l1 = c1;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
-        const char* sl = xs + (4 + ((2 * y - 1 + kh) & 3)) * kXSlot;
-        own_a[kh] = ld_frag_bf16(sl + xo_own);
-        own_b[kh] = ld_frag_bf16(sl + 2 * kXSp + xo_own);
-        rr[kh] = ld_frag_bf16(sl + xo_r);
+        l0 = mfma_bf16<2>(a1[4 * kh + 0], o1a[kh], l0);
+        l1 = mfma_bf16<2>(a1[4 * kh + 0], o1a[kh + 1], l1);
+        l0 = mfma_bf16<2>(a1[4 * kh + 1], o1b[kh], l0);
+        l1 = mfma_bf16<2>(a1[4 * kh + 1], o1b[kh + 1], l1);
+        l0 = mfma_bf16<2>(a1[4 * kh + 2], lr1a[kh], l0);
+        l1 = mfma_bf16<2>(a1[4 * kh + 2], lr1a[kh + 1], l1);
+        l0 = mfma_bf16<2>(a1[4 * kh + 3], lr1b[kh], l0);
+        l1 = mfma_bf16<2>(a1[4 * kh + 3], lr1b[kh + 1], l1);
       }
-      f32x16 acc = c2;
+      // ---- stem epilogue (overlaps the layer1 / layer2 MFMAs)
+      {
+        const uint32_t m0 = row_ok(q) ? cmask : 0u, m1 = row_ok(q + 1) ? cmask : 0u;
+        uint32_t v0[8], v1[8];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+          v0[d] = relu_pk(s0[2 * d], s0[2 * d + 1]) & m0;
+          v1[d] = relu_pk(s1[2 * d], s1[2 * d + 1]) & m1;
+        }
+        put_x(xs0, q, v0);
+        put_x(xs0, q + 1, v1);
+      }
+      // ---- layer2 (9 MFMAs): row j - 1
+      f32x16 t2 = c2;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
-        acc = mfma_bf16(a2[3 * kh + 0], own_a[kh], acc);
-        acc = mfma_bf16(a2[3 * kh + 1], own_b[kh], acc);
-        acc = mfma_bf16(a2[3 * kh + 2], rr[kh], acc);
+        t2 = mfma_bf16<4>(a2[3 * kh + 0], o2a[kh], t2);
+        t2 = mfma_bf16<4>(a2[3 * kh + 1], o2b[kh], t2);
+        t2 = mfma_bf16<4>(a2[3 * kh + 2], rr2[kh], t2);
       }
-      if (st_ok) {
-        bf16_t* o = a.y + ((static_cast<int64_t>(n) * a.h2 + y) * a.w2 + x2) * 32 + 4 * hh;
+      // ---- layer1 epilogue
+      {
+        const int p = 2 * j;
+        const uint32_t m0 = row_ok(p) ? cmask : 0u, m1 = row_ok(p + 1) ? cmask : 0u;
+        uint32_t v0[8], v1[8];
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<uint2*>(o + 8 * g) = make_uint2(relu_pk(acc[4 * g], acc[4 * g + 1]),
-                                                            relu_pk(acc[4 * g + 2], acc[4 * g + 3]));
+        for (int d = 0; d < 8; ++d) {
+          v0[d] = relu_pk(l0[2 * d], l0[2 * d + 1]) & m0;
+          v1[d] = relu_pk(l1[2 * d], l1[2 * d + 1]) & m1;
+        }
+        put_x(xs1, p, v0);
+        put_x(xs1, p + 1, v1);
       }
-    };
-
-    // prologue: the walk starts two steps early (ya - 2) so that stem rows 2ya-3 .. 2ya and layer1
-    // row 2ya-1 exist when layer2 row ya is computed; step y converts frame rows 2y+4, 2y+5
-    const int y0 = ya - 2;
-    for (int i = 0; i < 6; ++i) ring_put(2 * y0 - 2 + i, load_row(2 * y0 - 2 + i));
-    uint32_t raw0 = load_row(2 * y0 + 4), raw1 = load_row(2 * y0 + 5);
-    for (int y = y0; y < yb; ++y) {
-      ring_put(2 * y + 4, raw0);
-      ring_put(2 * y + 5, raw1);
-      if (y + 1 < yb) {
-        raw0 = load_row(2 * y + 6);
-        raw1 = load_row(2 * y + 7);
+      // ---- layer2 epilogue: NHWC bf16 stores, lane half h holds channels 8g + 4h .. + 3
+      {
+        const int y = j - 1;
+        const bool store = st_ok && y >= ya && y < yb && (DRNMI_FR_ABL & 8) == 0;
+        const unsigned off =
+            store ? static_cast<unsigned>(((static_cast<int>(n) * a.h2 + y) * a.w2 + x2) * 64 + 8 * hh) : kOob;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint2 v = make_uint2(relu_pk(t2[4 * g], t2[4 * g + 1]), relu_pk(t2[4 * g + 2], t2[4 * g + 3]));
+          __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{v.x, v.y}, ys, off, 16 * g, 0);
+        }
       }
-      stem_rows(2 * y + 1);
-      if (y > y0) l1_rows(2 * y);
-      if (y >= ya) l2_row(y);
+      // ---- frame rows 2j+8, 2j+9 into the ring (over rows 2j, 2j+1: read above), next loads
+      ring_put(2 * j + 8, raw0);
+      ring_put(2 * j + 9, raw1);
+      raw0 = load_row(2 * j + 10);
+      raw1 = load_row(2 * j + 11);
     }
   }
 }

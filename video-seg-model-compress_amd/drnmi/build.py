@@ -25,6 +25,11 @@ CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE,
           "-Wno-unused-function"]
 
 
+# per-source extra flags.  front.hip: MFMA results in VGPRs (the weights are pinned to AGPRs in the
+# source), so the epilogues read the accumulators without v_accvgpr_read copies
+EXTRA = {"front.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+
+
 def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
 
@@ -36,7 +41,7 @@ def _headers_mtime():
 
 
 def _compile(src: str, obj: str) -> None:
-    cmd = [HIPCC, *CFLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *EXTRA.get(os.path.basename(src), []), "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
