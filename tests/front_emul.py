@@ -46,8 +46,8 @@ def unpack(blob: np.ndarray):
         a = np.concatenate([v[:, :32, :], v[:, 32:, :]], axis=2)      # [m][32][16]
         frags.append(a)
         off += nf * 64 * 16
-    c0 = blob[off:off + 49 * 16 * 4].view(np.float32).reshape(7, 7, 16).astype(np.float64)
-    off += 49 * 16 * 4
+    c0 = blob[off:off + 64 * 16 * 4].view(np.float32).reshape(8, 8, 16).astype(np.float64)[:7, :7]
+    off += 64 * 16 * 4
     c1 = blob[off:off + 64].view(np.float32).astype(np.float64)
     off += 64
     c2 = blob[off:off + 128].view(np.float32).astype(np.float64)
