@@ -22,6 +22,15 @@
 #ifndef DRNMI_STAG_OLDINIT
 #define DRNMI_STAG_OLDINIT 0  // diagnostic: residual loaded and added before the prologue DMA (A/B)
 #endif
+#ifndef DRNMI_STAG_MAP
+#define DRNMI_STAG_MAP 0    // tile deal: 0 XCD-major rows x both channel blocks; 1 XCD-stationary channel
+#endif                      // block (XCD x keeps block x % 2, XCD pairs split the pixel tiles)
+#ifndef DRNMI_STAG_XAUX
+#define DRNMI_STAG_XAUX 0   // cache policy of the input-strip DMA (2 = nt: streaming)
+#endif
+#ifndef DRNMI_STAG_WAUX
+#define DRNMI_STAG_WAUX 0   // cache policy of the weight DMA
+#endif
 #ifndef DRNMI_STAG_PRIO
 #define DRNMI_STAG_PRIO 0   // diagnostic: s_setprio 1 for the lagging half (waves 4-7)
 #endif
@@ -64,6 +73,18 @@ namespace {
 //
 // WCO = channels per wave (tile = 2 WCO output channels x 256 pixels): 128 (the 256-channel tile
 // of layer5-8) or 64 (128-channel convs: D-22 layer4); GR = WCO / 32 MFMA groups per substep.
+// Tile deal (workgroups go to XCD bid % 8).  Default: XCD-major -- XCD x takes a contiguous run of
+// (pixel tile, channel block) tiles, i.e. its rows x both channel blocks.  DRNMI_STAG_MAP 1: with
+// two channel blocks, XCD x keeps block x % 2 for its whole share and XCD pair x / 2 takes a
+// quarter of the pixel tiles, in the same row order on both XCDs of the pair.
+__device__ __forceinline__ int stag_tile(int bid, int ntiles, int nco) {
+  if (DRNMI_STAG_MAP == 1 && nco == 2 && ntiles % 8 == 0) {
+    const int xcd = bid & 7, j = bid >> 3;
+    return ((xcd >> 1) * (ntiles / 8) + j) * 2 + (xcd & 1);
+  }
+  return xcd_remap2(bid, ntiles);
+}
+
 template <typename T, bool X2, int WCO = 128>
 __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   using K = KT<T>;
@@ -98,7 +119,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
   const int lrow = lane >> 3;
   const int lslot = lane & 7;
 
-  const int tile = xcd_remap2(blockIdx.x, ntiles);
+  const int tile = stag_tile(blockIdx.x, ntiles, nco);
   const int px0 = (tile / nco) * kBPX;
   const int co0 = (tile % nco) * BCO;
   const int s_n = px0 / hw_o;
@@ -114,9 +135,13 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
       const_cast<void*>(p.wgt), 0, p.cout_pad * p.k_pad * K::ESZ, 0x00020000);
   typedef __attribute__((address_space(3))) void lds_t;
   bool in_loop = false;                              // DRNMI_STAG_ABL bit 0: no DMA once the loop runs
-  auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, int soff, int lds_byte) {
+  auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, int soff, int lds_byte) {   // weights
     if ((DRNMI_STAG_ABL & 1) && in_loop) return;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, DRNMI_STAG_WAUX);
+  };
+  auto dma_x = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, int soff, int lds_byte) { // input strips
+    if ((DRNMI_STAG_ABL & 1) && in_loop) return;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, DRNMI_STAG_XAUX);
   };
   // weight rows (wave*4 + i)*8 + lrow: the swizzle depends on i only through its parity
   uint32_t a_off[2];
@@ -146,7 +171,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     const bool row_ok = static_cast<unsigned>(ih) < static_cast<unsigned>(H);   // wave-uniform
     const uint32_t voff = ok && row_ok ? static_cast<uint32_t>((iw * cin + (lslot ^ (R & 7)) * CE) * K::ESZ) : kOOB;
     const int soff = row_ok ? ((s_n * H + ih) * W * cin + cb * BK) * K::ESZ : 0;
-    dma(rs_x, voff, soff, 2 * AB + buf * kStripBytes + j * 1024);
+    dma_x(rs_x, voff, soff, 2 * AB + buf * kStripBytes + j * 1024);
   };
   // X2: share sh of x2 step e's B -- pixel R of the tile sampled at stride2 in x2, channels
   // e*BK..; strip row R, chunk slot c ^ (R & 7) as the tap strips (read at kw offset 0)
@@ -160,7 +185,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
       const uint32_t voff = R < kBPX ? static_cast<uint32_t>(((s_ow0 + R) * p.stride2 * p.cin2 + (lslot ^ (R & 7)) * CE) * K::ESZ)
                                      : kOOB;
       const int soff = ((s_n * p.h2 + s_oh * p.stride2) * p.w2 * p.cin2 + e * BK) * K::ESZ;
-      dma(rs_x2, voff, soff, 2 * AB + buf * kStripBytes + j * 1024);
+      dma_x(rs_x2, voff, soff, 2 * AB + buf * kStripBytes + j * 1024);
     }
   };
   auto issue_next_strip = [&](int g, int buf, int sh) {   // the strip of group g + 1 (or x2 step 0)
