@@ -95,7 +95,7 @@ def test_train_steps_match_reference(fused_mask):
 
 
 # D-54 (Bottleneck, 2048-channel 1x1 convs) has many pre-activations near zero: the reference's
-# own fp32 CPU gradients are 6e-3 (max-abs rel) away from fp64 on this case (scripts/train_diag.py)
+# own fp32 CPU gradients are 6e-3 (max-abs rel) away from fp64 on this case (scripts/archive/train_diag.py)
 @pytest.mark.parametrize("arch,seed,shape,tol", [("drn_d_38", 2, (1, 3, 64, 64), 1e-3),
                                                  ("drn_d_54", 3, (2, 3, 128, 128), 2e-2),
                                                  ("drn_d_22", 4, (1, 3, 72, 40), 1e-3)])
