@@ -37,6 +37,10 @@ typedef __attribute__((address_space(1))) const void g_void_t;
 
 __device__ uint4 g_x6_zero[64];   // zero-initialised: the source of padded taps / rows
 
+#ifndef DRNMI_X6_PIPE
+#define DRNMI_X6_PIPE 1     // 0: the round-3 step (A planes read right before their MFMA group, B split up front)
+#endif
+
 constexpr int kBPX = 256;   // pixels per tile
 constexpr int kBK = 32;     // input channels per K step
 
@@ -54,6 +58,13 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 __device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ (((row >> 3) & 1) * 3); }
 __device__ __forceinline__ int swz128(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }   // fp32 B rows
 
+
+// one ds_read_b128 at LDS byte address base + OFF (smem is the kernel's only LDS object: byte 0)
+template <int OFF, typename V>
+__device__ __forceinline__ void ds_rd(V& dst, uint32_t base) {
+  static_assert(sizeof(V) == 16 && OFF >= 0 && OFF < 65536, "ds_read_b128 offset");
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(OFF));
+}
 
 template <int WCO, int WC>
 struct X6Cfg {
@@ -109,12 +120,13 @@ conv_x6_kernel(const drnmi_conv_args p) {
   const char* zero_src = reinterpret_cast<const char*>(g_x6_zero) + lane * 16;
 
   // --- A pieces: 16 rows of 64 B each; linear row R = plane * BCO + r
-  int64_t a_off[C::A_PW];
+  // element offsets < 2^31: 3 planes x cout_pad x k_pad bf16 (x6_conv_dispatch checks)
+  int32_t a_off[C::A_PW];
 #pragma unroll
   for (int i = 0; i < C::A_PW; ++i) {
     const int R = (wave * C::A_PW + i) * 16 + (lane >> 2);
     const int pl = R / C::BCO, r = R - pl * C::BCO;
-    a_off[i] = pl * plane_stride + static_cast<int64_t>(co0 + r) * p.k_pad + swz64(r, lane & 3) * 8;
+    a_off[i] = static_cast<int32_t>(pl * plane_stride + static_cast<int64_t>(co0 + r) * p.k_pad + swz64(r, lane & 3) * 8);
   }
   // --- B pieces: 8 pixel rows of 128 B; (ih0, iw0) of tap (0,0) and the element offset of the
   // row's chunk at that tap (only dereferenced when the tap is inside the image)
@@ -153,7 +165,7 @@ conv_x6_kernel(const drnmi_conv_args p) {
   auto issue_piece = [&](const StepP& sp, int stage, int i) {
     char* sa = smem + stage * C::STAGE;
     if (i < C::A_PW) {
-      glds16(wt + a_off[i] + sp.k0, sa + (wave * C::A_PW + i) * 1024);
+      glds16(wt + (static_cast<uint32_t>(a_off[i]) + sp.k0), sa + (wave * C::A_PW + i) * 1024);
     } else {
       const int j = i - C::A_PW;
       const bool ok = static_cast<unsigned>(b_ih[j] + sp.dh) < static_cast<unsigned>(H) &&
@@ -176,6 +188,127 @@ conv_x6_kernel(const drnmi_conv_args p) {
 
   for (int t = 0; t < C::NST - 1 && t < nk; ++t) issue(t, t);
 
+#if DRNMI_X6_PIPE
+  const uint32_t a_lane = static_cast<uint32_t>((wc * WCO + fr) * 64 + swz64(fr, fq) * 16);
+  const uint32_t b_lane0 = static_cast<uint32_t>((wp * 64 + fr) * 128 + swz128(fr, 2 * fq) * 16);
+  const uint32_t b_lane1 = static_cast<uint32_t>((wp * 64 + fr) * 128 + swz128(fr, 2 * fq + 1) * 16);
+  // A plane `pl` of fragment fm: rows fm * 16 apart keep the swizzle (swz64 reads row bit 3 only)
+  auto ds_rd_fm = [&](bf16x8& dst, uint32_t base, int fm, int pl) {
+    switch (fm * 3 + pl) {
+#define X6_RD(I) case I: ds_rd<(I / 3) * 1024 + (I % 3) * C::A_PLANE>(dst, base); break;
+      X6_RD(0) X6_RD(1) X6_RD(2) X6_RD(3) X6_RD(4) X6_RD(5) X6_RD(6) X6_RD(7) X6_RD(8) X6_RD(9) X6_RD(10)
+      X6_RD(11) X6_RD(12) X6_RD(13) X6_RD(14) X6_RD(15) X6_RD(16) X6_RD(17) X6_RD(18) X6_RD(19) X6_RD(20)
+      X6_RD(21) X6_RD(22) X6_RD(23)
+#undef X6_RD
+      default: break;
+    }
+  };
+  // per step (each accumulator keeps the six products in the order below, so results are
+  // bit-identical to the unpipelined form): B fragments are read and split once (splitting b2 / b3
+  // under fm 0's first groups instead spilled 9 VGPRs); the three A
+  // planes of fragment fm + 1 are read while fm's MFMAs run, each into the registers a group of
+  // fm has just retired (plane 3 after group 1, plane 2 after group 4, plane 1 after group 6),
+  // 8-20 MFMAs ahead of their first use
+  constexpr int PPF = (C::GLDS + C::FM - 1) / C::FM;
+  for (int t = 0; t < nk; ++t) {
+    const int newer = ((nk - 1) < (t + C::NST - 2) ? (nk - 1) : (t + C::NST - 2)) - t;
+    if (C::NST >= 3 && newer >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::GLDS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const bool nxt = t + C::NST - 1 < nk;
+    const StepP spn = step_params(nxt ? t + C::NST - 1 : t);
+    const int nst = (t + C::NST - 1) % C::NST;
+
+    // A fragment reads as inline-asm ds_read_b128 with compile-time offsets (the swizzle does not
+    // depend on fm) and hand-counted lgkmcnt waits: hipcc's own waits drained every read in flight
+    // before each group (lgkmcnt(0))
+    const uint32_t st_off = static_cast<uint32_t>((t % C::NST) * C::STAGE);
+    const uint32_t va = a_lane + st_off, vb0 = b_lane0 + st_off, vb1 = b_lane1 + st_off;
+    bf16x8 a3, a2, a1;
+    ds_rd<2 * C::A_PLANE>(a3, va);                     // fragment 0's planes, then the B rows
+    ds_rd<C::A_PLANE>(a2, va);
+    ds_rd<0>(a1, va);
+    float4 blo[C::FN], bhi[C::FN];                     // (hipcc waits for these: lgkmcnt(0))
+#pragma unroll
+    for (int fn = 0; fn < C::FN; ++fn) {
+      blo[fn] = *reinterpret_cast<const float4*>(smem + vb0 + C::A_BYTES + fn * 2048);
+      bhi[fn] = *reinterpret_cast<const float4*>(smem + vb1 + C::A_BYTES + fn * 2048);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // split passes: u1 = bf16(x), u2 = bf16(x - u1), u3 = bf16(x - u1 - u2) (common.h split3)
+    bf16x8 b1[C::FN], b2[C::FN], b3[C::FN];
+    auto pairs = [&](int fn, int i) {
+      const float4& v = i < 2 ? blo[fn] : bhi[fn];
+      return (i & 1) ? f32x2_t{v.z, v.w} : f32x2_t{v.x, v.y};
+    };
+    auto split_b1 = [&](int fn) {
+      uint32_t u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) u[i] = pk_bf16x2(pairs(fn, i));
+      b1[fn] = __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
+    };
+    auto split_b2 = [&](int fn) {
+      const uint4 w1 = __builtin_bit_cast(uint4, b1[fn]);
+      const uint32_t v1[4] = {w1.x, w1.y, w1.z, w1.w};
+      uint32_t u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) u[i] = pk_bf16x2(pairs(fn, i) - widen_bf16x2(v1[i]));
+      b2[fn] = __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
+    };
+    auto split_b3 = [&](int fn) {
+      const uint4 w1 = __builtin_bit_cast(uint4, b1[fn]);
+      const uint4 w2 = __builtin_bit_cast(uint4, b2[fn]);
+      const uint32_t v1[4] = {w1.x, w1.y, w1.z, w1.w};
+      const uint32_t v2[4] = {w2.x, w2.y, w2.z, w2.w};
+      uint32_t u[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) u[i] = pk_bf16x2((pairs(fn, i) - widen_bf16x2(v1[i])) - widen_bf16x2(v2[i]));
+      b3[fn] = __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
+    };
+#pragma unroll
+    for (int fn = 0; fn < C::FN; ++fn) { split_b1(fn); split_b2(fn); split_b3(fn); }
+    auto grp = [&](int fm, const bf16x8& a, const bf16x8 (&b)[C::FN]) {
+#pragma unroll
+      for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[fn], acc[fm][fn], 0, 0, 0);
+    };
+#pragma unroll
+    for (int fm = 0; fm < C::FM; ++fm) {
+      // read order per fragment: a3(fm) after group 1 of fm - 1, a2(fm) after its group 4, a1(fm)
+      // after its group 6 (each into the registers that group retired); before group 1 the
+      // newer reads in flight are a2(fm), a1(fm)
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      grp(fm, a3, b1);                                   // 1: a3 b1
+      if (fm + 1 < C::FM) ds_rd_fm(a3, va, fm + 1, 2);
+      // branch-free (a branch here let the reads above sink past it, next to their MFMAs): the
+      // last step re-fetches its own K step into the stage step t - 1 used, which nobody reads
+#pragma unroll
+      for (int k = 0; k < PPF; ++k)
+        if (fm * PPF + k < C::GLDS) issue_piece(spn, nst, fm * PPF + k);
+      // a2(fm) landed: newer in flight a1(fm), a3(fm + 1)
+      if (fm + 1 < C::FM) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      grp(fm, a2, b2);                                   // 2: a2 b2
+      // a1(fm) landed: newer in flight a3(fm + 1)
+      if (fm + 1 < C::FM) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      grp(fm, a1, b3);                                   // 3: a1 b3
+      __builtin_amdgcn_sched_barrier(0);
+      grp(fm, a2, b1);                                   // 4: a2 b1
+      if (fm + 1 < C::FM) ds_rd_fm(a2, va, fm + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      grp(fm, a1, b2);                                   // 5: a1 b2
+      __builtin_amdgcn_sched_barrier(0);
+      grp(fm, a1, b1);                                   // 6: a1 b1
+      if (fm + 1 < C::FM) ds_rd_fm(a1, va, fm + 1, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last step's re-fetch
+#else
   // per step: B fragments read and split once; then per channel fragment fm, its three A
   // planes are read and the next step's DMA pieces go out between the MFMA groups (PPF per
   // group, behind the A reads), pinned with sched_barrier (a one-group-ahead A prefetch needs
@@ -254,6 +387,7 @@ conv_x6_kernel(const drnmi_conv_args p) {
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+#endif
 
   // --- split-K: raw fp32 partial sums [split][m][cout]; x6_splitk_epilogue_kernel finishes
   if (gridDim.y > 1) {
@@ -494,6 +628,7 @@ int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   const int v = x6_variant(p);
   // every weight row a tile's DMA reads must exist in each plane
   if ((p.cout + kX6Bco[v] - 1) / kX6Bco[v] * kX6Bco[v] > p.cout_pad) return DRNMI_EINVAL;
+  if (3 * static_cast<int64_t>(p.cout_pad) * p.k_pad >= (int64_t(1) << 31)) return DRNMI_EINVAL;
   int S = 1;
   if (p.ws != nullptr) {
     S = x6_splits(p);
