@@ -306,6 +306,20 @@ int drnmi_pack_conv_weight(const float* w, int32_t cout, int32_t cin, int32_t ks
                            int32_t rows_pad, int32_t k_pad, int32_t mode, const float* row_scale,
                            int32_t out_dtype, void* out, void* stream);
 
+/* Batched form of drnmi_pack_conv_weight (F32 output) + drnmi_split3_bf16 for a whole network:
+ * one launch packs every entry of a device-resident table (the fine-tune re-packs all forward
+ * and data-gradient weights after each SGD step; per layer that was 4 launches of ~6 us).
+ * table: DEVICE memory, n entries of DRNMI_PACK_ENTRY_WORDS int64 each:
+ *   [0] w (const float*), [1] out (float* [rows_pad][k_pad]), [2] planes (bf16 [3][rows_pad*k_pad]
+ *   or 0), [3] cout, [4] cin, [5] ks, [6] kin_stride, [7] rows_pad, [8] k_pad, [9] mode (0 | 1,
+ *   as drnmi_pack_conv_weight, no row scale), [10] first element index of the entry (prefix sum
+ *   of rows_pad*k_pad over the entries before it), [11] 0.
+ * total = sum of rows_pad*k_pad.  Values are bit-identical to the per-layer calls.
+ * drnmi_pack_table_check validates a HOST copy of the table before it is uploaded. */
+#define DRNMI_PACK_ENTRY_WORDS 12
+int drnmi_pack_table_check(const int64_t* table_host, int32_t n, int64_t* total_out);
+int drnmi_pack_conv_weights_batched(const int64_t* table, int32_t n, int64_t total, void* stream);
+
 /* Workspace bytes for the per-channel reductions over `rows` x `channels` (power of two >= 4). */
 int64_t drnmi_reduce_workspace_bytes(int64_t rows, int32_t channels);
 

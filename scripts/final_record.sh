@@ -1,7 +1,7 @@
 #!/bin/bash
 # Final-tree record: full GPU suite, smoke, every bench line (bf16 headline with exact_mode, fp32,
 # fp32x, int8, int8 + SRMB (C5), host frames, C3 block-sparse 16x16 dense/sparse, fine-tune fp32 /
-# fp32x).  usage: bash scripts/r5_final.sh OUTNAME
+# fp32x).  usage: bash scripts/final_record.sh OUTNAME
 set -u
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -4,6 +4,8 @@ import os
 import re
 import subprocess
 
+import numpy as np
+
 from drnmi import _lib
 from drnmi.build import LIB_PATH, build
 
@@ -48,6 +50,24 @@ def test_argument_validation_without_gpu():
     assert lib.drnmi_up8_logsoftmax_argmax(None, None, None, None, 2, 1, 19, 8, 8, None) == -1
     assert lib.drnmi_mask_apply_f32(-1, None, None, None, None) == -1
     assert lib.drnmi_mask_apply_f32(0, None, None, None, None) == 0
+
+
+def test_pack_table_check_without_gpu():
+    """The batched weight-pack table is validated on the host (prefix sums, geometry)."""
+    lib = _lib.load()
+    rows = [[0x1000, 0x2000, 0, 64, 32, 3, 32, 64, 288, 0, 0, 0],
+            [0x1000, 0x3000, 0x4000, 64, 32, 3, 64, 32, 576, 1, 64 * 288, 0]]
+    tab = np.array(rows, dtype=np.int64)
+    tot = ctypes.c_int64(0)
+    assert lib.drnmi_pack_table_check(tab.ctypes.data_as(ctypes.c_void_p), 2, ctypes.byref(tot)) == 0
+    assert tot.value == 64 * 288 + 32 * 576
+    bad = tab.copy()
+    bad[1, 10] += 1                                   # wrong prefix
+    assert lib.drnmi_pack_table_check(bad.ctypes.data_as(ctypes.c_void_p), 2, ctypes.byref(tot)) == -1
+    bad = tab.copy()
+    bad[0, 8] = 100                                   # k_pad < ks * ks * kin_stride
+    assert lib.drnmi_pack_table_check(bad.ctypes.data_as(ctypes.c_void_p), 2, ctypes.byref(tot)) == -1
+    assert lib.drnmi_pack_conv_weights_batched(None, 2, 10, None) == -1
 
 
 def test_fused_second_input_never_routes_to_halo():

@@ -155,6 +155,26 @@ def test_train_is_deterministic():
     assert all(torch.equal(a, b) for a, b in zip(outs[0][1], outs[1][1]))
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp32x"])
+def test_batched_weight_pack_matches_per_layer(precision, monkeypatch):
+    """From the second step on the fine-tune re-packs every forward / dgrad weight (and the fp32x
+    planes) in one launch (drnmi_pack_conv_weights_batched): losses and parameters after three
+    steps are bit-identical to the per-layer packing."""
+    import drnmi.train as T
+    g = TC.load()
+    outs = []
+    for batched in (False, True):
+        monkeypatch.setattr(T, "BATCHED_PACK", batched)
+        m, pr = TC.model_and_masks(g)
+        m.set_precision(precision)
+        xs, ts = TC.inputs(g)
+        m, losses = _run_hip_steps(m, pr, xs * 3, ts * 3)
+        outs.append((losses, [p.detach().cpu().clone() for p in m.parameters()]))
+        assert m._train_runner._packed_now == batched
+    assert outs[0][0] == outs[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(outs[0][1], outs[1][1]))
+
+
 def test_eval_after_train_uses_new_weights():
     """Training bumps parameter/buffer versions, so the eval plan repacks (drnseg._state_key)."""
     from drnmi.drnseg import DRNSeg

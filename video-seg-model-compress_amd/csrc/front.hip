@@ -90,7 +90,14 @@ constexpr uint32_t kF16Hi = 0x64646464u;
 // keep an epilogue value where it is computed (else it sinks to its first use, out of the MFMA shadow)
 #define FR_PINV(x) ({ uint32_t _v = (x); asm volatile("" : "+v"(_v)); _v; })
 // ... and read its inputs there (else the packing hoists to where they are ready, ahead of MFMAs)
+#ifndef DRNMI_FR_PINF
+#define DRNMI_FR_PINF 1
+#endif
+#if DRNMI_FR_PINF
 #define FR_PINF(x) ({ float _f = (x); asm volatile("" : "+v"(_f)); _f; })
+#else
+#define FR_PINF(x) (x)
+#endif
 #else
 #define FR_SB() do {} while (0)
 #define FR_PINV(x) (x)

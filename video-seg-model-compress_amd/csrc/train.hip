@@ -68,6 +68,56 @@ pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int ks, int k
   }
 }
 
+// one packed element of entry e (table layout: include/drnmi.h drnmi_pack_conv_weights_batched)
+__device__ __forceinline__ float pack_value(const float* __restrict__ w, int cout, int cin, int ks, int kin_stride,
+                                            int mode, int row, int k) {
+  const int tap = k / kin_stride;
+  const int c = k - tap * kin_stride;
+  float v = 0.f;
+  if (tap < ks * ks) {
+    const int kh = tap / ks, kw = tap - (tap / ks) * ks;
+    if (mode == 0) {
+      if (row < cout && c < cin) v = w[((static_cast<int64_t>(row) * cin + c) * ks + kh) * ks + kw];
+    } else if (row < cin && c < cout) {
+      v = w[((static_cast<int64_t>(c) * cin + row) * ks + (ks - 1 - kh)) * ks + (ks - 1 - kw)];
+    }
+  }
+  return v;
+}
+
+// all entries of the table in one grid-stride pass; the entry of element i is found by a binary
+// search over the entries' first-element indices (word 10)
+__global__ void __launch_bounds__(kThreads)
+pack_batched_kernel(const int64_t* __restrict__ tab, int n, int64_t total) {
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tab[mid * DRNMI_PACK_ENTRY_WORDS + 10] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t* e = tab + lo * DRNMI_PACK_ENTRY_WORDS;
+    const int64_t j = i - e[10];
+    const int k_pad = static_cast<int>(e[8]);
+    const int row = static_cast<int>(j / k_pad);
+    const int k = static_cast<int>(j - static_cast<int64_t>(row) * k_pad);
+    const float v = pack_value(reinterpret_cast<const float*>(e[0]), static_cast<int>(e[3]), static_cast<int>(e[4]),
+                               static_cast<int>(e[5]), static_cast<int>(e[6]), static_cast<int>(e[9]), row, k);
+    reinterpret_cast<float*>(e[1])[j] = v;
+    if (e[2] != 0) {                                   // split3_kernel's arithmetic
+      bf16_t* pl = reinterpret_cast<bf16_t*>(e[2]);
+      const int64_t m = e[7] * e[8];
+      const bf16_t a = f32_to_bf16(v);
+      const float r = v - bf16_to_f32(a);
+      const bf16_t b = f32_to_bf16(r);
+      pl[j] = a;
+      pl[m + j] = b;
+      pl[2 * m + j] = f32_to_bf16(r - bf16_to_f32(b));
+    }
+  }
+}
+
 // ------------------------------------------------------------------ column reductions
 // Rows x C (C = row stride, a power of two >= 4), fp32 in, fp64 partial sums.
 // Block: TPR threads per row (4 channels each, float4), RG = 256 / TPR row groups.
@@ -346,6 +396,9 @@ struct WgradP {
   int64_t pix_per_split;
 };
 
+#ifndef DRNMI_WGRAD_ROWS
+#define DRNMI_WGRAD_ROWS 1   // split-partial reduction one output channel per block (0: the flat kernel, A/B)
+#endif
 #ifndef DRNMI_WGRAD_BIG
 #define DRNMI_WGRAD_BIG 1    // fp32x: the 128 x 128 wgrad tile where cout and K >= 128 (0: 64 x 64 only, A/B)
 #endif
@@ -936,6 +989,36 @@ wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin,
   }
 }
 
+// The same sums (identical order: z ascending from 0.f), one block per output channel: the row's
+// K partial sums are staged in LDS (stride cs + 1 per tap: the 9 taps of a channel in distinct
+// banks) and dw's OIHW row is then written in order.  wgrad_reduce_kernel's OIHW writes landed
+// 9 floats apart (a 3x3 layer's whole dw written at ~1/9 of line efficiency, and read again to
+// accumulate).
+__global__ void __launch_bounds__(kThreads)
+wgrad_reduce_rows_kernel(const float* __restrict__ ws, int splits, int cout, int cin, int cs, int ks, int K,
+                         float* __restrict__ dw, int acc) {
+  extern __shared__ float srow[];
+  const int co = blockIdx.x;
+  const int taps = ks * ks;
+  const int64_t base = static_cast<int64_t>(co) * K;
+  const int64_t zs = static_cast<int64_t>(cout) * K;
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += ws[z * zs + base + k];
+    const int tap = k / cs;
+    srow[tap * (cs + 1) + (k - tap * cs)] = s;
+  }
+  __syncthreads();
+  const int n = cin * taps;
+  float* __restrict__ d = dw + static_cast<int64_t>(co) * n;
+  for (int o = threadIdx.x; o < n; o += blockDim.x) {
+    const int ci = o / taps, tap = o - ci * taps;
+    const float s = srow[tap * (cs + 1) + ci];
+    d[o] = acc ? d[o] + s : s;
+  }
+}
+constexpr int kReduceRowsMaxLds = 48 * 1024;
+
 // The pixel range is split so that the launch fills the chip: at least two rounds of the resident
 // workgroup slots, and among lo .. 4 lo splits the count whose last round is fullest (the first
 // rule alone put D-54 layer7.0's 576 big tiles on 512 slots at one split: 1.125 rounds, the
@@ -1266,6 +1349,30 @@ extern "C" int drnmi_pack_conv_weight(const float* w, int32_t cout, int32_t cin,
   return static_cast<int>(hipGetLastError());
 }
 
+extern "C" int drnmi_pack_table_check(const int64_t* t, int32_t n, int64_t* total_out) {
+  if (t == nullptr || n <= 0) return DRNMI_EINVAL;
+  int64_t total = 0;
+  for (int e = 0; e < n; ++e) {
+    const int64_t* q = t + static_cast<int64_t>(e) * DRNMI_PACK_ENTRY_WORDS;
+    const int64_t cout = q[3], cin = q[4], ks = q[5], kst = q[6], rows = q[7], kp = q[8], mode = q[9];
+    if (q[0] == 0 || q[1] == 0 || cout <= 0 || cin <= 0 || ks <= 0 || kst <= 0 || rows <= 0 || kp <= 0) return DRNMI_EINVAL;
+    if ((mode != 0 && mode != 1) || kp < ks * ks * kst || kp >= (int64_t(1) << 31) || rows >= (int64_t(1) << 31)) return DRNMI_EINVAL;
+    if (mode == 0 && (rows < cout || kst < cin)) return DRNMI_EINVAL;
+    if (mode == 1 && (rows < cin || kst < cout)) return DRNMI_EINVAL;
+    if (q[10] != total || q[11] != 0) return DRNMI_EINVAL;
+    total += rows * kp;
+  }
+  if (total_out != nullptr) *total_out = total;
+  return 0;
+}
+
+extern "C" int drnmi_pack_conv_weights_batched(const int64_t* table, int32_t n, int64_t total, void* stream) {
+  if (table == nullptr || n <= 0 || total <= 0) return DRNMI_EINVAL;
+  hipLaunchKernelGGL(pack_batched_kernel, dim3(grid_of(total)), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                     table, n, total);
+  return static_cast<int>(hipGetLastError());
+}
+
 static bool pow2_ge4(int c) { return c >= 4 && (c & (c - 1)) == 0; }
 
 extern "C" int64_t drnmi_reduce_workspace_bytes(int64_t rows, int32_t channels) {
@@ -1465,8 +1572,13 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
   const int64_t total = static_cast<int64_t>(a->cout) * p.K;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_of(total)), dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin,
-                     a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
+  const int64_t lds = static_cast<int64_t>(a->ks) * a->ks * (a->cin_stride + 1) * 4;
+  if (DRNMI_WGRAD_ROWS && lds <= kReduceRowsMaxLds)
+    hipLaunchKernelGGL(wgrad_reduce_rows_kernel, dim3(a->cout), dim3(kThreads), static_cast<unsigned>(lds), s, p.ws,
+                       splits, a->cout, a->cin, a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_of(total)), dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin,
+                       a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
   return static_cast<int>(hipGetLastError());
 }
 

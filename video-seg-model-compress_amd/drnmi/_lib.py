@@ -114,6 +114,8 @@ SIGNATURES = {
     "drnmi_abi_version": (ctypes.c_int32, []),
     "drnmi_conv_args_size": (ctypes.c_int64, []),
     "drnmi_conv_wgrad_f32_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
+    "drnmi_pack_table_check": (ctypes.c_int, [_VP, _I32, ctypes.POINTER(ctypes.c_int64)]),
+    "drnmi_pack_conv_weights_batched": (ctypes.c_int, [_VP, _I32, _I64, _VP]),
 }
 ABI_VERSION = 4          # include/drnmi.h DRNMI_ABI_VERSION
 

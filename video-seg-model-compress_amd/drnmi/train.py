@@ -30,6 +30,7 @@ CPU or ATen fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -37,6 +38,8 @@ from . import _lib
 from .engine import COUT_ALIGN, K_ALIGN, X6_PATCH_SHAPES, _conv_out, _pow2_at_least, _round_up
 
 F32 = _lib.DRNMI_F32
+# TrainRunner default (tests compare against the per-layer packs; DRNMI_BATCHED_PACK=0: A/B runs)
+BATCHED_PACK = os.environ.get("DRNMI_BATCHED_PACK", "1") != "0"
 
 
 def _vp(t):
@@ -47,11 +50,12 @@ class _NodeState:
     """Per-node packed weights (forward / dgrad layouts) cached across steps."""
 
     __slots__ = ("wf", "wd", "wfx", "wdx", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift", "patch",
-                 "dpatch")
+                 "dpatch", "dys")
 
     def __init__(self):
         self.wf = self.wd = self.wfx = self.wdx = self.shift = None
         self.patch = self.dpatch = False
+        self.dys = None
 
 
 class TrainRunner:
@@ -75,6 +79,15 @@ class TrainRunner:
         self._flat = None               # flat gradient buffer (views = param.grad)
         self._flat_params = None
         self.debug_value_grads = None   # dict -> filled with {value: NHWC grad clone} (diagnostics)
+        # batched re-pack (drnmi_pack_conv_weights_batched): after the first step has allocated every
+        # packed buffer, each forward re-packs all forward and dgrad weights (+ fp32x planes) in one
+        # launch instead of ~4 launches per layer; the table is rebuilt when a buffer moves
+        self.batched_pack = BATCHED_PACK
+        self._pack_key = None
+        self._pack_prec = None
+        self._pack_tab = None
+        self._pack_total = 0
+        self._packed_now = False
 
     # ------------------------------------------------------------------ helpers
     def _ws(self, attr, nbytes, device):
@@ -137,13 +150,14 @@ class TrainRunner:
         w = conv.weight.detach()
         if not (w.is_contiguous() and w.dtype == torch.float32):
             raise RuntimeError(f"{nd.name}: expected a contiguous fp32 weight")
-        _lib.check(lib.drnmi_pack_conv_weight(_vp(w), cout, cin, ks, cs, st.cout_pad, st.k_pad, 0, None, F32,
-                                              _vp(st.wf), stream), f"pack {nd.name}")
-        # fp32x: the full-resolution small-channel convs (stem, layer1, layer2 shapes) run on the
-        # split-bf16 patch kernels, as in the inference engine (engine.X6_PATCH_SHAPES)
-        st.patch = self.model.precision == "fp32x" and not nd.out_fp32_nchw and \
-            (cs, cout, ks, conv.stride[0], conv.dilation[0]) in X6_PATCH_SHAPES
-        st.wfx = self._split(st.wf, cs, st.k, st.k_pad, patch=st.patch)
+        if not self._packed_now:
+            _lib.check(lib.drnmi_pack_conv_weight(_vp(w), cout, cin, ks, cs, st.cout_pad, st.k_pad, 0, None, F32,
+                                                  _vp(st.wf), stream), f"pack {nd.name}")
+            # fp32x: the full-resolution small-channel convs (stem, layer1, layer2 shapes) run on
+            # the split-bf16 patch kernels, as in the inference engine (engine.X6_PATCH_SHAPES)
+            st.patch = self.model.precision == "fp32x" and not nd.out_fp32_nchw and \
+                (cs, cout, ks, conv.stride[0], conv.dilation[0]) in X6_PATCH_SHAPES
+            st.wfx = self._split(st.wf, cs, st.k, st.k_pad, patch=st.patch, out=st.wfx)
         if conv.bias is not None:
             st.shift[:cout].copy_(conv.bias.detach())
 
@@ -156,23 +170,72 @@ class TrainRunner:
             st.kd_pad = _round_up(st.kd, K_ALIGN)
             st.rows_d = _round_up(cin, COUT_ALIGN)
             st.wd = torch.empty(st.rows_d, st.kd_pad, dtype=torch.float32, device=device)
+        st.dys = dys
+        if self._packed_now:                      # packed with the forward weights (batched launch)
+            return dys
         _lib.check(lib.drnmi_pack_conv_weight(_vp(nd.conv.weight.detach()), cout, cin, ks, dys, st.rows_d,
                                               st.kd_pad, 1, None, F32, _vp(st.wd), stream), f"pack dgrad {nd.name}")
         # fp32x: a data gradient whose (stride-1) conv is a patch-kernel shape (layer1's 16 -> 16
         # at full resolution) runs split-bf16 on the patch kernel, not on the f32 igemm
         st.dpatch = self.model.precision == "fp32x" and \
             (dys, cin, ks, 1, nd.conv.dilation[0]) in X6_PATCH_SHAPES
-        st.wdx = self._split(st.wd, dys, st.kd, st.kd_pad, patch=st.dpatch)
+        st.wdx = self._split(st.wd, dys, st.kd, st.kd_pad, patch=st.dpatch, out=st.wdx)
         return dys
 
-    def _split(self, wpk, cin_stride, k, k_pad, patch=False):
+    def _batched_pack(self, device, stream) -> bool:
+        """Re-pack every forward and dgrad weight (and fp32x planes) of the network in one launch
+        (drnmi_pack_conv_weights_batched), bit-identical to the per-layer calls.  Needs the buffers
+        of a previous step (False on the first step, or when disabled)."""
+        if not self.batched_pack:
+            return False
+        if self._pack_prec != self.model.precision:   # a per-layer step sets the new mode's buffers
+            self._pack_prec = self.model.precision
+            self._pack_key = None
+            return False
+        key = [self.model.precision]
+        for nd, st in zip(self.nodes, self.state):
+            if st.wf is None or (nd.src != "input" and st.wd is None):
+                return False
+            key.append((nd.conv.weight.data_ptr(), st.wf.data_ptr(), st.wfx.data_ptr() if st.wfx is not None else 0,
+                        st.wd.data_ptr() if st.wd is not None else 0,
+                        st.wdx.data_ptr() if st.wdx is not None else 0))
+        key = tuple(key)
+        if key != self._pack_key:
+            rows = []
+            total = 0
+            for nd, st in zip(self.nodes, self.state):
+                cout, cin, ks, _ = nd.conv.weight.shape
+                w = nd.conv.weight.detach()
+                if not (w.is_contiguous() and w.dtype == torch.float32):
+                    return False
+                ents = [(st.wf, st.wfx, self.cstride[nd.src], st.cout_pad, st.k_pad, 0)]
+                if st.wd is not None:
+                    ents.append((st.wd, st.wdx, st.dys, st.rows_d, st.kd_pad, 1))
+                for out, planes, kst, rows_pad, k_pad, mode in ents:
+                    rows.append([w.data_ptr(), out.data_ptr(), planes.data_ptr() if planes is not None else 0,
+                                 cout, cin, ks, kst, rows_pad, k_pad, mode, total, 0])
+                    total += rows_pad * k_pad
+            tab = torch.tensor(rows, dtype=torch.int64)
+            tot = ctypes.c_int64(0)
+            _lib.check(_lib.load().drnmi_pack_table_check(ctypes.c_void_p(tab.data_ptr()), len(rows),
+                                                          ctypes.byref(tot)), "pack table")
+            self._pack_tab = tab.to(device)
+            self._pack_total = int(tot.value)
+            self._pack_key = key
+        _lib.check(_lib.load().drnmi_pack_conv_weights_batched(_vp(self._pack_tab), self._pack_tab.shape[0],
+                                                               self._pack_total, ctypes.c_void_p(stream)),
+                   "batched weight pack")
+        return True
+
+    def _split(self, wpk, cin_stride, k, k_pad, patch=False, out=None):
         """fp32x: the three bf16 planes of a packed fp32 weight, for the convs conv_x6 takes
         (>= 32 input channels, k == k_pad) or the split-bf16 patch kernels take (`patch`); None
-        keeps the launch on the exact-f32 kernel."""
+        keeps the launch on the exact-f32 kernel.  `out`: the previous step's planes (reused)."""
         if self.model.precision != "fp32x" or (not patch and (cin_stride < 32 or k != k_pad)):
             return None
         # one HIP pass (drnmi_split3_bf16), bit-identical to engine.split3_bf16
-        out = torch.empty((3,) + tuple(wpk.shape), dtype=torch.bfloat16, device=wpk.device)
+        if out is None or out.shape != (3,) + tuple(wpk.shape):
+            out = torch.empty((3,) + tuple(wpk.shape), dtype=torch.bfloat16, device=wpk.device)
         _lib.check(_lib.load().drnmi_split3_bf16(_vp(wpk), wpk.numel(), _vp(out), _lib.stream_ptr(wpk.device)),
                    "split3_bf16")
         return out
@@ -215,6 +278,8 @@ class TrainRunner:
         _lib.check(lib.drnmi_nchw_to_nhwc(x.data_ptr(), xin.data_ptr(), n, 3, h, w, 8, F32, ctypes.c_void_p(stream)),
                    "nchw_to_nhwc")
         vals["input"] = xin
+        self._packed_now = False
+        self._packed_now = self._batched_pack(dev, stream)
         per_node = []
         logits = None
         for nd, st in zip(self.nodes, self.state):
