@@ -103,6 +103,9 @@ constexpr uint32_t kF16Hi = 0x64646464u;
 #define FR_PINV(x) (x)
 #define FR_PINF(x) (x)
 #endif
+#ifndef DRNMI_FR_CSREG
+#define DRNMI_FR_CSREG 0          // 1: interior walks keep the stem's row-case-3 offsets in registers
+#endif
 #ifndef DRNMI_FR_FETCH
 #define DRNMI_FR_FETCH 8          // layer2 MFMA after which the next step's operands are fetched
 #endif
@@ -663,6 +666,7 @@ front3_kernel(const FrontParams a) {
     // in the shadows of this step's stem MFMAs, the stem epilogue under the layer1 MFMAs, the
     // layer1 epilogue and the next step's operand fetch under the layer2 MFMAs; the instruction
     // order is pinned (DRNMI_FR_ILV).
+    f32x16 cs_int;                                   // interior stem rows: row case 3 (DRNMI_FR_CSREG)
     auto step = [&](int j, auto ph_, auto border_) {
       constexpr int PH = decltype(ph_)::value;
       constexpr bool BORDER = decltype(border_)::value != 0;
@@ -688,8 +692,13 @@ front3_kernel(const FrontParams a) {
         // later stages' LDS operands, issued a stage ahead: layer1 starting values, the stem rows'
         // border-case offsets (interior segments: row case 3)
         if (i == 12) l0 = ld16(c1m);
-        if (i == 14) cs0 = BORDER ? cinit(p + 3) : cinit_case(3);
-        if (i == 16) cs1 = BORDER ? cinit(p + 4) : cinit_case(3);
+        if constexpr (BORDER || !DRNMI_FR_CSREG) {
+          if (i == 14) cs0 = BORDER ? cinit(p + 3) : cinit_case(3);
+          if (i == 16) cs1 = BORDER ? cinit(p + 4) : cinit_case(3);
+        } else if (i == 14) {
+          cs0 = cs_int;
+          cs1 = cs_int;
+        }
         FR_SB();
       }
       // ---- C: layer1 rows p, p+1 from stem rows p-1 .. p+2 (2 x 12 MFMAs); the stem epilogue
@@ -782,6 +791,7 @@ front3_kernel(const FrontParams a) {
     // interior segments skip all row checks: every frame row a stem row reads (<= 2jl+7) is inside
     // and every stem row is of row case 3 (rows fetch() converts past 2jl+7 are never read)
     auto walk = [&](auto border_) {
+      if constexpr (decltype(border_)::value == 0 && DRNMI_FR_CSREG) cs_int = cinit_case(3);
       fetch(jb, ic<0>{}, border_);
       for (int j = jb; j <= jl; j += 4) {
         step(j + 0, ic<0>{}, border_);

@@ -396,9 +396,6 @@ struct WgradP {
   int64_t pix_per_split;
 };
 
-#ifndef DRNMI_WGRAD_ROWS
-#define DRNMI_WGRAD_ROWS 1   // split-partial reduction one output channel per block (0: the flat kernel, A/B)
-#endif
 #ifndef DRNMI_WGRAD_BIG
 #define DRNMI_WGRAD_BIG 1    // fp32x: the 128 x 128 wgrad tile where cout and K >= 128 (0: 64 x 64 only, A/B)
 #endif
@@ -989,36 +986,6 @@ wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin,
   }
 }
 
-// The same sums (identical order: z ascending from 0.f), one block per output channel: the row's
-// K partial sums are staged in LDS (stride cs + 1 per tap: the 9 taps of a channel in distinct
-// banks) and dw's OIHW row is then written in order.  wgrad_reduce_kernel's OIHW writes landed
-// 9 floats apart (a 3x3 layer's whole dw written at ~1/9 of line efficiency, and read again to
-// accumulate).
-__global__ void __launch_bounds__(kThreads)
-wgrad_reduce_rows_kernel(const float* __restrict__ ws, int splits, int cout, int cin, int cs, int ks, int K,
-                         float* __restrict__ dw, int acc) {
-  extern __shared__ float srow[];
-  const int co = blockIdx.x;
-  const int taps = ks * ks;
-  const int64_t base = static_cast<int64_t>(co) * K;
-  const int64_t zs = static_cast<int64_t>(cout) * K;
-  for (int k = threadIdx.x; k < K; k += blockDim.x) {
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += ws[z * zs + base + k];
-    const int tap = k / cs;
-    srow[tap * (cs + 1) + (k - tap * cs)] = s;
-  }
-  __syncthreads();
-  const int n = cin * taps;
-  float* __restrict__ d = dw + static_cast<int64_t>(co) * n;
-  for (int o = threadIdx.x; o < n; o += blockDim.x) {
-    const int ci = o / taps, tap = o - ci * taps;
-    const float s = srow[tap * (cs + 1) + ci];
-    d[o] = acc ? d[o] + s : s;
-  }
-}
-constexpr int kReduceRowsMaxLds = 48 * 1024;
-
 // The pixel range is split so that the launch fills the chip: at least two rounds of the resident
 // workgroup slots, and among lo .. 4 lo splits the count whose last round is fullest (the first
 // rule alone put D-54 layer7.0's 576 big tiles on 512 slots at one split: 1.125 rounds, the
@@ -1572,13 +1539,8 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
   const int64_t total = static_cast<int64_t>(a->cout) * p.K;
-  const int64_t lds = static_cast<int64_t>(a->ks) * a->ks * (a->cin_stride + 1) * 4;
-  if (DRNMI_WGRAD_ROWS && lds <= kReduceRowsMaxLds)
-    hipLaunchKernelGGL(wgrad_reduce_rows_kernel, dim3(a->cout), dim3(kThreads), static_cast<unsigned>(lds), s, p.ws,
-                       splits, a->cout, a->cin, a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
-  else
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_of(total)), dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin,
-                       a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_of(total)), dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin,
+                     a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
   return static_cast<int>(hipGetLastError());
 }
 
