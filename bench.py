@@ -332,9 +332,15 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
     front = getattr(plan, "front_fused", False)
     fused_stem = getattr(plan, "stem_fused", False) and not front
 
+    blocks = getattr(plan, "block64", {})
+
     def launched_name(i):
         if front and i <= 2:                 # layer0..layer2 in one launch (drnmi_video_front_u8)
             return "" if i else "front_kernel"
+        if i in blocks:                      # a 64-channel BasicBlock in one launch (drnmi_basic_block64)
+            return "block64_kernel"
+        if i - 1 in blocks:
+            return ""
         if fused_stem and i <= 1:            # stem + layer1 in one launch (drnmi_stem_layer1)
             return "" if i == 1 else lib.drnmi_stem_layer1_kernel_name(
                 ctypes.byref(plan.stem_u8), ctypes.byref(plan.args[1])).decode()
@@ -355,6 +361,9 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
             density[:k] = [float(sum((nd.conv.weight != 0).sum() for nd in nodes[:k])) /
                            sum(nd.conv.weight.numel() for nd in nodes[:k])] * k
             break
+    for i in blocks:                         # the fused block's row carries both convs
+        d2 = [float((nd.conv.weight != 0).sum()) for nd in nodes[i:i + 2]]
+        density[i] = density[i + 1] = sum(d2) / sum(nd.conv.weight.numel() for nd in nodes[i:i + 2])
     dense_flops = {i: w[1] for i, w in enumerate(works)}
     works = [(w[0], w[1] * density[i], w[2]) if i < len(nodes) else w for i, w in enumerate(works)]
     events = []

@@ -175,6 +175,20 @@ int drnmi_front_pack(const float* w0, const float* scale0, const float* shift0, 
                      const float* shift1, const float* w2, const float* scale2, const float* shift2,
                                       const float* mean3, const float* std3, int32_t bgr, void* out_host);
 int drnmi_front_supported(int32_t n, int32_t h, int32_t w);
+
+/* Fused 64-channel BasicBlock (lmodels/drn.py:49-65 with inplanes = planes = 64, stride 1,
+ * dilation 1, no downsample: DRN-D-22 layer3.1, D-38 layer3.1/3.2):
+ *   y = relu(bn2(conv3x3(relu(bn1(conv3x3(x))))) + x), bf16 NHWC [n][h][w][64] in and out, eval BN
+ *   (scale folded into the weights, shift added; fp32 accumulation).
+ * The intermediate never reaches HBM (csrc/block64.hip).  `pack`: device copy of the blob that the
+ * HOST function drnmi_block64_pack(w1, scale1, shift1, w2, scale2, shift2, out) builds from the two
+ * convs' OIHW fp32 weights [64][64][3][3] and per-channel BN scale / shift (fp32 [64] each);
+ * drnmi_block64_pack_bytes() bytes.  x and y must not alias. */
+int64_t drnmi_block64_pack_bytes(void);
+int drnmi_block64_pack(const float* w1, const float* scale1, const float* shift1, const float* w2,
+                       const float* scale2, const float* shift2, void* out_host);
+int drnmi_block64_supported(int32_t n, int32_t h, int32_t w);
+int drnmi_basic_block64(const void* x, const void* pack, void* y, int32_t n, int32_t h, int32_t w, void* stream);
 int drnmi_video_front_u8(const uint8_t* frames, const void* pack, void* y, int32_t n, int32_t h, int32_t w,
                          void* stream);
 

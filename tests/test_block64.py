@@ -1,0 +1,89 @@
+"""Fused 64-channel BasicBlock (drnmi_basic_block64, csrc/block64.hip): conv3x3 + BN + ReLU, conv3x3
++ BN + residual + ReLU in one launch (lmodels/drn.py:49-65; DRN-D-22 layer3.1).
+
+Reference: the plain fp32 torch restatement on the same bf16 input, with the block's intermediate
+rounded to bf16 as the kernel stores it.  Tolerance (bf16 perf mode, written here): the kernel
+folds the BN scale into bf16 weights (one rounding of w * scale) and accumulates in fp32 in its own
+order, so a stored intermediate may flip by one bf16 ulp; bound |gpu - ref| <= 2^-6 |ref| +
+4e-3 max|ref|, and at most 0.5 % of the outputs beyond 2^-8 |ref| + 1e-3 max|ref|.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from drnmi import _lib
+
+
+def _params(seed):
+    g = torch.Generator().manual_seed(seed)
+    w1 = torch.randn(64, 64, 3, 3, generator=g) * (2 / 576) ** 0.5
+    w2 = torch.randn(64, 64, 3, 3, generator=g) * (2 / 576) ** 0.5
+    s1, s2 = torch.rand(64, generator=g) + 0.5, torch.rand(64, generator=g) + 0.5
+    b1, b2 = torch.randn(64, generator=g) * 0.2, torch.randn(64, generator=g) * 0.2
+    return w1, s1, b1, w2, s2, b2
+
+
+def _pack(lib, p):
+    arrs = [t.contiguous().float().numpy() for t in p]
+    out = np.zeros(int(lib.drnmi_block64_pack_bytes()), dtype=np.uint8)
+    rc = lib.drnmi_block64_pack(*[a.ctypes.data_as(ctypes.c_void_p) for a in arrs], out.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0
+    return out
+
+
+def reference(x_nhwc_bf16: torch.Tensor, p) -> torch.Tensor:
+    """fp32 torch restatement on the bf16 input; the intermediate rounded to bf16 (stored)."""
+    w1, s1, b1, w2, s2, b2 = p
+    x = x_nhwc_bf16.float().permute(0, 3, 1, 2)
+    w1f = (w1 * s1.view(-1, 1, 1, 1)).bfloat16().float()
+    w2f = (w2 * s2.view(-1, 1, 1, 1)).bfloat16().float()
+    t = torch.relu(F.conv2d(x, w1f, padding=1) + b1.view(1, -1, 1, 1)).bfloat16().float()
+    y = torch.relu(F.conv2d(t, w2f, padding=1) + b2.view(1, -1, 1, 1) + x)
+    return y.permute(0, 2, 3, 1)
+
+
+def test_block64_pack_and_supported_without_gpu():
+    lib = _lib.load()
+    assert lib.drnmi_block64_pack_bytes() == 2 * 2 * 36 * 64 * 16 + 512
+    assert lib.drnmi_block64_supported(8, 256, 512) == 1
+    assert lib.drnmi_block64_supported(0, 256, 512) == 0
+    assert lib.drnmi_basic_block64(None, None, None, 1, 8, 8, None) == -1
+    p = _params(3)
+    blob = _pack(lib, p)
+    # fragment (conv 0, half 0, slice 5 = tap 1 (kh 0, kw 1), cb 1), lane 33 (r 1, h 1), element 2:
+    # w1[1][16 + 8 + 2][0][1] * s1[1] in bf16
+    frag = blob[:2 * 2 * 36 * 64 * 16].view(np.uint16).reshape(2, 2, 36, 64, 8)
+    want = (p[0][1, 26, 0, 1] * p[1][1]).bfloat16().view(torch.int16).item() & 0xffff
+    assert int(frag[0, 0, 5, 33, 2]) == want
+    sh = blob[2 * 2 * 36 * 64 * 16:].view(np.float32)
+    np.testing.assert_array_equal(sh[:64], p[2].numpy())
+    np.testing.assert_array_equal(sh[64:], p[5].numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(1, 5, 9), (2, 17, 70), (1, 40, 130), (3, 64, 248), (2, 256, 512)])
+def test_block64_matches_reference(n, h, w):
+    lib = _lib.load()
+    p = _params(n + h + w)
+    blob = torch.from_numpy(_pack(lib, p)).cuda()
+    g = torch.Generator().manual_seed(w)
+    x = torch.relu(torch.randn(n, h, w, 64, generator=g)).bfloat16()
+    xd = x.cuda()
+    y = torch.full_like(xd, float("nan"))
+    _lib.check(lib.drnmi_basic_block64(xd.data_ptr(), blob.data_ptr(), y.data_ptr(), n, h, w,
+                                       ctypes.c_void_p(_lib.stream_ptr())), "basic_block64")
+    torch.cuda.synchronize()
+    got = y.float().cpu()
+    assert not torch.isnan(got).any()
+    ref = reference(x, p)
+    d = (got - ref).abs()
+    scale = ref.abs().max()
+    print(f"block64 {n}x{h}x{w}: max |d| {d.max():.3e} (|ref| max {scale:.2f})")
+    assert (d <= 2.0 ** -6 * ref.abs() + 4e-3 * scale).all()
+    loose = (d > 2.0 ** -8 * ref.abs() + 1e-3 * scale).float().mean()
+    assert loose <= 5e-3, float(loose)

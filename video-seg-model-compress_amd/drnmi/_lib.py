@@ -114,6 +114,10 @@ SIGNATURES = {
     "drnmi_abi_version": (ctypes.c_int32, []),
     "drnmi_conv_args_size": (ctypes.c_int64, []),
     "drnmi_conv_wgrad_f32_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
+    "drnmi_block64_pack_bytes": (ctypes.c_int64, []),
+    "drnmi_block64_pack": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "drnmi_block64_supported": (ctypes.c_int, [_I32, _I32, _I32]),
+    "drnmi_basic_block64": (ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _VP]),
     "drnmi_pack_table_check": (ctypes.c_int, [_VP, _I32, ctypes.POINTER(ctypes.c_int64)]),
     "drnmi_pack_conv_weights_batched": (ctypes.c_int, [_VP, _I32, _I64, _VP]),
 }

@@ -303,6 +303,8 @@ class PackedNet:
                 self.stem_u8_w = split3_bf16(full) if self.base == "fp32x" else full.to(self.tdtype).contiguous()
             self._front_packs = {}
             self.front_eligible = self._front_shapes_ok()
+            self.block64_pairs = self._block64_pairs()
+            self._block64_packs = {}
 
     def _front_shapes_ok(self) -> bool:
         """The fused video front (drnmi_video_front_u8: layer0 + layer1 + layer2 of every DRN-D,
@@ -319,6 +321,46 @@ class PackedNet:
                     not nd.relu or nd.i8 or nd.out_fp32_nchw:
                 return False
         return nodes[1].src == nodes[0].dst and nodes[2].src == nodes[1].dst and self.cstride[nodes[2].dst] == 32
+
+    def _block64_pairs(self) -> list[int]:
+        """Node indices i where nodes i, i+1 are a plain 64-channel BasicBlock (lmodels/drn.py:49-65:
+        conv3x3 64 -> 64 + BN + ReLU, conv3x3 + BN + residual = the block input + ReLU, stride 1,
+        dilation 1, no downsample) in bf16: drnmi_basic_block64 runs them as one launch."""
+        if self.base != "bf16" or not FUSE_BLOCK64 or self.block_sparse:
+            return []
+        nodes = self.graph.nodes
+        out = []
+        for i in range(len(nodes) - 1):
+            a, b = nodes[i], nodes[i + 1]
+            ok = True
+            for nd in (a, b):
+                c = nd.conv
+                ok &= (c.in_channels, c.out_channels, c.kernel_size[0], c.stride[0], c.padding[0], c.dilation[0],
+                       c.groups) == (64, 64, 3, 1, 1, 1, 1) and nd.bn is not None and nd.relu and not nd.i8 \
+                    and not nd.x6 and not nd.out_fp32_nchw and not nd.fused and nd.fused_into < 0
+            ok = ok and a.res is None and b.src == a.dst and b.res == a.src and \
+                all(self.cstride[v] == 64 for v in (a.src, a.dst, b.dst)) and \
+                self.value_code(a.src) == self.value_code(a.dst) == self.value_code(b.dst) == _lib.DRNMI_BF16
+            if ok and (not out or out[-1] + 1 < i):
+                out.append(i)
+        return out
+
+    def block64_pack(self, i: int) -> torch.Tensor:
+        """Device copy of drnmi_block64_pack for the block at nodes i, i+1 (cleared by every repack)."""
+        t = self._block64_packs.get(i)
+        if t is None:
+            import numpy as np
+            lib = _lib.load()
+            arrs = []
+            for nd in self.graph.nodes[i:i + 2]:
+                arrs += [nd.conv.weight.detach().float().cpu().contiguous().numpy(),
+                         nd.scale[:64].float().cpu().contiguous().numpy(), nd.shift[:64].float().cpu().contiguous().numpy()]
+            out = np.zeros(int(lib.drnmi_block64_pack_bytes()), dtype=np.uint8)
+            _lib.check(lib.drnmi_block64_pack(*[x.ctypes.data_as(ctypes.c_void_p) for x in arrs],
+                                              out.ctypes.data_as(ctypes.c_void_p)), "block64_pack")
+            t = torch.from_numpy(out).to(self.device)
+            self._block64_packs[i] = t
+        return t
 
     def front_pack(self, mean, std, bgr: bool) -> torch.Tensor:
         """Device copy of drnmi_front_pack for these weights and this normalisation (cached per
@@ -462,6 +504,8 @@ FUSE_STEM = True
 # bf16 video path: layer0 + layer1 + layer2 as one launch from the uint8 frames (drnmi_video_front_u8);
 # neither 16-channel full-resolution activation is written.  Plans with keep_all keep separate launches.
 FUSE_FRONT = True
+# 64-channel BasicBlocks (D-22 layer3.1) as one drnmi_basic_block64 launch (False: two conv launches)
+FUSE_BLOCK64 = True
 
 
 def _route_name(nd: ConvNode, cin_stride: int, cin2: int = 0, k_pad: int | None = None) -> str:
@@ -580,6 +624,14 @@ class Plan:
         self.stem_fused = self._stem_fusable(reads_of)
         self.front_fused = self._front_fusable(reads_of)
         self.front_pack_t = None
+        # fused 64-channel BasicBlocks: the first conv's output has no other reader
+        self.block64 = {}
+        lib = _lib.load()
+        for i in getattr(packed, "block64_pairs", []):
+            if self.fuse and not any(g.nodes[i].dst in reads_of[j] for j in range(len(g.nodes)) if j != i + 1) and \
+                    not packed.quant_after.get(i) and not packed.quant_after.get(i + 1) and \
+                    lib.drnmi_block64_supported(n, *self.shapes[g.nodes[i].dst]):
+                self.block64[i] = packed.block64_pack(i)
         self.src = "nchw"
 
     def _front_fusable(self, reads_of) -> bool:
@@ -677,6 +729,8 @@ class Plan:
                 continue
             self.args[i] = self._conv_args(nd)
         self.front_pack_t = None                  # re-fetched (repacked) at the next ingest_u8
+        for i in list(self.block64):
+            self.block64[i] = self.packed.block64_pack(i)
         if self.stem_u8 is not None:
             nd = self.packed.graph.nodes[0]
             self.stem_u8.wgt = self.packed.stem_u8_w.data_ptr()
@@ -688,9 +742,21 @@ class Plan:
         lib = _lib.load()
         front = self.src == "u8" and self.front_fused
         fused_stem = self.src == "u8" and self.stem_fused and not front
-        for i, (a, nd) in enumerate(zip(self.args, self.packed.graph.nodes)):
-            if a is None or (i == 1 and fused_stem) or (front and i in (1, 2)):
+        nodes = self.packed.graph.nodes
+        blocks = self.block64
+        for i, (a, nd) in enumerate(zip(self.args, nodes)):
+            if a is None or (i == 1 and fused_stem) or (front and i in (1, 2)) or (i - 1) in blocks:
                 continue                          # folded into another launch
+            if i in blocks:                       # conv1 + conv2 of a 64-channel BasicBlock
+                if timing_hook is not None:
+                    timing_hook(i, nd, True)
+                h, w = self.shapes[nd.dst]
+                _lib.check(lib.drnmi_basic_block64(self.bufs[nd.x_val].data_ptr(), blocks[i].data_ptr(),
+                                                   self.bufs[nodes[i + 1].dst].data_ptr(), self.n, h, w,
+                                                   ctypes.c_void_p(stream)), f"basic_block64 {nd.name}")
+                if timing_hook is not None:
+                    timing_hook(i, nd, False)
+                continue
             if front and i == 0:
                 if timing_hook is not None:
                     timing_hook(0, nd, True)

@@ -99,6 +99,13 @@ def launch_work(plan, video: bool = True):
         mid = plan.n * h0 * w0 * nodes[0].conv.out_channels * esz
         rows[0] = (rows[0][0], rows[0][1] + rows[1][1], rows[0][2] + rows[1][2] - 2 * mid)
         rows[1] = (rows[1][0], 0.0, 0.0)
+    for i in getattr(plan, "block64", {}):
+        # a 64-channel BasicBlock in one launch (drnmi_basic_block64): the intermediate is neither
+        # written nor read back, and the block input is read once (conv1 and the residual)
+        hb, wb = plan.shapes[nodes[i].dst]
+        mid = plan.n * hb * wb * 64 * esz
+        rows[i] = (rows[i][0], rows[i][1] + rows[i + 1][1], rows[i][2] + rows[i + 1][2] - 3 * mid)
+        rows[i + 1] = (rows[i + 1][0], 0.0, 0.0)
     return rows
 
 
