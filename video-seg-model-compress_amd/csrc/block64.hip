@@ -4,7 +4,7 @@
 //
 // The two halo launches wrote the block's intermediate t to HBM and read it back, and each re-ran
 // a 9-step K loop per 4 x 64 tile whose prologue / epilogue dominated (MFMA busy 0.31).  Here one
-// persistent workgroup per CU walks a 62-column strip of a frame down its rows:
+// persistent workgroup walks a 62-column strip of a frame down its rows:
 //   * waves 0, 1 compute t row j (conv1, output channels 32 w .. +31) from x rows j-1 .. j+1;
 //     waves 2, 3 compute y row j-2 (conv2, channels 32 (w - 2) .. +31) from t rows j-3 .. j-1 and
 //     add x row j-2 -- the two convs of a step are independent, and one barrier per row step
@@ -12,8 +12,9 @@
 //   * each wave's 36 weight fragments (32 channels x 576 K, v_mfma_f32_32x32x16_bf16 A operands)
 //     stay in AGPRs for the whole launch; B fragments are 16-B LDS reads of (tap, 16-channel)
 //     slices of the x / t rows, two 32-pixel blocks per row;
-//   * x rows arrive by buffer LDS-DMA two steps ahead into a 6-row ring (the residual row is the
-//     oldest), t rows live in a 4-row ring; 128-B pixel rows with the 16-B chunk c at slot
+//   * two such workgroups per CU (two waves per SIMD: one's barrier and epilogue bubbles under the
+//     other's MFMAs); x rows arrive by buffer LDS-DMA one step ahead into a 5-row ring (the
+//     residual row is the oldest), t rows live in a 4-row ring; 128-B pixel rows with the 16-B chunk c at slot
 //     c ^ ((pixel >> 1) & 7) (conflict-free ds_read_b128 at any pixel offset);
 //   * pixels and rows outside the image are zero in both rings (the convs' zero padding).
 #include "common.h"
@@ -33,12 +34,12 @@ constexpr int kOW = 62;                // output columns per strip
 constexpr int kTW = 64;                // t columns per strip (2 blocks of 32): image cols c0 - 1 ..
 constexpr int kXW = 66;                // x columns per strip: image cols c0 - 2 ..
 constexpr int kRowB = 128;             // bytes per pixel row (64 bf16)
-constexpr int kXSlot = kXW * kRowB;    // 8448
-constexpr int kXRing = 6;
+constexpr int kXSlot = 9 * 1024;       // 66 pixel rows (8448 B) padded to whole 1-KB DMA instructions
+constexpr int kXRing = 5;              // residual row j-2, conv1 rows j-1 .. j+1, DMA row j+2
 constexpr int kTSlot = kTW * kRowB;    // 8192
 constexpr int kTRing = 4;
-constexpr int kTBase = kXRing * kXSlot;                  // 50688
-constexpr int kLds = kTBase + kTRing * kTSlot + 512;     // + slack: conv2 reads t pixels 64, 65 (unstored columns)
+constexpr int kTBase = kXRing * kXSlot;                  // 46080
+constexpr int kLds = kTBase + kTRing * kTSlot + 512;     // + slack: conv2 reads t pixels 64, 65 (unstored columns); two workgroups per CU
 constexpr int kSlices = 36;            // 9 taps x 4 slices of 16 channels
 constexpr int kFragB = 16;             // bytes per lane per A fragment
 constexpr int kPackW = 2 * 2 * kSlices * 64 * kFragB;    // [conv][half][slice][lane][8 bf16]
@@ -60,7 +61,7 @@ __device__ __forceinline__ void ds_rd16(u32x4_t& dst, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
 }
 
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
 block64_kernel(const BlockParams a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -137,19 +138,18 @@ block64_kernel(const BlockParams a) {
         const int byte = i * 1024 + lane * 16;
         const int p = byte >> 7, sl = (byte >> 4) & 7;
         const int col = c0 - 2 + p;
-        const bool ok = row_ok && byte < kXSlot && static_cast<unsigned>(col) < static_cast<unsigned>(W);
+        const bool ok = row_ok && p < kXW && static_cast<unsigned>(col) < static_cast<unsigned>(W);
         const unsigned off = ok ? static_cast<unsigned>(((img0 + row) * W + col) * kRowB + ((sl ^ bswz(p)) << 4)) : kOob;
-        if (byte < kXSlot || i < kXPieces - 1)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(xs, (lds_t*)(smem + slot * kXSlot + i * 1024), 16, off, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xs, (lds_t*)(smem + slot * kXSlot + i * 1024), 16, off, 0, 0, 0);
       }
     };
-    // prologue: x rows ya-2 .. ya+1 (steps start at j = ya - 1; step j issues row j + 3)
-    for (int row = ya - 2; row <= ya + 1; ++row) x_dma(row);
+    // prologue: x rows ya-2 .. ya (steps start at j = ya - 1; step j issues row j + 2)
+    for (int row = ya - 2; row <= ya; ++row) x_dma(row);
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 
     for (int j = ya - 1; j <= yb + 1; ++j) {
-      x_dma(j + 3);
+      x_dma(j + 2);
       const int xs_m1 = ((j - 1) % kXRing + kXRing) % kXRing;
       f32x16 acc0 = cinit, acc1 = cinit;
       if (role == 0) {
@@ -243,12 +243,10 @@ block64_kernel(const BlockParams a) {
           }
         }
       }
-      // retire this wave's DMA pieces of row j + 2 (issued at the start of step j - 1): younger are
-      // step j - 1's stores, this step's pieces of row j + 3 and its stores (conv2 waves: 8 stores
-      // per step; pieces per wave: 3 for wave 0, 2 for waves 1-3); then hand the t row over
-      if (wave == 0) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (wave == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(18)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // retire this wave's DMA pieces of row j + 2 (issued at the start of this step; younger: the
+      // conv2 waves' 8 stores), then hand the t row and the x row over
+      if (role == 0) asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -319,7 +317,7 @@ extern "C" int drnmi_basic_block64(const void* x, const void* pack, void* y, int
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    g_block_wgs = cus;
+    g_block_wgs = 2 * cus;                             // two workgroups per CU (79 KB LDS each)
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&block64_kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     if (e != hipSuccess) return static_cast<int>(e);
