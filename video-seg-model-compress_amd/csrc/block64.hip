@@ -74,11 +74,12 @@ block64_kernel(const BlockParams a) {
   u32x4_t wf[kSlices];
   {
     const u32x4_t* pk = reinterpret_cast<const u32x4_t*>(a.pack) + ((role * 2 + half) * kSlices) * 64 + lane;
+    // all loads first, then the AGPR pins (a pin right after its load would wait for it: 36
+    // serial L2 round trips before the first step)
 #pragma unroll
-    for (int s = 0; s < kSlices; ++s) {
-      wf[s] = pk[s * 64];
-      asm volatile("" : "+a"(wf[s]));
-    }
+    for (int s = 0; s < kSlices; ++s) wf[s] = pk[s * 64];
+#pragma unroll
+    for (int s = 0; s < kSlices; ++s) asm volatile("" : "+a"(wf[s]));
   }
   // accumulator start: the conv's shift for the 16 D rows this lane holds
   f32x16 cinit;

@@ -265,6 +265,7 @@ constexpr TileDesc kTiles[] = {
     {256, 256, "strip256"},                                // conv_big.hip, strip-staged B (3x3, wo % 256 == 0)
     {256, 256, "stag256"},                                 // the strip tile, SIMD partners half a K step apart
     {32, 32, "seg32"},                                     // conv_seg.hip: the seg classifier (1x1, cout <= 32)
+    {64, 64, "s2row"},                                     // conv_s2row.hip: stride-2 3x3 32->64 / 64->128 row walk
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 

@@ -1,0 +1,362 @@
+// Row-walking stride-2 3x3 conv (bf16 NHWC, pad 1, BN scale folded): the BasicBlock conv1 of
+// DRN-D layer3.0 (32 -> 64) and layer4.0 (64 -> 128) (lmodels/drn.py:27-29 conv3x3, :49-52 with
+// stride 2; BN folded from eval running stats).
+//
+// On conv_big these launches gathered every tap's 256 pixels through an LDS-DMA ring per
+// 256-pixel tile: 9 K steps per tile, the ring's fill and the epilogue exposed once per tile
+// (121 us / 76 us per D-22 batch-8 step, 3.3 / 2.6 TB/s of algorithmic bytes, against HBM floors of
+// ~50 / ~25 us).  Here the work is one read of x and one write of y, streamed:
+//   * a workgroup owns an output column strip (OWS = 64 / 32 pixels) of a frame and walks a
+//     contiguous range of its output rows; input rows (2 OWS + 1 pixels) arrive by buffer LDS-DMA
+//     into a 7-slot ring two steps ahead (step oh reads rows 2 oh - 1 .. 2 oh + 1 and issues rows
+//     2 oh + 4, 2 oh + 5), so each input byte crosses HBM once and no tap is re-gathered;
+//   * wave (wc, wp) computes output channels 32 wc .. +31 x 32 pixels; its weights (32 rows x
+//     9 cin, v_mfma_f32_16x16x32_bf16 A fragments) are loaded once into AGPRs;
+//   * pixel rows in LDS: 16-B chunk c of pixel p at granule ((q gpp + c) ^ h(b)) of its 256-B block
+//     b (q = p within the block; h(b) = b & 7 for 64-B pixels, 2 b & 15 for 128-B pixels): the
+//     stride-2 fragment reads are 2-way (64-B pixels) / conflict-free (128-B pixels);
+//   * two workgroups per CU; out-of-image pixels and rows come in as zeros (buffer OOB).
+// Per accumulator the K order (32-channel chunks of the packed [cout_pad][9 cin] rows, tap-major),
+// the MFMA, the start value (shift) and the epilogue (ReLU, RNE to bf16) are conv_big's BK-32 /
+// BK-64 tiles': the output is bit-identical to them (tests/test_gpu_s2row.py).
+#include "common.h"
+#include "kernels.h"
+
+#include <cstdlib>
+#include <type_traits>
+
+namespace drnmi {
+namespace {
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+#ifndef DRNMI_S2_ABL
+#define DRNMI_S2_ABL 0         // diagnostic builds only: bit 0 drops the MFMAs, bit 1 the in-loop DMA,
+#endif                         // bit 2 the output stores, bit 3 the fragment reads, bit 4 the step barrier
+#ifndef DRNMI_S2_RING32
+#define DRNMI_S2_RING32 7      // input-row slots for cin 32: 3 in use + 2 per step of DMA lead
+#endif
+#ifndef DRNMI_S2_WGS32
+#define DRNMI_S2_WGS32 2       // workgroups per CU for cin 32
+#endif
+#ifndef DRNMI_S2_RING64
+#define DRNMI_S2_RING64 7
+#endif
+#ifndef DRNMI_S2_WGS64
+#define DRNMI_S2_WGS64 2
+#endif
+
+constexpr int kSlotB = 9 * 1024;       // input row slot: <= 8448 B used, whole 1-KB DMA pieces
+constexpr int kPieces = kSlotB / 1024;
+constexpr unsigned kOob = 0x80000000u;
+template <int RING>
+constexpr int s2_lds_bytes() { return RING * kSlotB + 1024; }   // + slack: reads of discarded columns past a slot, the dummy DMA piece
+
+struct S2Params {
+  const uint16_t* x;
+  const uint16_t* wgt;
+  const float* shift;
+  uint16_t* y;
+  int n, h, w, ho, wo, k_pad, relu, strips, total, per_wg;
+};
+
+template <int CIN>
+struct S2Cfg {
+  static constexpr int PB = 2 * CIN;             // bytes per input pixel
+  static constexpr int GPP = PB / 16;            // 16-B chunks per pixel
+  static constexpr int PPB = 256 / PB;           // pixels per 256-B block
+  static constexpr int NCW = CIN == 32 ? 2 : 4;  // channel waves (cout = 32 NCW)
+  static constexpr int NPW = 4 / NCW;            // pixel waves
+  static constexpr int COUT = 32 * NCW;
+  static constexpr int OWS = 32 * NPW;           // output columns per strip
+  static constexpr int XW = 2 * OWS + 1;         // input columns per strip
+  static constexpr int SUBS = CIN / 32;          // 32-channel K chunks per tap
+  static constexpr int NKS = 9 * SUBS;           // K chunks
+  static constexpr int NE = 2 * NKS;             // (K chunk, pixel fragment) entries per row
+  static_assert(XW * PB <= kSlotB - 256, "slot");
+};
+
+// LDS byte offset of 16-B chunk c of strip pixel p inside a slot
+template <int CIN>
+__host__ __device__ __forceinline__ int s2_lds(int p, int c) {
+  using C = S2Cfg<CIN>;
+  const int b = p / C::PPB, q = p % C::PPB;
+  const int h = C::GPP == 4 ? (b & 7) : ((2 * b) & 15);
+  return (b << 8) | ((((q * C::GPP) + c) ^ h) << 4);
+}
+
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+__device__ __forceinline__ void fake_rd(u32x4_t& dst, uint32_t addr) {   // DRNMI_S2_ABL bit 3
+  asm volatile("" : "+v"(dst) : "v"(addr));
+}
+
+template <int OFF>
+__device__ __forceinline__ void ds_rd16(u32x4_t& dst, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
+}
+
+template <int CIN, int RING, int WGS>
+__global__ void __launch_bounds__(256, WGS) __attribute__((amdgpu_waves_per_eu(WGS, WGS)))
+conv_s2row_kernel(const S2Params a) {
+  using C = S2Cfg<CIN>;
+  constexpr int D = (RING - 3) / 2;                  // steps of DMA lead
+  static_assert(RING == 3 + 2 * D && D >= 1 && D <= 2, "ring");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wc = wave % C::NCW, wp = wave / C::NCW;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // weights: A fragment (fm, ks) = packed row 32 wc + 16 fm + fr, columns 32 ks + 8 fq .. +7
+  // (all loads first, then the AGPR pins: a pin right after each load waits for it)
+  u32x4_t wf[C::NKS][2];
+#pragma unroll
+  for (int ks = 0; ks < C::NKS; ++ks)
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+      wf[ks][fm] = *reinterpret_cast<const u32x4_t*>(a.wgt + static_cast<int64_t>(32 * wc + 16 * fm + fr) * a.k_pad +
+                                                     32 * ks + 8 * fq);
+#pragma unroll
+  for (int ks = 0; ks < C::NKS; ++ks)
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm) asm volatile("" : "+a"(wf[ks][fm]));
+  f32x4 cinit[2];
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm) {
+    const float4 s = *reinterpret_cast<const float4*>(a.shift + 32 * wc + 16 * fm + 4 * fq);
+    cinit[fm] = f32x4{s.x, s.y, s.z, s.w};
+  }
+  const int H = a.h, W = a.w;
+  const __amdgpu_buffer_rsrc_t xs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.x), 0, a.n * H * W * C::PB, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ys =
+      __builtin_amdgcn_make_buffer_rsrc(a.y, 0, a.n * a.ho * a.wo * C::COUT * 2, 0x00020000);
+  typedef __attribute__((address_space(3))) void lds_t;
+
+  // B fragment (fn, kw, sub): output pixel wp 32 + 16 fn + fr -> strip pixel 2 (..) + kw, chunk 4 sub + fq
+  uint32_t boff[2][3][C::SUBS];
+#pragma unroll
+  for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int sb = 0; sb < C::SUBS; ++sb)
+        boff[fn][kw][sb] = static_cast<uint32_t>(s2_lds<CIN>(2 * (32 * wp + 16 * fn + fr) + kw, 4 * sb + fq));
+  int idx = blockIdx.x * a.per_wg;
+  const int end = min(idx + a.per_wg, a.total);
+  while (idx < end) {
+    const int seg = idx / a.ho;
+    const int ya = idx - seg * a.ho;
+    const int yb = min(a.ho, ya + (end - idx));
+    idx += yb - ya;
+    const int n = seg / a.strips, s = seg - n * a.strips;
+    const int ow0 = C::OWS * s;
+    const int col0 = 2 * ow0 - 1;                      // image column of strip pixel 0
+    const int img0 = n * H;
+
+    // the 18 DMA pieces of input rows (r0, r0 + 1): wave w issues pieces i = w + 4 k, k < 5 (row
+    // i / 9, 1-KB piece i % 9 of its slot); the lane's (pixel, chunk) and the strip/image column
+    // test depend only on (k, lane), so the per-step work is a scalar row offset and one select.
+    // Waves 2, 3 have no piece 4 (i >= 18): theirs is an all-OOB load into the slack KB after
+    // the ring (zeros nobody needs), so every wave issues 5 and the vmcnt counts are uniform.
+    uint32_t vo[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int i = wave + 4 * k;
+      const int g = (i % kPieces) * 64 + lane;
+      const int b = g >> 4;
+      const int hb = C::GPP == 4 ? (b & 7) : ((2 * b) & 15);
+      const int v = (g & 15) ^ hb;
+      const int pp = b * C::PPB + v / C::GPP, c = v % C::GPP;
+      const int col = col0 + pp;
+      vo[k] = i < 2 * kPieces && pp < C::XW && static_cast<unsigned>(col) < static_cast<unsigned>(W)
+                  ? static_cast<unsigned>(col * C::PB + c * 16) : kOob;
+    }
+    const int rowb = W * C::PB;                        // bytes per image row
+    auto piece = [&](int k, int r0, int slot0) {       // piece k of rows (r0, r0 + 1); slot0 = slot of r0
+      const int i = wave + 4 * k;
+      const int dr = i >= kPieces ? 1 : 0;
+      const int row = r0 + dr;
+      int slot = slot0 + dr;
+      slot = slot >= RING ? slot - RING : slot;
+      const bool row_ok = static_cast<unsigned>(row) < static_cast<unsigned>(H) && i < 2 * kPieces;
+      // wave-uniform by construction; readfirstlane keeps them in SGPRs (a VGPR soffset would
+      // make the compiler wrap the load in a waterfall loop)
+      const int soff = __builtin_amdgcn_readfirstlane(row_ok ? (img0 + row) * rowb : 0);
+      const int dst = __builtin_amdgcn_readfirstlane(i < 2 * kPieces ? slot * kSlotB + (i - dr * kPieces) * 1024 : RING * kSlotB);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xs, (lds_t*)(smem + dst), 16, row_ok ? vo[k] : kOob, soff, 0, 0);
+    };
+    auto mod_ring = [](int r) { return ((r % RING) + RING) % RING; };
+    // prologue: rows 2 ya - 1 .. 2 ya + 2 D (step ya re-issues 2 ya + 2 D: same bytes, no reader yet)
+#pragma unroll
+    for (int r = 0; r <= D; ++r)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) piece(k, 2 * ya - 1 + 2 * r, mod_ring(2 * ya - 1 + 2 * r));
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    int s_lo = mod_ring(2 * ya - 1);                   // slot of row 2 oh - 1
+    int s_dma = mod_ring(2 * ya + 2 * D);              // slot of row 2 oh + 2 D
+    for (int oh = ya; oh < yb; ++oh) {
+      uint32_t rb[3];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int sl = s_lo + kh;
+        rb[kh] = static_cast<uint32_t>((sl >= RING ? sl - RING : sl) * kSlotB);
+      }
+      const int r_dma = 2 * oh + 2 * D, sl_dma = s_dma;
+      f32x4 acc[2][2] = {{cinit[0], cinit[0]}, {cinit[1], cinit[1]}};
+      constexpr int PF = 4;
+      u32x4_t bq[PF + 1];
+      auto issue_rd = [&](auto e_c) {
+        constexpr int E = decltype(e_c)::value;
+        constexpr int KS = E / 2, FN = E % 2;
+        constexpr int TAP = KS / C::SUBS, SB = KS % C::SUBS;
+        if constexpr ((DRNMI_S2_ABL & 8) != 0) fake_rd(bq[E % (PF + 1)], rb[TAP / 3] + boff[FN][TAP % 3][SB]);
+        else ds_rd16<0>(bq[E % (PF + 1)], rb[TAP / 3] + boff[FN][TAP % 3][SB]);
+      };
+      static_for<0, PF>(issue_rd);
+      auto entry = [&](auto e_c) {
+        constexpr int E = decltype(e_c)::value;
+        constexpr int KS = E / 2, FN = E % 2;
+        if constexpr (E + PF < C::NE) issue_rd(std::integral_constant<int, E + PF>{});
+        constexpr int AHEAD = (E + PF < C::NE ? E + PF : C::NE - 1) - E;   // reads issued after entry E's
+        asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(AHEAD) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, bq[E % (PF + 1)]);
+        if constexpr ((DRNMI_S2_ABL & 1) != 0) {
+          asm volatile("" :: "v"(bv), "a"(wf[KS][0]), "a"(wf[KS][1]));
+        } else {
+          acc[0][FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[KS][0]), bv, acc[0][FN], 0, 0, 0);
+          acc[1][FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[KS][1]), bv, acc[1][FN], 0, 0, 0);
+        }
+        if constexpr (E < 5 && (DRNMI_S2_ABL & 2) == 0) piece(E, r_dma, sl_dma);   // this step's DMA, one piece per MFMA pair
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      static_for<0, C::NE>(entry);
+
+      // epilogue (store_tile_x4's conversion): ReLU, RNE, one 16-B piece per pixel fragment
+      const bool relu = a.relu != 0;
+      const int obase = (n * a.ho + oh) * a.wo;
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn) {
+        uint32_t wv[4];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          float v[4] = {acc[hh][fn][0], acc[hh][fn][1], acc[hh][fn][2], acc[hh][fn][3]};
+          if (relu) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          }
+          wv[2 * hh] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+          wv[2 * hh + 1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+        }
+        uint4 o = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        swap_halves(o);
+        const int ow = ow0 + 32 * wp + 16 * fn + fr;
+        const unsigned ob = ow < a.wo ? static_cast<unsigned>(((obase + ow) * C::COUT + 32 * wc + chunk_of_row(fq) * 8) * 2) : kOob;
+        if constexpr ((DRNMI_S2_ABL & 4) == 0) __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o.x, o.y, o.z, o.w}, ys, ob, 0, 0);
+        else asm volatile("" :: "v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w), "v"(ob));
+      }
+      // retire the DMA pieces of rows 2 oh + 2, 2 oh + 3 (issued D - 1 steps ago; younger ops stay
+      // in flight: the 2 stores, and with D = 2 this step's pieces), then publish them and free
+      // the slots of 2 oh - 1, 2 oh
+      if ((DRNMI_S2_ABL & 16) != 0) asm volatile("s_waitcnt vmcnt(7)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+      else if ((DRNMI_S2_ABL & 4) != 0) asm volatile("s_waitcnt vmcnt(5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (D == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(7)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      s_lo = s_lo + 2 >= RING ? s_lo + 2 - RING : s_lo + 2;
+      s_dma = s_dma + 2 >= RING ? s_dma + 2 - RING : s_dma + 2;
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+int g_cus = 0;
+constexpr auto kern32 = &conv_s2row_kernel<32, DRNMI_S2_RING32, DRNMI_S2_WGS32>;
+constexpr auto kern64 = &conv_s2row_kernel<64, DRNMI_S2_RING64, DRNMI_S2_WGS64>;
+
+// DRNMI_S2ROW=0 keeps these convs on conv_big (A/B runs)
+bool s2row_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("DRNMI_S2ROW");
+    on = (e != nullptr && e[0] == '0') ? 0 : 1;
+  }
+  return on == 1;
+}
+
+}  // namespace
+
+bool s2row_conv_supported(const drnmi_conv_args& p) {
+  const bool c32 = p.cin == 32 && p.cout == 64, c64 = p.cin == 64 && p.cout == 128;
+  return p.dtype == DRNMI_BF16 && p.out_dtype == DRNMI_BF16 && (c32 || c64) && p.ks == 3 && p.stride == 2 &&
+         p.pad == 1 && p.dil == 1 && p.scale == nullptr && p.res == nullptr && p.x2 == nullptr &&
+         p.unit_mask == nullptr && p.k == 9 * p.cin && p.k_pad >= p.k && p.k_pad % 8 == 0 && p.cout_pad >= p.cout &&
+         p.n > 0 && p.h >= 1 && p.w >= 1 && p.ho == (p.h - 1) / 2 + 1 && p.wo == (p.w - 1) / 2 + 1 && p.y_sc == 1 &&
+         p.y_sp == p.cout && p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout &&
+         static_cast<int64_t>(p.n) * p.h * p.w * p.cin * 2 < (int64_t(1) << 31) &&
+         static_cast<int64_t>(p.n) * p.ho * p.wo * p.cout * 2 < (int64_t(1) << 31);
+}
+
+bool s2row_auto(const drnmi_conv_args& p) { return s2row_enabled() && s2row_conv_supported(p); }
+
+const char* s2row_conv_name(const drnmi_conv_args& p) {
+  if (!s2row_conv_supported(p)) return nullptr;
+#define DRNMI_S2_STR2(x) #x
+#define DRNMI_S2_STR(x) DRNMI_S2_STR2(x)
+  return p.cin == 32 ? "conv_s2row_kernel<32, " DRNMI_S2_STR(DRNMI_S2_RING32) ", " DRNMI_S2_STR(DRNMI_S2_WGS32) ">"
+                     : "conv_s2row_kernel<64, " DRNMI_S2_STR(DRNMI_S2_RING64) ", " DRNMI_S2_STR(DRNMI_S2_WGS64) ">";
+}
+
+int s2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t st) {
+  if (!s2row_conv_supported(p)) return DRNMI_ENOTSUP;
+  if (g_cus == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern32), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       s2_lds_bytes<DRNMI_S2_RING32>());
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern64), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              s2_lds_bytes<DRNMI_S2_RING64>());
+    if (e != hipSuccess) return static_cast<int>(e);
+    g_cus = cus;
+  }
+  const bool c32 = p.cin == 32;
+  const int wgs = g_cus * (c32 ? DRNMI_S2_WGS32 : DRNMI_S2_WGS64);   // persistent: WGS workgroups per CU
+  S2Params a;
+  a.x = static_cast<const uint16_t*>(p.x);
+  a.wgt = static_cast<const uint16_t*>(p.wgt);
+  a.shift = p.shift;
+  a.y = static_cast<uint16_t*>(p.y);
+  a.n = p.n;
+  a.h = p.h;
+  a.w = p.w;
+  a.ho = p.ho;
+  a.wo = p.wo;
+  a.k_pad = p.k_pad;
+  a.relu = p.relu;
+  const int ows = p.cin == 32 ? S2Cfg<32>::OWS : S2Cfg<64>::OWS;
+  a.strips = (p.wo + ows - 1) / ows;
+  const int64_t total = static_cast<int64_t>(p.n) * a.strips * p.ho;
+  if (total >= (int64_t(1) << 31)) return DRNMI_ENOTSUP;
+  a.total = static_cast<int>(total);
+  a.per_wg = (a.total + wgs - 1) / wgs;
+  const int grid = (a.total + a.per_wg - 1) / a.per_wg;
+  if (c32) hipLaunchKernelGGL(kern32, dim3(grid), dim3(256), s2_lds_bytes<DRNMI_S2_RING32>(), st, a);
+  else hipLaunchKernelGGL(kern64, dim3(grid), dim3(256), s2_lds_bytes<DRNMI_S2_RING64>(), st, a);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace drnmi

@@ -34,4 +34,10 @@ hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s);
 // BK-32 tile.
 bool seg_conv_supported(const drnmi_conv_args& p);
 int seg_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
+// Row-walking stride-2 3x3 conv, 32 -> 64 / 64 -> 128 (conv_s2row.hip), bit-identical to conv_big's
+// BK-32 / BK-64 tiles; s2row_auto: supported and not disabled by DRNMI_S2ROW=0.
+bool s2row_conv_supported(const drnmi_conv_args& p);
+bool s2row_auto(const drnmi_conv_args& p);
+int s2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
+const char* s2row_conv_name(const drnmi_conv_args& p);
 }  // namespace drnmi
