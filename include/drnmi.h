@@ -251,6 +251,13 @@ int drnmi_up8_logsoftmax_argmax(const float* logits, const float* up_w, float* l
                                 void* labels, int32_t label_dtype, int32_t n, int32_t c,
                                 int32_t h, int32_t w, void* stream);
 
+/* Labels-only form of the same head (the video path: no log-prob planes) on NHWC logits: fp32
+ * [n][h][w][cs] rows, classes 0..c-1 first (cs % 4 == 0, cs >= c, 16-B aligned), as the seg conv
+ * writes them with y_sp = cs, y_sc = 1.  Same per-pixel arithmetic, near-tie fallback and argmax
+ * order as drnmi_up8_logsoftmax_argmax: identical labels.  c == 19 (else DRNMI_ENOTSUP). */
+int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const float* up_w, void* labels, int32_t label_dtype,
+                          int32_t n, int32_t c, int32_t h, int32_t w, void* stream);
+
 /* Same head for DRNSeg(use_torch_up=True): nn.UpsamplingBilinear2d(scale_factor=8) (bilinear,
  * align_corners=True; lmodels/drnseg.py:285-287) + LogSoftmax + argmax.  Source index and
  * weights follow ATen's CPU kernel: scale = (in-1)/(out-1) in fp32, i0 = floor(scale*dst),

@@ -1,0 +1,80 @@
+"""Labels-only head on NHWC logits (drnmi_up8_labels_nhwc, csrc/ops.hip up8_labels_oct_kernel<.., true>)
+and the seg conv's NHWC fp32 store it reads (conv_tile.h store_tile, 16-B rows): the video path's
+DRNSeg.segment (lmodels/drnseg.py:285-299 up + LogSoftmax, seg_video_old_no_plot.py:166 argmax).
+
+Oracle: the NCHW head the engine used before (drnmi_up8_logsoftmax_argmax, itself checked against
+the fp32 torch restatement in test_gpu_kernels) -- same values, same per-pixel arithmetic, so the
+labels must be identical, including at exact and near ties between classes.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import pytest
+import torch
+
+from drnmi import _lib, drnseg
+from drnmi.drnseg import INFO_MEAN, INFO_STD
+from drnmi.weights import bilinear_up_kernel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _up_plane():
+    return torch.from_numpy(bilinear_up_kernel(16)).float().contiguous().to(DEV)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (2, 5, 7), (3, 17, 33), (8, 128, 256)])
+@pytest.mark.parametrize("ldt", [torch.uint8, torch.int64])
+def test_labels_nhwc_match_nchw_head(shape, ldt):
+    n, h, w = shape
+    g = torch.Generator().manual_seed(h * 31 + w)
+    logits = torch.randn(n, 19, h, w, generator=g) * 3
+    # exact ties and near ties (the fallback path): copy class 4 into class 11 (+ tiny offsets)
+    logits[:, 11] = logits[:, 4]
+    logits[:, 12, ::2] = logits[:, 4, ::2] + 2 ** -20
+    logits = logits.to(DEV)
+    cs = 20
+    nhwc = torch.full((n, h, w, cs), float("nan"), device=DEV)
+    nhwc[..., :19] = logits.permute(0, 2, 3, 1)
+    up = _up_plane()
+    code = _lib.DRNMI_I64 if ldt == torch.int64 else _lib.DRNMI_U8
+    a = torch.empty(n, 8 * h, 8 * w, dtype=ldt, device=DEV)
+    b = torch.empty_like(a)
+    lib = _lib.load()
+    st = ctypes.c_void_p(_lib.stream_ptr())
+    _lib.check(lib.drnmi_up8_logsoftmax_argmax(logits.data_ptr(), up.data_ptr(), None, a.data_ptr(), code, n, 19,
+                                               h, w, st), "nchw head")
+    _lib.check(lib.drnmi_up8_labels_nhwc(nhwc.data_ptr(), cs, up.data_ptr(), b.data_ptr(), code, n, 19, h, w, st),
+               "nhwc head")
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
+def test_labels_nhwc_rejects_bad_args():
+    lib = _lib.load()
+    x = torch.zeros(1, 4, 4, 20, device=DEV)
+    up = _up_plane()
+    lab = torch.empty(1, 32, 32, dtype=torch.uint8, device=DEV)
+    st = ctypes.c_void_p(_lib.stream_ptr())
+    assert lib.drnmi_up8_labels_nhwc(x.data_ptr(), 18, up.data_ptr(), lab.data_ptr(), _lib.DRNMI_U8, 1, 19, 4, 4, st) == -1
+    assert lib.drnmi_up8_labels_nhwc(x.data_ptr(), 20, up.data_ptr(), lab.data_ptr(), _lib.DRNMI_U8, 1, 21, 4, 4, st) == -2
+
+
+@pytest.mark.parametrize("arch,hw", [("drn_d_22", (64, 128)), ("drn_d_22", (96, 200)), ("drn_d_38", (64, 96))])
+def test_segment_labels_nhwc_identical(arch, hw):
+    m = drnseg.build(arch, 19, seed=3, device=torch.device(DEV), precision="bf16").eval()
+    g = torch.Generator(device=DEV).manual_seed(9)
+    frames = torch.randint(0, 256, (2, *hw, 3), dtype=torch.uint8, device=DEV, generator=g)
+    old = drnseg.LABELS_NHWC
+    try:
+        drnseg.LABELS_NHWC = False
+        ref = m.segment(frames, INFO_MEAN, INFO_STD, False).clone()
+        drnseg.LABELS_NHWC = True
+        got = m.segment(frames, INFO_MEAN, INFO_STD, False)
+    finally:
+        drnseg.LABELS_NHWC = old
+    plans = list(m._plans.values())
+    assert plans and all(p.seg_nhwc_args is not None for p in plans), "the bf16 plan must take the NHWC logits path"
+    assert torch.equal(ref, got)

@@ -280,6 +280,10 @@ __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4
   const int hw_o = p.ho * p.wo;
   const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
   const bool nhwc16 = p.out_dtype == DRNMI_BF16 && p.y_sc == 1;
+  // fp32 NHWC rows with room for a whole 4-channel group (y_sp a multiple of 4): one 16-B store;
+  // channels past cout inside the row (the labels-only seg logits' padding) get the padded
+  // weight rows' values, which no reader uses
+  const bool nhwc32 = p.out_dtype == DRNMI_F32 && p.y_sc == 1 && p.y_sp % 4 == 0;
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
     const int m = cur_px0 + wp * PXW + fn * 16 + fr;
@@ -324,7 +328,9 @@ __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
       }
-      if (nhwc16 && full) {
+      if (nhwc32 && co + 4 <= p.y_sp) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.y) + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
+      } else if (nhwc16 && full) {
         uint2 o;
         o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
         o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);

@@ -267,10 +267,13 @@ up8_lsm_quad_kernel(const float* __restrict__ logits, const float* __restrict__ 
 // those 8 rows: the 4 taps per class are loaded once for 32 pixels (the quad kernel re-loads
 // them for every output row).  Per pixel: the quad kernel's labels-only arithmetic, near-tie
 // fallback and argmax order, so the labels are identical.
-template <int NC, int LABEL_DTYPE>
+// NHWC: logits as [n][h][w][cs] fp32 rows (cs % 4 == 0, cs >= NC; the seg conv's labels-only
+// output, one float4 per 4 classes) instead of NC planes; the values and the per-pixel arithmetic
+// are the same, so are the labels.
+template <int NC, int LABEL_DTYPE, bool NHWC = false>
 __global__ void __launch_bounds__(256)
 up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict__ up_w,
-                      void* __restrict__ labels, int h, int w) {
+                      void* __restrict__ labels, int h, int w, int cs = 0) {
   __shared__ float wk[256];
   wk[threadIdx.x] = up_w[threadIdx.x];
   __syncthreads();
@@ -285,15 +288,35 @@ up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict_
   const bool vi0 = i0 >= 0, vi1 = i1 < h, vj0 = j0 >= 0, vj1 = j1 < w;
   const int ci0 = vi0 ? i0 : 0, ci1 = vi1 ? i1 : 0, cj0 = vj0 ? j0 : 0, cj1 = vj1 ? j1 : 0;
   const int64_t plane = static_cast<int64_t>(h) * w;
-  const float* src = logits + static_cast<int64_t>(n) * NC * plane;
   float s00[NC], s01[NC], s10[NC], s11[NC];
+  if constexpr (NHWC) {
+    constexpr int NC4 = (NC + 3) / 4;
+    const float* src = logits + static_cast<int64_t>(n) * plane * cs;
+    auto taps = [&](float (&d)[NC], int iy, int ix) {
+      const float4* r = reinterpret_cast<const float4*>(src + (static_cast<int64_t>(iy) * w + ix) * cs);
 #pragma unroll
-  for (int k = 0; k < NC; ++k) {
-    const float* s = src + k * plane;
-    s00[k] = s[ci0 * w + cj0];
-    s01[k] = s[ci0 * w + cj1];
-    s10[k] = s[ci1 * w + cj0];
-    s11[k] = s[ci1 * w + cj1];
+      for (int k4 = 0; k4 < NC4; ++k4) {
+        const float4 v = r[k4];
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (4 * k4 + j < NC) d[4 * k4 + j] = e[j];
+      }
+    };
+    taps(s00, ci0, cj0);
+    taps(s01, ci0, cj1);
+    taps(s10, ci1, cj0);
+    taps(s11, ci1, cj1);
+  } else {
+    const float* src = logits + static_cast<int64_t>(n) * NC * plane;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const float* s = src + k * plane;
+      s00[k] = s[ci0 * w + cj0];
+      s01[k] = s[ci0 * w + cj1];
+      s10[k] = s[ci1 * w + cj0];
+      s11[k] = s[ci1 * w + cj1];
+    }
   }
   const int kx1_0 = 4 * q + 4 - 8 * j1;   // kx1 of column p is kx1_0 + p, kx0 = kx1 + 8
   const int64_t HW = static_cast<int64_t>(H) * W;
@@ -583,6 +606,23 @@ extern "C" int drnmi_nhwc_to_nchw(const void* x, float* out, int32_t n, int32_t 
   } else {
     return DRNMI_EINVAL;
   }
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const float* up_w, void* labels,
+                                     int32_t label_dtype, int32_t n, int32_t c, int32_t h, int32_t w, void* stream) {
+  if (logits == nullptr || up_w == nullptr || labels == nullptr || n <= 0 || h <= 0 || w <= 0) return DRNMI_EINVAL;
+  if (c != 19) return DRNMI_ENOTSUP;                   // the 19-class oct kernel
+  if (cs < c || cs % 4 != 0 || (reinterpret_cast<uintptr_t>(logits) & 15) != 0) return DRNMI_EINVAL;
+  if (label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64) return DRNMI_EINVAL;
+  if (h + 1 > 65535 || n > 65535) return DRNMI_EINVAL;
+  const int W = w * 8;
+  dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (label_dtype == DRNMI_I64)
+    hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_I64, true>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs);
+  else
+    hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_U8, true>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs);
   return static_cast<int>(hipGetLastError());
 }
 

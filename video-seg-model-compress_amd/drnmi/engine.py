@@ -632,7 +632,37 @@ class Plan:
                     not packed.quant_after.get(i) and not packed.quant_after.get(i + 1) and \
                     lib.drnmi_block64_supported(n, *self.shapes[g.nodes[i].dst]):
                 self.block64[i] = packed.block64_pack(i)
+        self._setup_seg_nhwc()
         self.src = "nchw"
+
+    # labels-only video path: the seg conv writes fp32 NHWC rows of SEG_NHWC_CS floats (16-B
+    # stores instead of 19 strided planes) and drnmi_up8_labels_nhwc reads them; same values,
+    # same labels.  Only where the seg conv runs on conv_big (bf16 input) and the 19-class head.
+    SEG_NHWC_CS = 20
+
+    def _setup_seg_nhwc(self):
+        self.seg_idx, self.seg_nhwc_args = -1, None
+        nodes = self.packed.graph.nodes
+        idx = [i for i, nd in enumerate(nodes) if nd.out_fp32_nchw]
+        if len(idx) != 1 or self.args[idx[0]] is None:
+            return
+        i = idx[0]
+        nd, a0 = nodes[i], self.args[i]
+        if nd.conv.out_channels != 19 or nd.conv.kernel_size[0] != 1:
+            return
+        cs = self.SEG_NHWC_CS
+        lh, lw = self.shapes[nd.dst]
+        if "logits_nhwc" not in self.bufs:
+            self.bufs["logits_nhwc"] = torch.empty(self.n * lh * lw * cs, dtype=torch.float32,
+                                                   device=self.packed.device)
+        a = _lib.ConvArgs()
+        ctypes.pointer(a)[0] = a0
+        a.y = self.bufs["logits_nhwc"].data_ptr()
+        a.y_sn, a.y_sp, a.y_sc = lh * lw * cs, cs, 1
+        name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
+        if name is None or not name.decode().startswith("conv_big_kernel"):
+            return
+        self.seg_idx, self.seg_nhwc_args = i, a
 
     def _front_fusable(self, reads_of) -> bool:
         """layer0..layer2 run as one drnmi_video_front_u8 launch on the u8 path when the packed net
@@ -731,6 +761,7 @@ class Plan:
         self.front_pack_t = None                  # re-fetched (repacked) at the next ingest_u8
         for i in list(self.block64):
             self.block64[i] = self.packed.block64_pack(i)
+        self._setup_seg_nhwc()
         if self.stem_u8 is not None:
             nd = self.packed.graph.nodes[0]
             self.stem_u8.wgt = self.packed.stem_u8_w.data_ptr()
@@ -738,7 +769,9 @@ class Plan:
             self.stem_u8.shift = nd.shift.data_ptr()
 
     # ------------------------------------------------------------------ execution
-    def run_backbone(self, stream: int, timing_hook=None):
+    def run_backbone(self, stream: int, timing_hook=None, labels_only: bool = False):
+        """labels_only: the seg conv writes the NHWC logits for head_labels_nhwc (when the plan has
+        that form, seg_nhwc_args); the NCHW logits buffer is then not written."""
         lib = _lib.load()
         front = self.src == "u8" and self.front_fused
         fused_stem = self.src == "u8" and self.stem_fused and not front
@@ -768,6 +801,8 @@ class Plan:
                 continue
             if i == 0 and self.src == "u8":
                 a = self.stem_u8
+            if labels_only and i == self.seg_idx and self.seg_nhwc_args is not None:
+                a = self.seg_nhwc_args
             if timing_hook is not None:
                 timing_hook(i, nd, True)
             if i == 0 and fused_stem:
@@ -832,6 +867,14 @@ class Plan:
             logprobs.data_ptr() if logprobs is not None else None,
             labels.data_ptr() if labels is not None else None,
             lab_dtype, n, c, lh, lw, ctypes.c_void_p(stream)), "up8_logsoftmax_argmax")
+
+    def head_labels_nhwc(self, up_w: torch.Tensor, stream: int, labels: torch.Tensor):
+        """Labels from the NHWC logits run_backbone(labels_only=True) wrote (drnmi_up8_labels_nhwc)."""
+        lh, lw = self.shapes["logits"]
+        lab_dtype = _lib.DRNMI_I64 if labels.dtype == torch.int64 else _lib.DRNMI_U8
+        _lib.check(_lib.load().drnmi_up8_labels_nhwc(
+            self.bufs["logits_nhwc"].data_ptr(), self.SEG_NHWC_CS, up_w.data_ptr(), labels.data_ptr(), lab_dtype,
+            self.n, 19, lh, lw, ctypes.c_void_p(stream)), "up8_labels_nhwc")
 
     def head_bilinear(self, stream: int, logprobs: torch.Tensor | None, labels: torch.Tensor | None):
         """use_torch_up head: UpsamplingBilinear2d(8) + LogSoftmax + argmax (lmodels/drnseg.py:285-287)."""
