@@ -580,8 +580,9 @@ def test_conv_fused_downsample(case):
     a.x2, a.cin2, a.h2, a.w2, a.stride2 = x2d.data_ptr(), cin2, h2, w2, s2
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
     stag = ks == 3 and wo % 256 == 0 and cin % 128 == 0 and kp == k1 + cin2
+    s1x2 = halo and cin == 64 and cout == 64 and cin2 == 32 and s2 == 2 and dil == 1   # conv_s1x2row_kernel
     assert name.startswith("conv_stag128_x2_kernel" if stag and cout <= 128 else "conv_stag_x2_kernel" if stag
-                           else "conv_halo_kernel" if halo else "conv_big_kernel"), name
+                           else "conv_s1x2row_kernel" if s1x2 else "conv_halo_kernel" if halo else "conv_big_kernel"), name
     _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds")
     torch.cuda.synchronize()
     err = (y.float().cpu() - ref).abs().max().item()

@@ -93,3 +93,49 @@ def test_s2row_refuses_other_shapes():
     lib = _lib.load()
     assert lib.drnmi_conv_kernel_name(ctypes.byref(a)) is None
     assert lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())) == -2
+
+
+@pytest.mark.parametrize("shape", [(1, 3, 5), (2, 17, 70), (1, 40, 130), (3, 33, 200), (8, 256, 512)])
+def test_s1x2row_bit_identical_to_halo(shape):
+    """Layer3.0 conv2 + the folded 1x1 stride-2 downsample (conv_s1x2row_kernel, tile 22) against
+    conv_halo's x2 form (tile 17): same packed [W2 | W_ds | 0] rows, K order, start and epilogue."""
+    n, h, w = shape
+    h2, w2 = 2 * h, 2 * w
+    g = torch.Generator().manual_seed(h * 7 + w)
+    x = (torch.randn(n, h, w, 64, generator=g) * 0.7).bfloat16().to(DEV)
+    x2 = (torch.randn(n, h2, w2, 32, generator=g) * 0.7).bfloat16().to(DEV)
+    wt = (torch.randn(64, 64, 3, 3, generator=g) / 24).bfloat16()
+    wd = (torch.randn(64, 32, 1, 1, generator=g) / 5.7).bfloat16()
+    kp = 640
+    wpk = torch.zeros(128, kp, dtype=torch.bfloat16)
+    wpk[:64, :576] = wt.permute(0, 2, 3, 1).reshape(64, 576)
+    wpk[:64, 576:608] = wd.reshape(64, 32)
+    wpk = wpk.to(DEV)
+    sh = torch.zeros(128, device=DEV)
+    sh[:64] = (torch.randn(64, generator=g) * 0.3).to(DEV)
+    lib = _lib.load()
+    outs = {}
+    for tile in (-1, 22, 17):
+        y = torch.full((n, h, w, 64), float("nan"), device=DEV, dtype=torch.bfloat16)
+        a = _lib.ConvArgs()
+        a.x, a.wgt, a.scale, a.shift, a.res, a.y = x.data_ptr(), wpk.data_ptr(), None, sh.data_ptr(), None, y.data_ptr()
+        a.y_sn, a.y_sp, a.y_sc = h * w * 64, 64, 1
+        a.n, a.h, a.w, a.cin, a.ho, a.wo, a.cout, a.cout_pad = n, h, w, 64, h, w, 64, 128
+        a.ks, a.stride, a.pad, a.dil = 3, 1, 1, 1
+        a.k, a.k_pad = 608, kp
+        a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_BF16, _lib.DRNMI_BF16, tile, _lib.ALGO_IGEMM
+        a.x2, a.cin2, a.h2, a.w2, a.stride2 = x2.data_ptr(), 32, h2, w2, 2
+        name = lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
+        assert name == ("conv_halo_kernel<64, 1, 64>" if tile == 17 else "conv_s1x2row_kernel"), name
+        _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "s1x2row")
+        torch.cuda.synchronize()
+        outs[tile] = y
+    assert not torch.isnan(outs[22].float()).any()
+    assert torch.equal(outs[-1], outs[22])
+    assert torch.equal(outs[22], outs[17]), f"{int((outs[22] != outs[17]).sum())} of {outs[22].numel()} differ"
+    if n * h * w <= 3 * 33 * 200:
+        r = F.conv2d(x.float().permute(0, 3, 1, 2), wt.float().to(DEV), padding=1) \
+            + F.conv2d(x2.float().permute(0, 3, 1, 2), wd.float().to(DEV), stride=2) + sh[:64].view(1, -1, 1, 1)
+        r = torch.relu(r).permute(0, 2, 3, 1)
+        err = (outs[22].float() - r).abs()
+        assert bool((err <= 2 ** -7 * r.abs() + 1e-3 * r.abs().max()).all())

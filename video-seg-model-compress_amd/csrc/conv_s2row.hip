@@ -281,6 +281,206 @@ conv_s2row_kernel(const S2Params a) {
   }
 }
 
+// --- Stride-1 3x3 64 -> 64 with the block's 1x1 stride-2 downsample folded in (x2, 32 channels):
+// DRN-D layer3.0 conv2 + downsample (lmodels/drn.py:49-65, :181-186), the launch conv_halo's x2
+// form served.  Same walk as conv_s2row_kernel with one input row per step: wave (wc, wp) owns
+// output channels 32 wc .. +31 x 32 pixels of a 64-column strip; the conv input rows (66 pixels x
+// 128 B, chunk c of pixel p at c ^ (p & 7)) arrive two steps ahead into a 5-slot ring, the x2 row
+// of each output row (its 64 even pixels (2 oh, 2 ow) gathered by the DMA, 64 B each, chunk c at
+// c ^ ((p >> 1) & 3)) into a 3-slot ring.  K: the 18 32-channel tap chunks of the packed
+// [W2 | W_ds | 0] rows, then the x2 chunk (k 576 .. 607) -- conv_halo's order, start (the summed
+// shifts) and epilogue, so the output is bit-identical to it.
+constexpr int kX1Slot = 9 * 1024;     // 66 x 128 B = 8448 B used
+constexpr int kX2Slot = 4 * 1024;     // 64 x 64 B
+constexpr int kX1Ring = 5, kX2Ring = 3;
+constexpr int kS1Lds = kX1Ring * kX1Slot + kX2Ring * kX2Slot + 1024;   // + the dummy DMA piece's KB
+
+struct S1Params {
+  const uint16_t* x;
+  const uint16_t* x2;
+  const uint16_t* wgt;
+  const float* shift;
+  uint16_t* y;
+  int n, h, w, h2, w2, k_pad, relu, strips, total, per_wg;
+};
+
+__global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
+conv_s1x2row_kernel(const S1Params a) {
+  constexpr int NKS = 19, NE = 2 * NKS, OWS = 64, XW = 66;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wc = wave & 1, wp = wave >> 1;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  u32x4_t wf[NKS][2];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm)
+      wf[ks][fm] = *reinterpret_cast<const u32x4_t*>(a.wgt + static_cast<int64_t>(32 * wc + 16 * fm + fr) * a.k_pad +
+                                                     32 * ks + 8 * fq);
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+    for (int fm = 0; fm < 2; ++fm) asm volatile("" : "+a"(wf[ks][fm]));
+  f32x4 cinit[2];
+#pragma unroll
+  for (int fm = 0; fm < 2; ++fm) {
+    const float4 s = *reinterpret_cast<const float4*>(a.shift + 32 * wc + 16 * fm + 4 * fq);
+    cinit[fm] = f32x4{s.x, s.y, s.z, s.w};
+  }
+  const int H = a.h, W = a.w;
+  const __amdgpu_buffer_rsrc_t xs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.x), 0, a.n * H * W * 128, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x2s =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.x2), 0, a.n * a.h2 * a.w2 * 64, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, a.n * H * W * 128, 0x00020000);
+  typedef __attribute__((address_space(3))) void lds_t;
+
+  // B fragments: conv rows (fn, kw, sub): strip pixel 32 wp + 16 fn + fr + kw, chunk 4 sub + fq;
+  // x2 (fn): x2 pixel 32 wp + 16 fn + fr, chunk fq
+  uint32_t boff[2][3][2], b2off[2];
+#pragma unroll
+  for (int fn = 0; fn < 2; ++fn) {
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int p = 32 * wp + 16 * fn + fr + kw, c = 4 * sb + fq;
+        boff[fn][kw][sb] = static_cast<uint32_t>(p * 128 + ((c ^ (p & 7)) << 4));
+      }
+    const int p = 32 * wp + 16 * fn + fr;
+    b2off[fn] = static_cast<uint32_t>(kX1Ring * kX1Slot + p * 64 + ((fq ^ ((p >> 1) & 3)) << 4));
+  }
+
+  int idx = blockIdx.x * a.per_wg;
+  const int end = min(idx + a.per_wg, a.total);
+  while (idx < end) {
+    const int seg = idx / H;
+    const int ya = idx - seg * H;
+    const int yb = min(H, ya + (end - idx));
+    idx += yb - ya;
+    const int n = seg / a.strips, s = seg - n * a.strips;
+    const int ow0 = OWS * s;
+
+    // 16 DMA pieces per step: 0..8 the conv row (9 KB slot), 9..12 the x2 row (4 KB), 13..15
+    // dummies into the slack KB; wave w issues pieces w + 4 k, k < 4.  Lane offsets (column part)
+    // depend only on (k, lane); the row part is a scalar offset.
+    uint32_t vo[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = wave + 4 * k;
+      uint32_t v = kOob;
+      if (i < 9) {
+        const int g = i * 64 + lane, p = g >> 3, c = (g & 7) ^ (p & 7);
+        const int col = ow0 - 1 + p;
+        if (p < XW && static_cast<unsigned>(col) < static_cast<unsigned>(W)) v = static_cast<unsigned>(col * 128 + c * 16);
+      } else if (i < 13) {
+        const int g = (i - 9) * 64 + lane, p = g >> 2, c = (g & 3) ^ ((p >> 1) & 3);
+        const int ow = ow0 + p;
+        if (ow < W && 2 * ow < a.w2) v = static_cast<unsigned>(2 * ow * 64 + c * 16);
+      }
+      vo[k] = v;
+    }
+    auto piece = [&](int k, int row, int slot1, int slot2) {   // conv row `row` (slot1); x2 row of output row row - 1 (slot2)
+      const int i = wave + 4 * k;
+      int soff = 0, dst = kX1Ring * kX1Slot + kX2Ring * kX2Slot;
+      bool ok = false;
+      if (i < 9) {
+        ok = static_cast<unsigned>(row) < static_cast<unsigned>(H);
+        soff = ok ? ((n * H + row) * W) * 128 : 0;
+        dst = slot1 * kX1Slot + i * 1024;
+      } else if (i < 13) {
+        const int r2 = 2 * (row - 1);
+        ok = row - 1 >= 0 && row - 1 < H && r2 < a.h2;
+        soff = ok ? ((n * a.h2 + r2) * a.w2) * 64 : 0;
+        dst = kX1Ring * kX1Slot + slot2 * kX2Slot + (i - 9) * 1024;
+      }
+      soff = __builtin_amdgcn_readfirstlane(soff);
+      dst = __builtin_amdgcn_readfirstlane(dst);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 9 ? xs : x2s, (lds_t*)(smem + dst), 16, ok ? vo[k] : kOob, soff, 0, 0);
+    };
+    auto m5 = [](int r) { return ((r % kX1Ring) + kX1Ring) % kX1Ring; };
+    auto m3 = [](int r) { return ((r % kX2Ring) + kX2Ring) % kX2Ring; };
+    // prologue: conv rows ya - 1 .. ya + 2 with the x2 rows of output rows ya - 2 .. ya + 1 (the
+    // first two are never read); step oh then issues conv row oh + 3 and x2 row of oh + 2
+#pragma unroll
+    for (int r = -1; r <= 2; ++r)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) piece(k, ya + r, m5(ya + r), m3(ya + r - 1));
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    int s_lo = m5(ya - 1), s_dma = m5(ya + 3), s2_cur = m3(ya), s2_dma = m3(ya + 2);
+    for (int oh = ya; oh < yb; ++oh) {
+      uint32_t rb[3];
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int sl = s_lo + kh;
+        rb[kh] = static_cast<uint32_t>((sl >= kX1Ring ? sl - kX1Ring : sl) * kX1Slot);
+      }
+      const uint32_t rb2 = static_cast<uint32_t>(s2_cur * kX2Slot);
+      const int r_dma = oh + 3, sl1 = s_dma, sl2 = s2_dma;
+      f32x4 acc[2][2] = {{cinit[0], cinit[0]}, {cinit[1], cinit[1]}};
+      constexpr int PF = 4;
+      u32x4_t bq[PF + 1];
+      auto issue_rd = [&](auto e_c) {
+        constexpr int E = decltype(e_c)::value;
+        constexpr int KS = E / 2, FN = E % 2;
+        if constexpr (KS < 18) ds_rd16<0>(bq[E % (PF + 1)], rb[KS / 6] + boff[FN][(KS / 2) % 3][KS % 2]);
+        else ds_rd16<0>(bq[E % (PF + 1)], rb2 + b2off[FN]);
+      };
+      static_for<0, PF>(issue_rd);
+      auto entry = [&](auto e_c) {
+        constexpr int E = decltype(e_c)::value;
+        constexpr int KS = E / 2, FN = E % 2;
+        if constexpr (E + PF < NE) issue_rd(std::integral_constant<int, E + PF>{});
+        constexpr int AHEAD = (E + PF < NE ? E + PF : NE - 1) - E;
+        asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(AHEAD) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, bq[E % (PF + 1)]);
+        acc[0][FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[KS][0]), bv, acc[0][FN], 0, 0, 0);
+        acc[1][FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[KS][1]), bv, acc[1][FN], 0, 0, 0);
+        if constexpr (E < 4) piece(E, r_dma, sl1, sl2);
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      static_for<0, NE>(entry);
+
+      const bool relu = a.relu != 0;
+      const int obase = (n * H + oh) * W;
+#pragma unroll
+      for (int fn = 0; fn < 2; ++fn) {
+        uint32_t wv[4];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          float v[4] = {acc[hh][fn][0], acc[hh][fn][1], acc[hh][fn][2], acc[hh][fn][3]};
+          if (relu) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          }
+          wv[2 * hh] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+          wv[2 * hh + 1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+        }
+        uint4 o = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        swap_halves(o);
+        const int ow = ow0 + 32 * wp + 16 * fn + fr;
+        const unsigned ob = ow < W ? static_cast<unsigned>(((obase + ow) * 64 + 32 * wc + chunk_of_row(fq) * 8) * 2) : kOob;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o.x, o.y, o.z, o.w}, ys, ob, 0, 0);
+      }
+      // retire the pieces issued a step ago (this step's 4 and the 2 stores stay in flight)
+      asm volatile("s_waitcnt vmcnt(6)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      s_lo = s_lo + 1 >= kX1Ring ? 0 : s_lo + 1;
+      s_dma = s_dma + 1 >= kX1Ring ? 0 : s_dma + 1;
+      s2_cur = s2_cur + 1 >= kX2Ring ? 0 : s2_cur + 1;
+      s2_dma = s2_dma + 1 >= kX2Ring ? 0 : s2_dma + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 int g_cus = 0;
 constexpr auto kern32 = &conv_s2row_kernel<32, DRNMI_S2_RING32, DRNMI_S2_WGS32>;
 constexpr auto kern64 = &conv_s2row_kernel<64, DRNMI_S2_RING64, DRNMI_S2_WGS64>;
@@ -309,6 +509,58 @@ bool s2row_conv_supported(const drnmi_conv_args& p) {
 }
 
 bool s2row_auto(const drnmi_conv_args& p) { return s2row_enabled() && s2row_conv_supported(p); }
+
+bool s1x2row_conv_supported(const drnmi_conv_args& p) {
+  return p.dtype == DRNMI_BF16 && p.out_dtype == DRNMI_BF16 && p.cin == 64 && p.cout == 64 && p.ks == 3 &&
+         p.stride == 1 && p.pad == 1 && p.dil == 1 && p.x2 != nullptr && p.cin2 == 32 && p.stride2 == 2 &&
+         p.scale == nullptr && p.res == nullptr && p.unit_mask == nullptr && p.k == 9 * 64 + 32 && p.k_pad >= p.k &&
+         p.k_pad % 8 == 0 && p.cout_pad >= 64 && p.n > 0 && p.h >= 1 && p.w >= 1 && p.ho == p.h && p.wo == p.w &&
+         2 * (p.ho - 1) < p.h2 && 2 * (p.wo - 1) < p.w2 && p.y_sc == 1 && p.y_sp == 64 &&
+         p.y_sn == static_cast<int64_t>(p.ho) * p.wo * 64 && static_cast<int64_t>(p.n) * p.h * p.w * 128 < (int64_t(1) << 31) &&
+         static_cast<int64_t>(p.n) * p.h2 * p.w2 * 64 < (int64_t(1) << 31);
+}
+
+bool s1x2row_auto(const drnmi_conv_args& p) { return s2row_enabled() && s1x2row_conv_supported(p); }
+
+const char* s1x2row_conv_name(const drnmi_conv_args& p) {
+  return s1x2row_conv_supported(p) ? "conv_s1x2row_kernel" : nullptr;
+}
+
+int s1x2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t st) {
+  if (!s1x2row_conv_supported(p)) return DRNMI_ENOTSUP;
+  static int wgs = 0;
+  if (wgs == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_s1x2row_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kS1Lds);
+    if (e != hipSuccess) return static_cast<int>(e);
+    wgs = 2 * cus;                                      // two workgroups per CU (58 KB LDS each)
+  }
+  S1Params a;
+  a.x = static_cast<const uint16_t*>(p.x);
+  a.x2 = static_cast<const uint16_t*>(p.x2);
+  a.wgt = static_cast<const uint16_t*>(p.wgt);
+  a.shift = p.shift;
+  a.y = static_cast<uint16_t*>(p.y);
+  a.n = p.n;
+  a.h = p.h;
+  a.w = p.w;
+  a.h2 = p.h2;
+  a.w2 = p.w2;
+  a.k_pad = p.k_pad;
+  a.relu = p.relu;
+  a.strips = (p.w + 63) / 64;
+  const int64_t total = static_cast<int64_t>(p.n) * a.strips * p.h;
+  if (total >= (int64_t(1) << 31)) return DRNMI_ENOTSUP;
+  a.total = static_cast<int>(total);
+  a.per_wg = (a.total + wgs - 1) / wgs;
+  const int grid = (a.total + a.per_wg - 1) / a.per_wg;
+  hipLaunchKernelGGL(conv_s1x2row_kernel, dim3(grid), dim3(256), kS1Lds, st, a);
+  return static_cast<int>(hipGetLastError());
+}
 
 const char* s2row_conv_name(const drnmi_conv_args& p) {
   if (!s2row_conv_supported(p)) return nullptr;

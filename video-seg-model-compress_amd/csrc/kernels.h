@@ -40,4 +40,10 @@ bool s2row_conv_supported(const drnmi_conv_args& p);
 bool s2row_auto(const drnmi_conv_args& p);
 int s2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
 const char* s2row_conv_name(const drnmi_conv_args& p);
+// Row-walking stride-1 3x3 64 -> 64 + folded 1x1 stride-2 downsample from 32 channels (conv_s2row.hip),
+// bit-identical to conv_halo's x2 form.
+bool s1x2row_conv_supported(const drnmi_conv_args& p);
+bool s1x2row_auto(const drnmi_conv_args& p);
+int s1x2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
+const char* s1x2row_conv_name(const drnmi_conv_args& p);
 }  // namespace drnmi
