@@ -871,7 +871,18 @@ const char* sparse_name(int ks, int base) {
 #ifndef DRNMI_AUTO_PERSIST
 #define DRNMI_AUTO_PERSIST 0
 #endif
+// DRNMI_SEG_VARIANT=v: the seg classifier (1x1, cout <= 32) on conv_big variant v (A/B runs only)
+int seg_variant_override() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("DRNMI_SEG_VARIANT");
+    v = e != nullptr ? atoi(e) : -1;
+  }
+  return v;
+}
+
 int auto_variant(const drnmi_conv_args& p) {
+  if (p.ks == 1 && p.cout <= 32 && seg_variant_override() >= 0) return seg_variant_override();
   if (p.cin < 64) return p.cout % 256 == 0 ? 4 : p.cout % 128 == 0 ? 5 : 2;   // K steps of 32
   if (DRNMI_AUTO_PERSIST && p.cout % 256 == 0) return 7;
   // cout <= 32 (the seg 1x1) also takes the 64-wide BK-32 tile: 57 vs 66 us on the D-22 seg conv
