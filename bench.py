@@ -350,6 +350,9 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
         return lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
 
     names = [launched_name(i) for i in range(len(plan.args))]
+    if plan.labels_path() == "seg2":           # the seg classifier in the last conv's epilogue (drnmi_conv_stag_seg)
+        names[plan.seg_fused["conv"]] = "conv_stag_seg_kernel"
+        names[plan.seg_idx] = ""
     nodes = plan.packed.graph.nodes
     # per-launch work (roofline.launch_work): a folded downsample's FLOPs and input run inside its
     # block's last conv, the fused stem launch carries layer1; useful work of a pruned layer

@@ -258,6 +258,22 @@ int drnmi_up8_logsoftmax_argmax(const float* logits, const float* up_w, float* l
 int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const float* up_w, void* labels, int32_t label_dtype,
                           int32_t n, int32_t c, int32_t h, int32_t w, void* stream);
 
+/* The labels-only video path with the seg classifier (1x1 c_in -> 19 + bias, lmodels/drnseg.py:278-284)
+ * folded into the epilogue of the last 3x3 conv (D-22 layer8): `a` is that conv's argument block
+ * exactly as for drnmi_conv2d_bn_act (bf16, scale folded, no residual / x2, cout % 256 == 0, a shape
+ * the staggered strip tile takes) but its activation is NOT stored (a->y unused); instead each
+ * 256-channel block's partial logits go to partials[cout / 256][n*ho*wo][20] (fp32, 16-B aligned):
+ * partial_b[m][k] = sum over the block's channels c of seg_w[k][c] * bf16(relu(conv)[m][c]).
+ * seg_w: packed bf16 [seg_rows >= 32][seg_k_pad] (rows 19.. zero).  DRNMI_ENOTSUP if the conv does
+ * not take the staggered tile. */
+int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, int32_t seg_k_pad, int32_t seg_rows,
+                        float* partials, void* stream);
+
+/* Labels from those partials: logit[k] = (bias[k] + partial_0[k]) + partial_1[k] (bias: >= cs
+ * floats), then the labels-only head's arithmetic (drnmi_up8_labels_nhwc).  partials: [2][n][h][w][cs]. */
+int drnmi_up8_labels_seg2(const float* partials, int32_t cs, const float* bias, const float* up_w, void* labels,
+                          int32_t label_dtype, int32_t n, int32_t c, int32_t h, int32_t w, void* stream);
+
 /* Same head for DRNSeg(use_torch_up=True): nn.UpsamplingBilinear2d(scale_factor=8) (bilinear,
  * align_corners=True; lmodels/drnseg.py:285-287) + LogSoftmax + argmax.  Source index and
  * weights follow ATen's CPU kernel: scale = (in-1)/(out-1) in fp32, i0 = floor(scale*dst),

@@ -13,7 +13,7 @@ import ctypes
 import pytest
 import torch
 
-from drnmi import _lib, drnseg
+from drnmi import _lib, drnseg, engine
 from drnmi.drnseg import INFO_MEAN, INFO_STD
 from drnmi.weights import bilinear_up_kernel
 
@@ -67,14 +67,46 @@ def test_segment_labels_nhwc_identical(arch, hw):
     m = drnseg.build(arch, 19, seed=3, device=torch.device(DEV), precision="bf16").eval()
     g = torch.Generator(device=DEV).manual_seed(9)
     frames = torch.randint(0, 256, (2, *hw, 3), dtype=torch.uint8, device=DEV, generator=g)
-    old = drnseg.LABELS_NHWC
+    old = engine.LABELS_NHWC, engine.SEG_FUSE
     try:
-        drnseg.LABELS_NHWC = False
+        engine.SEG_FUSE = False
+        engine.LABELS_NHWC = False
         ref = m.segment(frames, INFO_MEAN, INFO_STD, False).clone()
-        drnseg.LABELS_NHWC = True
+        engine.LABELS_NHWC = True
+        got = m.segment(frames, INFO_MEAN, INFO_STD, False)
+        plans = list(m._plans.values())
+        assert plans and all(p.labels_path() == "nhwc" for p in plans), "the bf16 plan must take the NHWC logits path"
+    finally:
+        engine.LABELS_NHWC, engine.SEG_FUSE = old
+    assert torch.equal(ref, got)
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_segment_seg_fused_into_last_conv(n):
+    """D-22 at 1024 x 2048 (layer8 on the staggered tile): the seg classifier folded into layer8's
+    epilogue (drnmi_conv_stag_seg) + the SEG2 head against the separate seg conv + NHWC head.  The
+    logits differ only by fp32 summation order (two 256-channel partials): bound 2^-16 max|logit|;
+    labels may flip only at near ties."""
+    m = drnseg.build("drn_d_22", 19, seed=4, device=torch.device(DEV), precision="bf16").eval()
+    g = torch.Generator(device=DEV).manual_seed(2)
+    frames = torch.randint(0, 256, (n, 1024, 2048, 3), dtype=torch.uint8, device=DEV, generator=g)
+    old = engine.SEG_FUSE
+    try:
+        engine.SEG_FUSE = False
+        ref = m.segment(frames, INFO_MEAN, INFO_STD, False).clone()
+        plan = next(iter(m._plans.values()))
+        logits = plan.bufs["logits_nhwc"].view(n, 128, 256, 20)[..., :19].clone()
+        engine.SEG_FUSE = True
+        plan.refresh_weight_ptrs()                     # re-derives the labels path with the flag on
+        assert plan.labels_path() == "seg2"
         got = m.segment(frames, INFO_MEAN, INFO_STD, False)
     finally:
-        drnseg.LABELS_NHWC = old
-    plans = list(m._plans.values())
-    assert plans and all(p.seg_nhwc_args is not None for p in plans), "the bf16 plan must take the NHWC logits path"
-    assert torch.equal(ref, got)
+        engine.SEG_FUSE = old
+    part = plan.bufs["seg_part"].view(2, n, 128, 256, 20)
+    seg = plan.packed.graph.nodes[plan.seg_idx]
+    fused = (seg.shift[:19].view(1, 1, 1, 19) + part[0, ..., :19]) + part[1, ..., :19]
+    err = (fused - logits).abs().max().item()
+    assert err <= 2 ** -16 * logits.abs().max().item() + 1e-6, err
+    agree = (got == ref).float().mean().item()
+    print(f"seg-fused labels agreement {agree:.6f}, logits max |diff| {err:.3e}")
+    assert agree >= 0.9995

@@ -1111,3 +1111,26 @@ int weight_unit_mask(const void* wgt, int dtype, int rows_pad, int k_pad, uint32
 }
 
 }  // namespace drnmi
+
+using namespace drnmi;
+
+// The labels-only video path's last 3x3 conv (D-22 layer8) with the seg classifier folded into its
+// epilogue (conv_stag.hip SEGF): same launch geometry and MFMA work as conv_stag_kernel, the
+// activation is never stored.  Validated like the conv it replaces plus the seg operands.
+extern "C" int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, int32_t seg_k_pad, int32_t seg_rows,
+                                   float* partials, void* stream) {
+  if (a == nullptr || seg_w == nullptr || partials == nullptr) return DRNMI_EINVAL;
+  const drnmi_conv_args& p = *a;
+  if (p.x == nullptr || p.wgt == nullptr || p.shift == nullptr) return DRNMI_EINVAL;
+  if (p.algo != DRNMI_ALGO_IGEMM || p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.src_u8) return DRNMI_EINVAL;
+  if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
+      p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
+    return DRNMI_EINVAL;
+  if (seg_k_pad < p.cout || seg_k_pad % 8 != 0 || seg_rows < 32 || (reinterpret_cast<uintptr_t>(partials) & 15) != 0)
+    return DRNMI_EINVAL;
+  if (!(big_conv_supported(p) && strip_enabled() && stag_enabled() && stag_ok(p)) || p.x2 != nullptr ||
+      p.scale != nullptr || p.res != nullptr || p.cout % 256 != 0 || p.cout_pad < p.cout)
+    return DRNMI_ENOTSUP;
+  const hipError_t e = launch_stag_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream));
+  return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+}

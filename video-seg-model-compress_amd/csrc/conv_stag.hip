@@ -85,8 +85,19 @@ __device__ __forceinline__ int stag_tile(int bid, int ntiles, int nco) {
   return xcd_remap2(bid, ntiles);
 }
 
-template <typename T, bool X2, int WCO = 128>
-__device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
+// SEGF (the labels-only video path's last conv, drnmi_conv_stag_seg): the conv's own output is not
+// stored; its epilogue feeds the seg classifier (1x1 512 -> 19 + bias, lmodels/drnseg.py:278-284)
+// instead -- per tile, the partial logits over its 256 channels go to part[channel block][pixel][20]
+// and the head adds bias + block 0 + block 1 in that order.
+struct SegFuse {
+  const uint16_t* w;    // seg weights, packed [>= 32 rows][k_pad] bf16 (scale folded; rows 19.. zero)
+  int k_pad;
+  float* part;          // [nco][n ho wo][kSegCS] fp32
+};
+constexpr int kSegCS = 20;
+
+template <typename T, bool X2, int WCO = 128, bool SEGF = false>
+__device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const SegFuse& sf = SegFuse{nullptr, 0, nullptr}) {
   using K = KT<T>;
   constexpr int BK = 128 / K::ESZ;                   // 128-B LDS rows (bf16 64, int8 128 channels)
   using C = BigCfg<WCO, 2, 2, BK, 4, K::ESZ>;
@@ -420,6 +431,72 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped re-fetches
+  if constexpr (SEGF) {
+    // the activation as store_tile_x4 would store it (ReLU, RNE to bf16, 16-B pieces: lane
+    // (fr, fq) holds channels 8 s(fq) .. +7 of 32-channel group f2 of pixel fr) is the B operand of
+    // the seg GEMM, the A fragments the matching seg weight columns; then the two channel halves
+    // of the tile (waves wc = 0, 1) are added in that order through LDS
+    static_assert(K::ESZ == 2 && !X2 && WCO == 128, "seg fusion: the 256-channel bf16 tile");
+    bf16x8 aw[2][FM / 2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int f2 = 0; f2 < FM / 2; ++f2)
+        aw[mt][f2] = *reinterpret_cast<const bf16x8*>(sf.w + static_cast<int64_t>(16 * mt + fr) * sf.k_pad + co0 + wc * WCO +
+                                                      32 * f2 + chunk_of_row(fq) * 8);
+    const bool relu = p.relu != 0;
+    f32x4 pacc[2][4];
+#pragma unroll
+    for (int fn = 0; fn < 4; ++fn) {
+      pacc[0][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      pacc[1][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int f2 = 0; f2 < FM / 2; ++f2) {
+        uint32_t w[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v[4] = {acc[2 * f2 + h][fn][0], acc[2 * f2 + h][fn][1], acc[2 * f2 + h][fn][2], acc[2 * f2 + h][fn][3]};
+          if (relu) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          }
+          w[2 * h] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+          w[2 * h + 1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+        }
+        uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
+        swap_halves(o);
+        const bf16x8 b = __builtin_bit_cast(bf16x8, o);
+        pacc[0][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][f2], b, pacc[0][fn], 0, 0, 0);
+        pacc[1][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1][f2], b, pacc[1][fn], 0, 0, 0);
+      }
+    }
+    // every wave is past its last fragment read (the loop's last barriers): the LDS is free
+    float4* xch = reinterpret_cast<float4*>(smem) + (wp * 64 + lane) * 8;
+    if (wc == 1) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn) xch[mt * 4 + fn] = make_float4(pacc[mt][fn][0], pacc[mt][fn][1], pacc[mt][fn][2], pacc[mt][fn][3]);
+    }
+    __syncthreads();
+    if (wc == 0) {
+      const int M = p.n * p.ho * p.wo;
+      float* __restrict__ part = sf.part + static_cast<int64_t>(co0 / (2 * WCO)) * M * kSegCS;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int cls = 16 * mt + 4 * fq;
+        if (cls >= kSegCS) continue;
+#pragma unroll
+        for (int fn = 0; fn < 4; ++fn) {
+          const float4 o = xch[mt * 4 + fn];
+          const int64_t m = px0 + wp * 64 + fn * 16 + fr;
+          *reinterpret_cast<float4*>(part + m * kSegCS + cls) =
+              make_float4(pacc[mt][fn][0] + o.x, pacc[mt][fn][1] + o.y, pacc[mt][fn][2] + o.z, pacc[mt][fn][3] + o.w);
+        }
+      }
+    }
+    return;
+  }
   if constexpr (K::ESZ == 2) {
     if (fast_epi && !DRNMI_STAG_OLDINIT) store_tile_x4<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
     else store_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
@@ -456,6 +533,15 @@ conv_stag128_x2_kernel(const drnmi_conv_args p) {
   conv_stag_body<uint16_t, true, 64>(p);
 }
 
+struct StagSegArgs {
+  drnmi_conv_args p;
+  SegFuse sf;
+};
+__global__ void __launch_bounds__(512, 1)
+conv_stag_seg_kernel(const StagSegArgs a) {
+  conv_stag_body<uint16_t, false, 128, true>(a.p, a.sf);
+}
+
 // + the fused 1x1 downsample (x2 != NULL; layer5.0 / layer6.0 conv2 of D-22)
 __global__ void __launch_bounds__(512, 1)
 conv_stag_x2_kernel(const drnmi_conv_args p) {
@@ -466,6 +552,23 @@ conv_stag_x2_kernel(const drnmi_conv_args p) {
 
 constexpr int kStagLds = 2 * 256 * 128 + 2 * kStripBytes;     // 2 A stages + 2 strips (130 KB)
 constexpr int kStag128Lds = 2 * 128 * 128 + 2 * kStripBytes;  // 128-channel tile (98 KB)
+
+hipError_t launch_stag_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_pad, float* part, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_stag_seg_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kStagLds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  StagSegArgs a;
+  a.p = p;
+  a.sf = SegFuse{static_cast<const uint16_t*>(seg_w), seg_k_pad, part};
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const dim3 grid(static_cast<unsigned>((M / kBPX) * ((p.cout + 255) / 256)));
+  hipLaunchKernelGGL(conv_stag_seg_kernel, grid, dim3(512), kStagLds, s, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s) {
   static bool attr_set = false;

@@ -30,6 +30,9 @@ const char* x6_conv_name(const drnmi_conv_args& p);
 // The strip tile with staggered SIMD partners (conv_stag.hip): 3x3 stride-1 bf16, wo % 256 == 0,
 // cin % 128 == 0 (conv_big.hip's dispatch checks the shape).
 hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s);
+// conv_stag_kernel with the seg classifier in its epilogue (drnmi_conv_stag_seg): no activation store,
+// partial logits per 256-channel block into part[cout / 256][n ho wo][20].
+hipError_t launch_stag_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_pad, float* part, hipStream_t s);
 // The seg classifier (1x1, cout <= 32, cin % 256 == 0; conv_seg.hip), bit-identical to conv_big's
 // BK-32 tile.
 bool seg_conv_supported(const drnmi_conv_args& p);

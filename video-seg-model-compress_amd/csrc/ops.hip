@@ -270,10 +270,13 @@ up8_lsm_quad_kernel(const float* __restrict__ logits, const float* __restrict__ 
 // NHWC: logits as [n][h][w][cs] fp32 rows (cs % 4 == 0, cs >= NC; the seg conv's labels-only
 // output, one float4 per 4 classes) instead of NC planes; the values and the per-pixel arithmetic
 // are the same, so are the labels.
-template <int NC, int LABEL_DTYPE, bool NHWC = false>
+// SEG2 (with NHWC): `logits` holds two partial-logit planes [2][n h w][cs] (the seg classifier
+// folded into the last conv's epilogue, one partial per 256-channel block) and the logit is
+// (bias + partial 0) + partial 1, in that order.
+template <int NC, int LABEL_DTYPE, bool NHWC = false, bool SEG2 = false>
 __global__ void __launch_bounds__(256)
 up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict__ up_w,
-                      void* __restrict__ labels, int h, int w, int cs = 0) {
+                      void* __restrict__ labels, int h, int w, int cs = 0, const float* __restrict__ bias = nullptr) {
   __shared__ float wk[256];
   wk[threadIdx.x] = up_w[threadIdx.x];
   __syncthreads();
@@ -292,11 +295,17 @@ up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict_
   if constexpr (NHWC) {
     constexpr int NC4 = (NC + 3) / 4;
     const float* src = logits + static_cast<int64_t>(n) * plane * cs;
+    const int64_t half = static_cast<int64_t>(gridDim.z) * plane * cs;   // SEG2: second partial plane
     auto taps = [&](float (&d)[NC], int iy, int ix) {
       const float4* r = reinterpret_cast<const float4*>(src + (static_cast<int64_t>(iy) * w + ix) * cs);
 #pragma unroll
       for (int k4 = 0; k4 < NC4; ++k4) {
-        const float4 v = r[k4];
+        float4 v = r[k4];
+        if constexpr (SEG2) {
+          const float4 v1 = r[k4 + half / 4];
+          v = make_float4((bias[4 * k4] + v.x) + v1.x, (bias[4 * k4 + 1] + v.y) + v1.y, (bias[4 * k4 + 2] + v.z) + v1.z,
+                          (bias[4 * k4 + 3] + v.w) + v1.w);
+        }
         const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -623,6 +632,25 @@ extern "C" int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const floa
     hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_I64, true>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs);
   else
     hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_U8, true>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_up8_labels_seg2(const float* partials, int32_t cs, const float* bias, const float* up_w,
+                                     void* labels, int32_t label_dtype, int32_t n, int32_t c, int32_t h, int32_t w,
+                                     void* stream) {
+  if (partials == nullptr || bias == nullptr || up_w == nullptr || labels == nullptr || n <= 0 || h <= 0 || w <= 0)
+    return DRNMI_EINVAL;
+  if (c != 19) return DRNMI_ENOTSUP;
+  if (cs < 20 || cs % 4 != 0 || (reinterpret_cast<uintptr_t>(partials) & 15) != 0) return DRNMI_EINVAL;
+  if (label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64) return DRNMI_EINVAL;
+  if (h + 1 > 65535 || n > 65535) return DRNMI_EINVAL;
+  const int W = w * 8;
+  dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (label_dtype == DRNMI_I64)
+    hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_I64, true, true>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs, bias);
+  else
+    hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_U8, true, true>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs, bias);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -42,10 +42,6 @@ from .engine import PackedNet, Plan, lower_drnseg
 from .weights import bilinear_up_kernel
 
 # info.json:1 (Cityscapes normalisation used by every reference driver)
-# segment(): the seg conv writes NHWC logits rows and the labels head reads them (Plan.seg_nhwc_args;
-# identical labels); DRNMI_LABELS_NHWC=0 keeps the NCHW logits planes (A/B runs)
-LABELS_NHWC = os.environ.get("DRNMI_LABELS_NHWC", "1") != "0"
-
 INFO_MEAN = (0.29010095242892997, 0.32808144844279574, 0.28696394422942517)
 INFO_STD = (0.1829540508368939, 0.18656561047509476, 0.18447508988480435)
 
@@ -189,8 +185,8 @@ class DRNSeg(nn.Module):
         plan, stream = self._prepare(frames_u8.shape[0], frames_u8.shape[1], frames_u8.shape[2],
                                      frames_u8.device)
         plan.ingest_u8(frames_u8.contiguous(), mean, std, bgr, stream)
-        nhwc = LABELS_NHWC and not self.use_torch_up and plan.seg_nhwc_args is not None
-        plan.run_backbone(stream, self.timing_hook, labels_only=nhwc)
+        path = plan.labels_path(self.use_torch_up)
+        plan.run_backbone(stream, self.timing_hook, labels_only=path != "nchw")
         oh, ow = plan.out_hw
         if labels is None:
             labels = torch.empty(frames_u8.shape[0], oh, ow, dtype=torch.uint8, device=frames_u8.device)
@@ -198,7 +194,9 @@ class DRNSeg(nn.Module):
                 or not labels.is_contiguous() or labels.device != frames_u8.device:
             raise ValueError(f"labels must be a contiguous uint8/int64 [{frames_u8.shape[0]}, {oh}, {ow}] tensor "
                              f"on {frames_u8.device}")
-        if nhwc:
+        if path == "seg2":
+            plan.head_labels_seg2(self._up_plane(plan.packed.device), stream, labels)
+        elif path == "nhwc":
             plan.head_labels_nhwc(self._up_plane(plan.packed.device), stream, labels)
         else:
             self._head(plan, stream, None, labels)

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -557,6 +558,12 @@ def _conv_out(h, k, s, p, d):
     return (h + 2 * p - d * (k - 1) - 1) // s + 1
 
 
+# segment(): NHWC logits rows for the labels head, and the seg classifier folded into the last conv
+# (drnmi_conv_stag_seg); DRNMI_LABELS_NHWC=0 / DRNMI_SEG_FUSE=0 switch them off (A/B runs)
+LABELS_NHWC = os.environ.get("DRNMI_LABELS_NHWC", "1") != "0"
+SEG_FUSE = os.environ.get("DRNMI_SEG_FUSE", "1") != "0"
+
+
 class Plan:
     """Launch plan for one (batch, H, W, precision): shapes, buffers, C-ABI arg structs."""
 
@@ -619,6 +626,7 @@ class Plan:
                         t = self.bufs[v]
                         pool.setdefault((t.numel(), t.dtype), []).append(t)
         self.keep_all = keep_all
+        self._reads_of = reads_of
         self.args = [None if i in self.skip else self._conv_args(nd) for i, nd in enumerate(g.nodes)]
         self.stem_u8 = self._stem_u8_args()
         self.stem_fused = self._stem_fusable(reads_of)
@@ -641,7 +649,7 @@ class Plan:
     SEG_NHWC_CS = 20
 
     def _setup_seg_nhwc(self):
-        self.seg_idx, self.seg_nhwc_args = -1, None
+        self.seg_idx, self.seg_nhwc_args, self.seg_fused = -1, None, None
         nodes = self.packed.graph.nodes
         idx = [i for i, nd in enumerate(nodes) if nd.out_fp32_nchw]
         if len(idx) != 1 or self.args[idx[0]] is None:
@@ -663,6 +671,43 @@ class Plan:
         if name is None or not name.decode().startswith("conv_big_kernel"):
             return
         self.seg_idx, self.seg_nhwc_args = i, a
+        self._setup_seg_fused(i)
+
+    def _setup_seg_fused(self, i: int):
+        """The seg classifier folded into its producer's epilogue (drnmi_conv_stag_seg) when that
+        producer is a 512-channel staggered-tile conv whose output nothing else reads."""
+        self.seg_fused = None
+        if not SEG_FUSE or not self.fuse:
+            return
+        nodes = self.packed.graph.nodes
+        seg = nodes[i]
+        prod = [j for j, nd in enumerate(nodes) if nd.dst == seg.x_val and j not in self.skip]
+        if len(prod) != 1 or seg.x_val != seg.src or seg.r_val or not seg.scale_folded:
+            return
+        j = prod[0]
+        a = self.args[j]
+        if a is None or j in self.block64 or (j - 1) in self.block64 or j <= 2 or self.packed.quant_after.get(j):
+            return
+        if any(nodes[j].dst in self._reads_of[k] for k in range(len(nodes)) if k != i):
+            return
+        if a.cout != 512 or a.scale or a.res or a.x2 or seg.k != a.cout or seg.cout_pad < 32:
+            return
+        name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
+        if name is None or name.decode() != "conv_stag_kernel":
+            return
+        lh, lw = self.shapes[seg.dst]
+        if "seg_part" not in self.bufs:
+            self.bufs["seg_part"] = torch.empty(2 * self.n * lh * lw * self.SEG_NHWC_CS, dtype=torch.float32,
+                                                device=self.packed.device)
+        self.seg_fused = {"conv": j, "seg_w": seg.wpk.data_ptr(), "seg_k_pad": seg.k_pad, "seg_rows": seg.cout_pad,
+                          "bias": seg.shift.data_ptr()}
+
+    def labels_path(self, use_torch_up: bool = False) -> str:
+        """How segment() produces labels on this plan: "seg2" (seg folded into the last conv),
+        "nhwc" (NHWC logits rows) or "nchw" (the logits planes)."""
+        if use_torch_up or not LABELS_NHWC or self.seg_nhwc_args is None:
+            return "nchw"
+        return "seg2" if self.seg_fused is not None else "nhwc"
 
     def _front_fusable(self, reads_of) -> bool:
         """layer0..layer2 run as one drnmi_video_front_u8 launch on the u8 path when the packed net
@@ -773,6 +818,7 @@ class Plan:
         """labels_only: the seg conv writes the NHWC logits for head_labels_nhwc (when the plan has
         that form, seg_nhwc_args); the NCHW logits buffer is then not written."""
         lib = _lib.load()
+        segf = self.seg_fused if labels_only and self.seg_nhwc_args is not None else None
         front = self.src == "u8" and self.front_fused
         fused_stem = self.src == "u8" and self.stem_fused and not front
         nodes = self.packed.graph.nodes
@@ -802,7 +848,18 @@ class Plan:
             if i == 0 and self.src == "u8":
                 a = self.stem_u8
             if labels_only and i == self.seg_idx and self.seg_nhwc_args is not None:
+                if segf is not None:
+                    continue                      # folded into its producer's epilogue
                 a = self.seg_nhwc_args
+            if segf is not None and i == segf["conv"]:
+                if timing_hook is not None:
+                    timing_hook(i, nd, True)
+                _lib.check(lib.drnmi_conv_stag_seg(ctypes.byref(a), segf["seg_w"], segf["seg_k_pad"], segf["seg_rows"],
+                                                   self.bufs["seg_part"].data_ptr(), ctypes.c_void_p(stream)),
+                           f"conv_stag_seg {nd.name}")
+                if timing_hook is not None:
+                    timing_hook(i, nd, False)
+                continue
             if timing_hook is not None:
                 timing_hook(i, nd, True)
             if i == 0 and fused_stem:
@@ -875,6 +932,15 @@ class Plan:
         _lib.check(_lib.load().drnmi_up8_labels_nhwc(
             self.bufs["logits_nhwc"].data_ptr(), self.SEG_NHWC_CS, up_w.data_ptr(), labels.data_ptr(), lab_dtype,
             self.n, 19, lh, lw, ctypes.c_void_p(stream)), "up8_labels_nhwc")
+
+    def head_labels_seg2(self, up_w: torch.Tensor, stream: int, labels: torch.Tensor):
+        """Labels from the partial logits run_backbone(labels_only=True) wrote with the seg folded into
+        the last conv (drnmi_up8_labels_seg2)."""
+        lh, lw = self.shapes["logits"]
+        lab_dtype = _lib.DRNMI_I64 if labels.dtype == torch.int64 else _lib.DRNMI_U8
+        _lib.check(_lib.load().drnmi_up8_labels_seg2(
+            self.bufs["seg_part"].data_ptr(), self.SEG_NHWC_CS, self.seg_fused["bias"], up_w.data_ptr(),
+            labels.data_ptr(), lab_dtype, self.n, 19, lh, lw, ctypes.c_void_p(stream)), "up8_labels_seg2")
 
     def head_bilinear(self, stream: int, logprobs: torch.Tensor | None, labels: torch.Tensor | None):
         """use_torch_up head: UpsamplingBilinear2d(8) + LogSoftmax + argmax (lmodels/drnseg.py:285-287)."""

@@ -106,6 +106,20 @@ def launch_work(plan, video: bool = True):
         mid = plan.n * hb * wb * 64 * esz
         rows[i] = (rows[i][0], rows[i][1] + rows[i + 1][1], rows[i][2] + rows[i + 1][2] - 3 * mid)
         rows[i + 1] = (rows[i + 1][0], 0.0, 0.0)
+    segf = getattr(plan, "seg_fused", None)
+    if video and segf is not None and plan.labels_path() == "seg2":
+        # the seg classifier in the last conv's epilogue (drnmi_conv_stag_seg): the conv's output is
+        # neither written nor read back, nor are the fp32 logits; the two partial-logit planes are
+        # written by it and read by the head instead
+        j, i = segf["conv"], plan.seg_idx
+        oh, ow = plan.shapes[nodes[j].dst]
+        act = plan.n * oh * ow * nodes[j].conv.out_channels * esz
+        lh, lw = plan.shapes[nodes[i].dst]
+        logits = plan.n * lh * lw * nodes[i].conv.out_channels * 4
+        part = 2 * plan.n * lh * lw * plan.SEG_NHWC_CS * 4
+        rows[j] = (rows[j][0], rows[j][1] + rows[i][1], rows[j][2] + rows[i][2] - 2 * act - logits + part)
+        rows[i] = (rows[i][0], 0.0, 0.0)
+        rows[-1] = (rows[-1][0], rows[-1][1], rows[-1][2] - logits + part)
     return rows
 
 
