@@ -57,9 +57,11 @@ def test_block64_pack_and_supported_without_gpu():
     blob = _pack(lib, p)
     # fragment (conv 0, half 0, slice 5 = tap 1 (kh 0, kw 1), cb 1), lane 33 (r 1, h 1), element 2:
     # w1[1][16 + 8 + 2][0][1] * s1[1] in bf16
-    frag = blob[:2 * 2 * 36 * 64 * 16].view(np.uint16).reshape(2, 2, 36, 64, 8)
-    want = (p[0][1, 26, 0, 1] * p[1][1]).bfloat16().view(torch.int16).item() & 0xffff
-    assert int(frag[0, 0, 5, 33, 2]) == want
+    frag = blob[:2 * 2 * 36 * 64 * 16].view(np.uint16).reshape(2, 2, 18, 2, 64, 8)
+    # (conv 0, half 0, chunk 5 = tap 2 (kh 0, kw 2) x channels 32.., row tile 1, lane 33 (fr 1, fq 2),
+    # element 2): w1[16 + 1][32 + 16 + 2][0][2] * s1[17] in bf16
+    want = (p[0][17, 50, 0, 2] * p[1][17]).bfloat16().view(torch.int16).item() & 0xffff
+    assert int(frag[0, 0, 5, 1, 33, 2]) == want
     sh = blob[2 * 2 * 36 * 64 * 16:].view(np.float32)
     np.testing.assert_array_equal(sh[:64], p[2].numpy())
     np.testing.assert_array_equal(sh[64:], p[5].numpy())
