@@ -31,6 +31,9 @@
 #ifndef DRNMI_STAG_WAUX
 #define DRNMI_STAG_WAUX 0   // cache policy of the weight DMA
 #endif
+#ifndef DRNMI_STAG_SERP
+#define DRNMI_STAG_SERP 0   // diagnostic: odd rounds of tiles (blockIdx / 256) walk the tap groups in reverse
+#endif                      // order, so a round starts on the weight slices the previous one ended on (L2)
 #ifndef DRNMI_STAG_PRIO
 #define DRNMI_STAG_PRIO 0   // diagnostic: s_setprio 1 for the lagging half (waves 4-7)
 #endif
@@ -164,7 +167,9 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
   constexpr uint32_t kOOB = 0x80000000u;             // beyond every buffer (sizes < 2^31)
 
   // weight piece i (rows (wave*4 + i)*8 .. +8) of K step kt into A stage `stage`
+  const bool serp = DRNMI_STAG_SERP != 0 && ((blockIdx.x >> 8) & 1) != 0;
   auto issue_a = [&](int kt, int stage, int i) {
+    if (serp && kt < nk) kt = 3 * (ngroups - 1 - kt / 3) + kt % 3;
     const int cb = kt / 9;
     const int tap = kt - cb * 9;
     const int k0 = (X2 && kt >= nk) ? 9 * cin + (kt - nk) * BK : (tap << lc) + cb * BK;
@@ -172,6 +177,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
   };
   // strip share sh of group g (channel block g / 3, tap row g % 3) into strip buffer `buf`
   auto issue_strip = [&](int g, int buf, int sh) {
+    if (serp) g = ngroups - 1 - g;
     const int j = wave + 8 * sh;
     if (j >= kStripPieces) return;                   // wave-uniform
     const int R = j * 8 + lrow;
