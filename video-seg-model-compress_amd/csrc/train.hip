@@ -124,6 +124,10 @@ pack_batched_kernel(const int64_t* __restrict__ tab, int n, int64_t total) {
 // grid = (G splits, C / (4 * TPR) channel chunks).  Partials ws[2][G][C] (S1, S2).
 enum { RED_STATS = 0, RED_BNBWD = 1, RED_SUM = 2 };
 
+#ifndef DRNMI_RED_BATCH
+#define DRNMI_RED_BATCH 4    // column-reduction rows loaded ahead per thread (1: one load in flight)
+#endif
+
 struct RedArgs {
   const float* a;       // STATS: y ; BNBWD: dz ; SUM: x
   const float* z;       // BNBWD: z (relu mask), or NULL
@@ -147,7 +151,50 @@ __global__ void __launch_bounds__(kThreads) colred_kernel(const RedArgs r) {
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * r.rows_per_split;
   const int64_t r1 = (r0 + r.rows_per_split) < r.rows ? (r0 + r.rows_per_split) : r.rows;
   double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
-  for (int64_t row = r0 + tr; row < r1; row += rg) {
+  // DRNMI_RED_BATCH rows' loads go out before their (in-order) fp64 accumulation: the same sums,
+  // with that many loads in flight per thread instead of one
+  constexpr int RB = DRNMI_RED_BATCH;
+  int64_t row = r0 + tr;
+  for (; row + (RB - 1) * rg < r1; row += RB * rg) {
+    float4 av[RB], zv[RB], yv[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int64_t off = (row + u * rg) * r.C + c0;
+      av[u] = *reinterpret_cast<const float4*>(r.a + off);
+      if constexpr (MODE == RED_BNBWD) {
+        if (r.relu) zv[u] = *reinterpret_cast<const float4*>(r.z + off);
+        yv[u] = *reinterpret_cast<const float4*>(r.y + off);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      float a[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+      if constexpr (MODE == RED_STATS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s1[j] += a[j];
+          s2[j] += static_cast<double>(a[j]) * a[j];
+        }
+      } else if constexpr (MODE == RED_BNBWD) {
+        if (r.relu) {
+          a[0] = zv[u].x > 0.f ? a[0] : 0.f;
+          a[1] = zv[u].y > 0.f ? a[1] : 0.f;
+          a[2] = zv[u].z > 0.f ? a[2] : 0.f;
+          a[3] = zv[u].w > 0.f ? a[3] : 0.f;
+        }
+        const float y[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s1[j] += a[j];
+          s2[j] += static_cast<double>(a[j]) * y[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s1[j] += a[j];
+      }
+    }
+  }
+  for (; row < r1; row += rg) {
     const int64_t off = row * r.C + c0;
     const float4 av = *reinterpret_cast<const float4*>(r.a + off);
     float a[4] = {av.x, av.y, av.z, av.w};
