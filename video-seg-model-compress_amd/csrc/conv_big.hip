@@ -764,6 +764,7 @@ constexpr int kStag = 15;   // conv_stag_kernel (tile id 19): the strip tile wit
 constexpr int kSeg = 16;    // conv_seg_kernel (tile id 20): the seg classifier, 1x1 to <= 32 classes
 constexpr int kS2Row = 17;  // conv_s2row_kernel (tile id 21): stride-2 3x3 32 -> 64 / 64 -> 128, row walk
 constexpr int kS1X2Row = 18;  // conv_s1x2row_kernel (tile id 22): stride-1 3x3 64 -> 64 + 1x1 s2 downsample 32 -> 64
+constexpr int kRow128 = 19;   // conv_row128_kernel (tile id 23): stride-1 3x3 128 -> 128 (+ residual), row walk
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // the seg classifier (1x1, cout <= 32) stays on conv_big's BK-32 tile by default: conv_seg_kernel
@@ -1007,6 +1008,7 @@ bool big_conv_supported(const drnmi_conv_args& p) {
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   if (variant == kS2Row || (variant < 0 && s2row_auto(p))) return s2row_conv_dispatch(p, s);
   if (variant == kS1X2Row || (variant < 0 && s1x2row_auto(p))) return s1x2row_conv_dispatch(p, s);
+  if (variant == kRow128 || (variant < 0 && row128_auto(p))) return row128_conv_dispatch(p, s);
   if (variant == kSeg || (variant < 0 && seg_enabled() && seg_conv_supported(p))) return seg_conv_dispatch(p, s);
   // the halo kernel (cin/cout 64-128) stays dense: it beats unit skipping on those shapes
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_dispatch(p, s);
@@ -1056,6 +1058,7 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   if (variant == kS2Row || (variant < 0 && s2row_auto(p))) return s2row_conv_name(p);
   if (variant == kS1X2Row || (variant < 0 && s1x2row_auto(p))) return s1x2row_conv_name(p);
+  if (variant == kRow128 || (variant < 0 && row128_auto(p))) return row128_conv_name(p);
   if (variant == kSeg || (variant < 0 && seg_enabled() && seg_conv_supported(p)))
     return seg_conv_supported(p) ? "conv_seg_kernel" : nullptr;
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_name(p);

@@ -49,4 +49,9 @@ bool s1x2row_conv_supported(const drnmi_conv_args& p);
 bool s1x2row_auto(const drnmi_conv_args& p);
 int s1x2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
 const char* s1x2row_conv_name(const drnmi_conv_args& p);
+// Row-walking stride-1 3x3 128 -> 128 (+ residual) with K split over wave pairs (conv_row128.hip).
+bool row128_conv_supported(const drnmi_conv_args& p);
+bool row128_auto(const drnmi_conv_args& p);
+int row128_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
+const char* row128_conv_name(const drnmi_conv_args& p);
 }  // namespace drnmi
