@@ -110,3 +110,24 @@ def test_segment_seg_fused_into_last_conv(n):
     agree = (got == ref).float().mean().item()
     print(f"seg-fused labels agreement {agree:.6f}, logits max |diff| {err:.3e}")
     assert agree >= 0.9995
+
+
+def test_segment_labels_nhwc_identical_int8():
+    """int8 nets (C5): the int8 seg conv writes the same fp32 values as NHWC rows (store_tile_i8's
+    16-B path) -- labels identical to the NCHW-planes head."""
+    m = drnseg.build("drn_d_22", 19, seed=5, device=torch.device(DEV))
+    g = torch.Generator(device=DEV).manual_seed(11)
+    frames = torch.randint(0, 256, (2, 128, 256, 3), dtype=torch.uint8, device=DEV, generator=g)
+    m.calibrate_int8(frames)
+    m.set_precision("int8")
+    old = engine.LABELS_NHWC
+    try:
+        engine.LABELS_NHWC = False
+        ref = m.segment(frames, INFO_MEAN, INFO_STD, False).clone()
+        engine.LABELS_NHWC = True
+        got = m.segment(frames, INFO_MEAN, INFO_STD, False)
+        plans = [p for k, p in m._plans.items() if k[0] == "int8"]
+        assert plans and all(p.labels_path() == "nhwc" for p in plans), "the int8 plan must take the NHWC logits path"
+    finally:
+        engine.LABELS_NHWC = old
+    assert torch.equal(ref, got)

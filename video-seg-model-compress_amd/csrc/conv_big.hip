@@ -829,9 +829,24 @@ constexpr I8Variant kI8Variants[] = {
     {128, "conv_i8_kernel<3, 128, 1, 4, 64>", "conv_i8_kernel<1, 128, 1, 4, 64>"},
 };
 
+// DRNMI_I8_V1 / DRNMI_I8_V3 = 0..3: force the 1x1 / 3x3 tile variant where it fits (A/B runs;
+// every variant accumulates in int32 and shares store_tile_i8, so the outputs are identical)
+static int i8_variant_override(int ks) {
+  static int ov[2] = {-2, -2};
+  int& o = ov[ks == 3 ? 1 : 0];
+  if (o == -2) {
+    const char* e = getenv(ks == 3 ? "DRNMI_I8_V3" : "DRNMI_I8_V1");
+    o = (e != nullptr && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : -1;
+  }
+  return o;
+}
+
 int i8_variant(const drnmi_conv_args& p) {
   const int wide = p.cout % 256 == 0 ? 0 : 1;
-  return (p.cin >= 128 ? 0 : 2) + wide;
+  const int v = (p.cin >= 128 ? 0 : 2) + wide;
+  const int o = i8_variant_override(p.ks);
+  if (o >= 0 && (o >= 2 || p.cin % 128 == 0) && p.cout_pad % kI8Variants[o].bco == 0) return o;
+  return v;
 }
 
 template <int KS>

@@ -424,6 +424,10 @@ __device__ __forceinline__ void store_tile_i8(const drnmi_conv_args& p, const i3
             y[ybase + static_cast<int64_t>(co + j) * p.y_sc] = static_cast<int8_t>((o >> (8 * j)) & 0xff);
           }
         }
+      } else if (p.out_dtype == DRNMI_F32 && p.y_sc == 1 && (p.y_sp & 3) == 0 && co + 4 <= p.y_sp) {
+        // fp32 NHWC rows padded to y_sp (the labels head's logits, SEG_NHWC_CS): one 16-B store;
+        // the pad channels cout .. y_sp hold scale/shift padding values nobody reads
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.y) + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

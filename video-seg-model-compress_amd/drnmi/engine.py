@@ -636,8 +636,9 @@ class Plan:
         self.block64 = {}
         lib = _lib.load()
         for i in getattr(packed, "block64_pairs", []):
+            # (int8 nets: the block output's int8 copy for layer4 is quantised after the launch)
             if self.fuse and not any(g.nodes[i].dst in reads_of[j] for j in range(len(g.nodes)) if j != i + 1) and \
-                    not packed.quant_after.get(i) and not packed.quant_after.get(i + 1) and \
+                    not packed.quant_after.get(i) and \
                     lib.drnmi_block64_supported(n, *self.shapes[g.nodes[i].dst]):
                 self.block64[i] = packed.block64_pack(i)
         self._setup_seg_nhwc()
@@ -645,7 +646,8 @@ class Plan:
 
     # labels-only video path: the seg conv writes fp32 NHWC rows of SEG_NHWC_CS floats (16-B
     # stores instead of 19 strided planes) and drnmi_up8_labels_nhwc reads them; same values,
-    # same labels.  Only where the seg conv runs on conv_big (bf16 input) and the 19-class head.
+    # same labels.  Only where the seg conv runs on conv_big (bf16 input) or on the int8 tile
+    # (int8 nets: store_tile_i8's 16-B fp32 rows) and the 19-class head.
     SEG_NHWC_CS = 20
 
     def _setup_seg_nhwc(self):
@@ -668,7 +670,7 @@ class Plan:
         a.y = self.bufs["logits_nhwc"].data_ptr()
         a.y_sn, a.y_sp, a.y_sc = lh * lw * cs, cs, 1
         name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
-        if name is None or not name.decode().startswith("conv_big_kernel"):
+        if name is None or not name.decode().startswith(("conv_big_kernel", "conv_i8_kernel")):
             return
         self.seg_idx, self.seg_nhwc_args = i, a
         self._setup_seg_fused(i)
@@ -835,6 +837,8 @@ class Plan:
                                                    ctypes.c_void_p(stream)), f"basic_block64 {nd.name}")
                 if timing_hook is not None:
                     timing_hook(i, nd, False)
+                for v in self.packed.quant_after.get(i + 1, ()):
+                    self._quantize(lib, v, stream)
                 continue
             if front and i == 0:
                 if timing_hook is not None:
