@@ -42,6 +42,11 @@ TORCH_OF_CODE = {_lib.DRNMI_F32: torch.float32, _lib.DRNMI_BF16: torch.bfloat16,
 # (conv_i8_kernel: K steps of 64/128 int8 channels); the full-resolution small-channel layers
 # (stem, layer1-3: ~5 % of D-22's FLOPs) stay bf16.
 INT8_MIN_CIN = 64
+# ... and whose output has at least this many channels.  256: D-22's 128-channel layer4 stays on
+# the bf16 row / staggered kernels (s2row, stag128 with the downsample folded in), which beat the
+# int8 tiles there (cin 128 gives the int8 staggered tile an odd tap-group count): 1786-1788 vs
+# 1750-1755 fps interleaved (profiles/r6_int8_fusions); DRNMI_INT8_MIN_COUT=128 restores it.
+INT8_MIN_COUT = int(os.environ.get("DRNMI_INT8_MIN_COUT", "256"))
 
 # (cin_stride, cout, ks, stride, dil) served by the LDS-patch kernel (bf16 only; include/drnmi.h)
 # (32 -> 64 stride 2 runs faster on the K-32 LDS-DMA implicit GEMM: 67 vs 108 us per 4 frames)
@@ -216,7 +221,7 @@ class PackedNet:
         # the bf16 halo kernel)
         elig = {i for i, nd in enumerate(g.nodes)
                 if self.cstride[nd.src] >= INT8_MIN_CIN and nd.conv.kernel_size[0] in (1, 3)
-                and (nd.conv.out_channels >= 128 or nd.out_fp32_nchw)}
+                and (nd.conv.out_channels >= INT8_MIN_COUT or nd.out_fp32_nchw)}
         readers = {}
         for i, nd in enumerate(g.nodes):
             for v in (nd.src, nd.res):
