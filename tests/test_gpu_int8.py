@@ -57,6 +57,8 @@ CONV_CASES = [
     (1, 16, 16, 64, 128, 1, 2, 0, 1, False, "i8"),      # 1x1 stride-2 downsample
     (1, 12, 20, 512, 512, 3, 1, 4, 4, False, "bf16"),   # dilation 4, bf16 out
     (1, 10, 10, 512, 19, 1, 1, 0, 1, False, "f32"),     # seg head: cout 19, fp32 NCHW logits
+    (2, 32, 64, 256, 512, 1, 1, 0, 1, False, "i8"),     # layer6.0 downsample shape (occ2 1x1 tile)
+    (1, 9, 17, 128, 256, 1, 1, 0, 1, True, "bf16"),     # ragged 1x1 with a residual
     (1, 8, 8, 256, 256, 3, 1, 1, 1, True, "f32"),
     # whole 256-pixel output rows: the strip-staged int8 kernels (cin % 256 == 0: the staggered
     # conv_i8_stag_kernel; cin 128: conv_i8_strip_kernel)
@@ -108,7 +110,9 @@ def test_conv_i8_matches_oracle(case):
     name = lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
     strip = wo % 256 == 0 and ks == 3 and st == 1 and cin >= 128 and cout % 256 == 0
     assert name.startswith(("conv_i8_stag_kernel" if cin % 256 == 0 else "conv_i8_strip_kernel") if strip
-                           else "conv_i8_kernel<"), name
+                           else ("conv_i8_kernel<", "conv_i8_occ2_kernel<")), name
+    if ks == 1:   # 1x1 launches take the two-workgroups-per-CU tile
+        assert name.startswith("conv_i8_occ2_kernel<"), name
     L.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), _stream()), "conv i8")
     torch.cuda.synchronize()
     ref = Q.conv_i8(x, wpk, scale, shift, cout, ks, st, pad, dil, bool(a.relu), res, res_scale,

@@ -430,6 +430,15 @@ conv_i8_kernel(const drnmi_conv_args p) {
   conv_big_body<int8_t, KS, WCO, WC, NST, BK, false, 4, false>(p);
 }
 
+// the same body at two workgroups per CU (register budget 256, 2 x 24 KB of LDS with 64-B rows):
+// the 1x1 launches have 1-2 K steps per tile, so one resident tile per CU leaves its loads and
+// stores serialised tile after tile; a second tile overlaps them
+template <int KS, int WCO, int WC, int NST, int BK>
+__global__ void __launch_bounds__(64 * 4 * WC, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
+conv_i8_occ2_kernel(const drnmi_conv_args p) {
+  conv_big_body<int8_t, KS, WCO, WC, NST, BK, false, 4, false>(p);
+}
+
 // --- Ping-pong 256 x 256 schedule (variant "pp256").
 //
 // Same tile, LDS image and fragment layout as conv_big_kernel<KS, 128, 2, 2, 64>, but each
@@ -798,20 +807,26 @@ hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
   }
 }
 
-template <int KS, int WCO, int WC, int NST, int BK>
+template <int KS, int WCO, int WC, int NST, int BK, bool OCC2 = false>
 hipError_t launch_i8(const drnmi_conv_args& p, hipStream_t s) {
   using C = BigCfg<WCO, WC, NST, BK, 4, 1>;
+  const void* f;
+  if constexpr (OCC2) f = reinterpret_cast<const void*>(&conv_i8_occ2_kernel<KS, WCO, WC, NST, BK>);
+  else f = reinterpret_cast<const void*>(&conv_i8_kernel<KS, WCO, WC, NST, BK>);
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_i8_kernel<KS, WCO, WC, NST, BK>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const int64_t blocks = ((M + kBPX - 1) / kBPX) * ((p.cout + C::BCO - 1) / C::BCO);
-  hipLaunchKernelGGL((conv_i8_kernel<KS, WCO, WC, NST, BK>), dim3(static_cast<unsigned>(blocks)), dim3(C::THREADS),
-                     C::LDS, s, p);
+  if constexpr (OCC2)
+    hipLaunchKernelGGL((conv_i8_occ2_kernel<KS, WCO, WC, NST, BK>), dim3(static_cast<unsigned>(blocks)), dim3(C::THREADS),
+                       C::LDS, s, p);
+  else
+    hipLaunchKernelGGL((conv_i8_kernel<KS, WCO, WC, NST, BK>), dim3(static_cast<unsigned>(blocks)), dim3(C::THREADS),
+                       C::LDS, s, p);
   return hipGetLastError();
 }
 
@@ -827,23 +842,27 @@ constexpr I8Variant kI8Variants[] = {
     {128, "conv_i8_kernel<3, 128, 1, 3, 128>", "conv_i8_kernel<1, 128, 1, 3, 128>"},
     {256, "conv_i8_kernel<3, 128, 2, 4, 64>", "conv_i8_kernel<1, 128, 2, 4, 64>"},
     {128, "conv_i8_kernel<3, 128, 1, 4, 64>", "conv_i8_kernel<1, 128, 1, 4, 64>"},
+    {128, "conv_i8_occ2_kernel<3, 128, 1, 2, 64>", "conv_i8_occ2_kernel<1, 128, 1, 2, 64>"},
 };
+constexpr int kI8Occ2 = 4;   // 128 x 256 / 64-B rows, 2 stages, two workgroups per CU
 
-// DRNMI_I8_V1 / DRNMI_I8_V3 = 0..3: force the 1x1 / 3x3 tile variant where it fits (A/B runs;
+// DRNMI_I8_V1 / DRNMI_I8_V3 = 0..4: force the 1x1 / 3x3 tile variant where it fits (A/B runs;
 // every variant accumulates in int32 and shares store_tile_i8, so the outputs are identical)
 static int i8_variant_override(int ks) {
   static int ov[2] = {-2, -2};
   int& o = ov[ks == 3 ? 1 : 0];
   if (o == -2) {
     const char* e = getenv(ks == 3 ? "DRNMI_I8_V3" : "DRNMI_I8_V1");
-    o = (e != nullptr && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : -1;
+    o = (e != nullptr && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : -1;
   }
   return o;
 }
 
 int i8_variant(const drnmi_conv_args& p) {
   const int wide = p.cout % 256 == 0 ? 0 : 1;
-  const int v = (p.cin >= 128 ? 0 : 2) + wide;
+  // 1x1: the two-workgroups-per-CU tile (71.6-73.5 vs 86.7-86.9 us for layer5.0 / layer6.0's
+  // downsample, 65.6-67.0 for the seg conv: profiles/r6_int8_fusions/occ2_ab.txt)
+  const int v = p.ks == 1 && p.cout_pad % kI8Variants[kI8Occ2].bco == 0 ? kI8Occ2 : (p.cin >= 128 ? 0 : 2) + wide;
   const int o = i8_variant_override(p.ks);
   if (o >= 0 && (o >= 2 || p.cin % 128 == 0) && p.cout_pad % kI8Variants[o].bco == 0) return o;
   return v;
@@ -856,6 +875,7 @@ hipError_t launch_i8_variant(const drnmi_conv_args& p, int v, hipStream_t s) {
     case 1: return launch_i8<KS, 128, 1, 3, 128>(p, s);   // 3 x 48 KB
     case 2: return launch_i8<KS, 128, 2, 4, 64>(p, s);    // 4 x 32 KB
     case 3: return launch_i8<KS, 128, 1, 4, 64>(p, s);    // 4 x 24 KB
+    case kI8Occ2: return launch_i8<KS, 128, 1, 2, 64, true>(p, s);   // 2 x 24 KB, 2 WGs / CU
     default: return hipErrorInvalidValue;
   }
 }

@@ -675,7 +675,7 @@ class Plan:
         a.y = self.bufs["logits_nhwc"].data_ptr()
         a.y_sn, a.y_sp, a.y_sc = lh * lw * cs, cs, 1
         name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
-        if name is None or not name.decode().startswith(("conv_big_kernel", "conv_i8_kernel")):
+        if name is None or not name.decode().startswith(("conv_big_kernel", "conv_i8_kernel", "conv_i8_occ2_kernel")):
             return
         self.seg_idx, self.seg_nhwc_args = i, a
         self._setup_seg_fused(i)
