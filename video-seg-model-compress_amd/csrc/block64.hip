@@ -42,6 +42,9 @@ constexpr int kTSlot = kTW * kRowB;    // 8192
 constexpr int kTRing = 4;
 constexpr int kTBase = kXRing * kXSlot;                  // 46080
 constexpr int kLds = kTBase + kTRing * kTSlot + 512;     // + slack: conv2 reads t pixels 64, 65 (unstored columns); two workgroups per CU
+#ifndef DRNMI_B64_LATEPIN
+#define DRNMI_B64_LATEPIN 1    // pin the weights after the first ring fill is issued (0: before)
+#endif
 #ifndef DRNMI_B64_PF
 #define DRNMI_B64_PF 4         // B fragment reads in flight ahead of their MFMAs
 #endif
@@ -91,9 +94,14 @@ block64_kernel(const BlockParams a) {
     // serial L2 round trips before the first step)
 #pragma unroll
     for (int s = 0; s < kSlices; ++s) wf[s] = pk[s * 64];
+  }
+  // the pins wait for every weight load: with DRNMI_B64_LATEPIN they follow the first segment's
+  // ring-fill DMA, so the two latencies overlap (conv_s2row.hip, scripts/s2row_stamps.py)
+  auto pin_weights = [&]() {
 #pragma unroll
     for (int s = 0; s < kSlices; ++s) asm volatile("" : "+a"(wf[s]));
-  }
+  };
+  if constexpr (!DRNMI_B64_LATEPIN) pin_weights();
   // accumulator start: the conv's shift for the 16 D rows this lane holds
   f32x4 cinit[2];
   {
@@ -130,33 +138,40 @@ block64_kernel(const BlockParams a) {
 
   int idx = blockIdx.x * a.per_wg;
   const int end = min(idx + a.per_wg, a.total);
-  while (idx < end) {
-    const int seg = idx / H;
-    const int ya = idx - seg * H;
-    const int yb = min(H, ya + (end - idx));
-    idx += yb - ya;
-    const int n = seg / a.strips, s = seg - n * a.strips;
-    const int c0 = kOW * s;                            // first output column of the strip
-    const int img0 = n * H;
-
-    // x row DMA (all four waves: instruction i = wave + 4 k of the row's 9)
-    auto x_dma = [&](int row) {
-      const int slot = ((row % kXRing) + kXRing) % kXRing;
-      const bool row_ok = static_cast<unsigned>(row) < static_cast<unsigned>(H);
+  int ya = 0, yb = 0, n = 0, c0 = 0, img0 = 0;
+  // x row DMA (all four waves: instruction i = wave + 4 k of the row's 9)
+  auto x_dma = [&](int row) {
+    const int slot = ((row % kXRing) + kXRing) % kXRing;
+    const bool row_ok = static_cast<unsigned>(row) < static_cast<unsigned>(H);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int i = wave + 4 * k;
-        if (i >= kXPieces) break;                      // wave-uniform
-        const int byte = i * 1024 + lane * 16;
-        const int p = byte >> 7, sl = (byte >> 4) & 7;
-        const int col = c0 - 2 + p;
-        const bool ok = row_ok && p < kXW && static_cast<unsigned>(col) < static_cast<unsigned>(W);
-        const unsigned off = ok ? static_cast<unsigned>(((img0 + row) * W + col) * kRowB + ((sl ^ bswz(p)) << 4)) : kOob;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xs, (lds_t*)(smem + slot * kXSlot + i * 1024), 16, off, 0, 0, 0);
-      }
-    };
-    // prologue: x rows ya-2 .. ya (steps start at j = ya - 1; step j issues row j + 2)
+    for (int k = 0; k < 3; ++k) {
+      const int i = wave + 4 * k;
+      if (i >= kXPieces) break;                        // wave-uniform
+      const int byte = i * 1024 + lane * 16;
+      const int p = byte >> 7, sl = (byte >> 4) & 7;
+      const int col = c0 - 2 + p;
+      const bool ok = row_ok && p < kXW && static_cast<unsigned>(col) < static_cast<unsigned>(W);
+      const unsigned off = ok ? static_cast<unsigned>(((img0 + row) * W + col) * kRowB + ((sl ^ bswz(p)) << 4)) : kOob;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xs, (lds_t*)(smem + slot * kXSlot + i * 1024), 16, off, 0, 0, 0);
+    }
+  };
+  // next segment: its state and its prologue, x rows ya-2 .. ya (steps start at j = ya - 1; step
+  // j issues row j + 2)
+  auto begin_segment = [&]() {
+    const int seg = idx / H;
+    ya = idx - seg * H;
+    yb = min(H, ya + (end - idx));
+    idx += yb - ya;
+    n = seg / a.strips;
+    const int s = seg - n * a.strips;
+    c0 = kOW * s;                                      // first output column of the strip
+    img0 = n * H;
     for (int row = ya - 2; row <= ya; ++row) x_dma(row);
+  };
+  bool more = idx < end;
+  if (more) begin_segment();
+  if constexpr (DRNMI_B64_LATEPIN) pin_weights();   // waits for the weights only: the fill stays in flight
+  while (more) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 
@@ -244,6 +259,8 @@ block64_kernel(const BlockParams a) {
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    more = idx < end;
+    if (more) begin_segment();
   }
 }
 

@@ -33,6 +33,25 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef DRNMI_S2_ABL
 #define DRNMI_S2_ABL 0         // diagnostic builds only: bit 0 drops the MFMAs, bit 1 the in-loop DMA,
 #endif                         // bit 2 the output stores, bit 3 the fragment reads, bit 4 the step barrier
+#ifndef DRNMI_S2_LATEPIN
+#define DRNMI_S2_LATEPIN 1     // pin the weights into AGPRs after the first ring fill is issued (0: before)
+#endif
+#ifndef DRNMI_S2_STAMP
+#define DRNMI_S2_STAMP 0       // diagnostic builds only: per-workgroup clock stamps (drnmi_diag_s2_stamps)
+#endif
+#if DRNMI_S2_STAMP
+constexpr int kStampWgs = 8192;
+__device__ unsigned long long g_s2_stamp[kStampWgs * 8];
+// lanes 0..7 of wave 0 store one value each (per-lane addresses: plain vector stores)
+__device__ __forceinline__ void s2_stamp_store(const unsigned long long (&v)[8]) {
+  if (threadIdx.x < 8 && blockIdx.x < kStampWgs) {
+    unsigned long long x = v[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) x = threadIdx.x == static_cast<unsigned>(i) ? v[i] : x;
+    g_s2_stamp[blockIdx.x * 8 + threadIdx.x] = x;
+  }
+}
+#endif
 #ifndef DRNMI_S2_RING32
 #define DRNMI_S2_RING32 7      // input-row slots for cin 32: 3 in use + 2 per step of DMA lead
 #endif
@@ -106,6 +125,9 @@ template <int CIN, int RING, int WGS>
 __global__ void __launch_bounds__(256, WGS) __attribute__((amdgpu_waves_per_eu(WGS, WGS)))
 conv_s2row_kernel(const S2Params a) {
   using C = S2Cfg<CIN>;
+#if DRNMI_S2_STAMP
+  unsigned long long stamp[8] = {__builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0};
+#endif
   constexpr int D = (RING - 3) / 2;                  // steps of DMA lead
   static_assert(RING == 3 + 2 * D && D >= 1 && D <= 2, "ring");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -123,10 +145,16 @@ conv_s2row_kernel(const S2Params a) {
     for (int fm = 0; fm < 2; ++fm)
       wf[ks][fm] = *reinterpret_cast<const u32x4_t*>(a.wgt + static_cast<int64_t>(32 * wc + 16 * fm + fr) * a.k_pad +
                                                      32 * ks + 8 * fq);
+  // the AGPR pins wait for every weight load: with DRNMI_S2_LATEPIN they come after the first
+  // segment's ring-fill DMA is issued, so the weight and input-row latencies overlap (stamps:
+  // the fill was 12.2 us of a 40 us workgroup with the pins first, scripts/s2row_stamps.py)
+  auto pin_weights = [&]() {
 #pragma unroll
-  for (int ks = 0; ks < C::NKS; ++ks)
+    for (int ks = 0; ks < C::NKS; ++ks)
 #pragma unroll
-    for (int fm = 0; fm < 2; ++fm) asm volatile("" : "+a"(wf[ks][fm]));
+      for (int fm = 0; fm < 2; ++fm) asm volatile("" : "+a"(wf[ks][fm]));
+  };
+  if constexpr (!DRNMI_S2_LATEPIN) pin_weights();
   f32x4 cinit[2];
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm) {
@@ -151,22 +179,41 @@ conv_s2row_kernel(const S2Params a) {
         boff[fn][kw][sb] = static_cast<uint32_t>(s2_lds<CIN>(2 * (32 * wp + 16 * fn + fr) + kw, 4 * sb + fq));
   int idx = blockIdx.x * a.per_wg;
   const int end = min(idx + a.per_wg, a.total);
-  while (idx < end) {
+  // segment state (a run of output rows ya .. yb - 1 of one strip of one image)
+  int ya = 0, yb = 0, n = 0, ow0 = 0, img0 = 0;
+  uint32_t vo[5];
+  const int rowb = W * C::PB;                          // bytes per image row
+  auto piece = [&](int k, int r0, int slot0) {         // piece k of rows (r0, r0 + 1); slot0 = slot of r0
+    const int i = wave + 4 * k;
+    const int dr = i >= kPieces ? 1 : 0;
+    const int row = r0 + dr;
+    int slot = slot0 + dr;
+    slot = slot >= RING ? slot - RING : slot;
+    const bool row_ok = static_cast<unsigned>(row) < static_cast<unsigned>(H) && i < 2 * kPieces;
+    // wave-uniform by construction; readfirstlane keeps them in SGPRs (a VGPR soffset would
+    // make the compiler wrap the load in a waterfall loop)
+    const int soff = __builtin_amdgcn_readfirstlane(row_ok ? (img0 + row) * rowb : 0);
+    const int dst = __builtin_amdgcn_readfirstlane(i < 2 * kPieces ? slot * kSlotB + (i - dr * kPieces) * 1024 : RING * kSlotB);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(xs, (lds_t*)(smem + dst), 16, row_ok ? vo[k] : kOob, soff, 0, 0);
+  };
+  auto mod_ring = [](int r) { return ((r % RING) + RING) % RING; };
+  // next segment: its state and its ring fill, rows 2 ya - 1 .. 2 ya + 2 D (step ya re-issues
+  // 2 ya + 2 D: same bytes, no reader yet)
+  auto begin_segment = [&]() {
     const int seg = idx / a.ho;
-    const int ya = idx - seg * a.ho;
-    const int yb = min(a.ho, ya + (end - idx));
+    ya = idx - seg * a.ho;
+    yb = min(a.ho, ya + (end - idx));
     idx += yb - ya;
-    const int n = seg / a.strips, s = seg - n * a.strips;
-    const int ow0 = C::OWS * s;
+    n = seg / a.strips;
+    const int s = seg - n * a.strips;
+    ow0 = C::OWS * s;
     const int col0 = 2 * ow0 - 1;                      // image column of strip pixel 0
-    const int img0 = n * H;
-
+    img0 = n * H;
     // the 18 DMA pieces of input rows (r0, r0 + 1): wave w issues pieces i = w + 4 k, k < 5 (row
     // i / 9, 1-KB piece i % 9 of its slot); the lane's (pixel, chunk) and the strip/image column
     // test depend only on (k, lane), so the per-step work is a scalar row offset and one select.
     // Waves 2, 3 have no piece 4 (i >= 18): theirs is an all-OOB load into the slack KB after
     // the ring (zeros nobody needs), so every wave issues 5 and the vmcnt counts are uniform.
-    uint32_t vo[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int i = wave + 4 * k;
@@ -179,28 +226,21 @@ conv_s2row_kernel(const S2Params a) {
       vo[k] = i < 2 * kPieces && pp < C::XW && static_cast<unsigned>(col) < static_cast<unsigned>(W)
                   ? static_cast<unsigned>(col * C::PB + c * 16) : kOob;
     }
-    const int rowb = W * C::PB;                        // bytes per image row
-    auto piece = [&](int k, int r0, int slot0) {       // piece k of rows (r0, r0 + 1); slot0 = slot of r0
-      const int i = wave + 4 * k;
-      const int dr = i >= kPieces ? 1 : 0;
-      const int row = r0 + dr;
-      int slot = slot0 + dr;
-      slot = slot >= RING ? slot - RING : slot;
-      const bool row_ok = static_cast<unsigned>(row) < static_cast<unsigned>(H) && i < 2 * kPieces;
-      // wave-uniform by construction; readfirstlane keeps them in SGPRs (a VGPR soffset would
-      // make the compiler wrap the load in a waterfall loop)
-      const int soff = __builtin_amdgcn_readfirstlane(row_ok ? (img0 + row) * rowb : 0);
-      const int dst = __builtin_amdgcn_readfirstlane(i < 2 * kPieces ? slot * kSlotB + (i - dr * kPieces) * 1024 : RING * kSlotB);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xs, (lds_t*)(smem + dst), 16, row_ok ? vo[k] : kOob, soff, 0, 0);
-    };
-    auto mod_ring = [](int r) { return ((r % RING) + RING) % RING; };
-    // prologue: rows 2 ya - 1 .. 2 ya + 2 D (step ya re-issues 2 ya + 2 D: same bytes, no reader yet)
 #pragma unroll
     for (int r = 0; r <= D; ++r)
 #pragma unroll
       for (int k = 0; k < 5; ++k) piece(k, 2 * ya - 1 + 2 * r, mod_ring(2 * ya - 1 + 2 * r));
+  };
+  bool more = idx < end;
+  if (more) begin_segment();
+  if constexpr (DRNMI_S2_LATEPIN) pin_weights();   // waits for the weights only: the fill stays in flight
+  while (more) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#if DRNMI_S2_STAMP
+    if (stamp[2] == 0) stamp[2] = __builtin_amdgcn_s_memtime();   // weights + first ring landed
+    stamp[5] += yb - ya;                                            // rows walked
+#endif
 
     int s_lo = mod_ring(2 * ya - 1);                   // slot of row 2 oh - 1
     int s_dma = mod_ring(2 * ya + 2 * D);              // slot of row 2 oh + 2 D
@@ -273,12 +313,25 @@ conv_s2row_kernel(const S2Params a) {
       else if (D == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(7)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+#if DRNMI_S2_STAMP
+      if (stamp[3] == 0) stamp[3] = __builtin_amdgcn_s_memtime();   // first row step done
+#endif
       s_lo = s_lo + 2 >= RING ? s_lo + 2 - RING : s_lo + 2;
       s_dma = s_dma + 2 >= RING ? s_dma + 2 - RING : s_dma + 2;
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#if DRNMI_S2_STAMP
+    stamp[7] += 1;                                                  // segments (ring refills)
+#endif
+    more = idx < end;
+    if (more) begin_segment();
   }
+#if DRNMI_S2_STAMP
+  stamp[4] = __builtin_amdgcn_s_memtime();
+  stamp[6] = __builtin_amdgcn_s_memrealtime();
+  s2_stamp_store(stamp);
+#endif
 }
 
 // --- Stride-1 3x3 64 -> 64 with the block's 1x1 stride-2 downsample folded in (x2, 32 channels):
@@ -320,10 +373,13 @@ conv_s1x2row_kernel(const S1Params a) {
     for (int fm = 0; fm < 2; ++fm)
       wf[ks][fm] = *reinterpret_cast<const u32x4_t*>(a.wgt + static_cast<int64_t>(32 * wc + 16 * fm + fr) * a.k_pad +
                                                      32 * ks + 8 * fq);
+  auto pin_weights = [&]() {   // as in conv_s2row_kernel
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks)
+    for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-    for (int fm = 0; fm < 2; ++fm) asm volatile("" : "+a"(wf[ks][fm]));
+      for (int fm = 0; fm < 2; ++fm) asm volatile("" : "+a"(wf[ks][fm]));
+  };
+  if constexpr (!DRNMI_S2_LATEPIN) pin_weights();
   f32x4 cinit[2];
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm) {
@@ -356,18 +412,42 @@ conv_s1x2row_kernel(const S1Params a) {
 
   int idx = blockIdx.x * a.per_wg;
   const int end = min(idx + a.per_wg, a.total);
-  while (idx < end) {
+  int ya = 0, yb = 0, n = 0, ow0 = 0;
+  // 16 DMA pieces per step: 0..8 the conv row (9 KB slot), 9..12 the x2 row (4 KB), 13..15
+  // dummies into the slack KB; wave w issues pieces w + 4 k, k < 4.  Lane offsets (column part)
+  // depend only on (k, lane); the row part is a scalar offset.
+  uint32_t vo[4];
+  auto piece = [&](int k, int row, int slot1, int slot2) {   // conv row `row` (slot1); x2 row of output row row - 1 (slot2)
+    const int i = wave + 4 * k;
+    int soff = 0, dst = kX1Ring * kX1Slot + kX2Ring * kX2Slot;
+    bool ok = false;
+    if (i < 9) {
+      ok = static_cast<unsigned>(row) < static_cast<unsigned>(H);
+      soff = ok ? ((n * H + row) * W) * 128 : 0;
+      dst = slot1 * kX1Slot + i * 1024;
+    } else if (i < 13) {
+      const int r2 = 2 * (row - 1);
+      ok = row - 1 >= 0 && row - 1 < H && r2 < a.h2;
+      soff = ok ? ((n * a.h2 + r2) * a.w2) * 64 : 0;
+      dst = kX1Ring * kX1Slot + slot2 * kX2Slot + (i - 9) * 1024;
+    }
+    soff = __builtin_amdgcn_readfirstlane(soff);
+    dst = __builtin_amdgcn_readfirstlane(dst);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 9 ? xs : x2s, (lds_t*)(smem + dst), 16, ok ? vo[k] : kOob, soff, 0, 0);
+  };
+  auto m5 = [](int r) { return ((r % kX1Ring) + kX1Ring) % kX1Ring; };
+  auto m3 = [](int r) { return ((r % kX2Ring) + kX2Ring) % kX2Ring; };
+  // next segment: its state and its ring fill -- conv rows ya - 1 .. ya + 2 with the x2 rows of
+  // output rows ya - 2 .. ya + 1 (the first two are never read); step oh then issues conv row
+  // oh + 3 and the x2 row of oh + 2
+  auto begin_segment = [&]() {
     const int seg = idx / H;
-    const int ya = idx - seg * H;
-    const int yb = min(H, ya + (end - idx));
+    ya = idx - seg * H;
+    yb = min(H, ya + (end - idx));
     idx += yb - ya;
-    const int n = seg / a.strips, s = seg - n * a.strips;
-    const int ow0 = OWS * s;
-
-    // 16 DMA pieces per step: 0..8 the conv row (9 KB slot), 9..12 the x2 row (4 KB), 13..15
-    // dummies into the slack KB; wave w issues pieces w + 4 k, k < 4.  Lane offsets (column part)
-    // depend only on (k, lane); the row part is a scalar offset.
-    uint32_t vo[4];
+    n = seg / a.strips;
+    const int s = seg - n * a.strips;
+    ow0 = OWS * s;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = wave + 4 * k;
@@ -383,32 +463,15 @@ conv_s1x2row_kernel(const S1Params a) {
       }
       vo[k] = v;
     }
-    auto piece = [&](int k, int row, int slot1, int slot2) {   // conv row `row` (slot1); x2 row of output row row - 1 (slot2)
-      const int i = wave + 4 * k;
-      int soff = 0, dst = kX1Ring * kX1Slot + kX2Ring * kX2Slot;
-      bool ok = false;
-      if (i < 9) {
-        ok = static_cast<unsigned>(row) < static_cast<unsigned>(H);
-        soff = ok ? ((n * H + row) * W) * 128 : 0;
-        dst = slot1 * kX1Slot + i * 1024;
-      } else if (i < 13) {
-        const int r2 = 2 * (row - 1);
-        ok = row - 1 >= 0 && row - 1 < H && r2 < a.h2;
-        soff = ok ? ((n * a.h2 + r2) * a.w2) * 64 : 0;
-        dst = kX1Ring * kX1Slot + slot2 * kX2Slot + (i - 9) * 1024;
-      }
-      soff = __builtin_amdgcn_readfirstlane(soff);
-      dst = __builtin_amdgcn_readfirstlane(dst);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 9 ? xs : x2s, (lds_t*)(smem + dst), 16, ok ? vo[k] : kOob, soff, 0, 0);
-    };
-    auto m5 = [](int r) { return ((r % kX1Ring) + kX1Ring) % kX1Ring; };
-    auto m3 = [](int r) { return ((r % kX2Ring) + kX2Ring) % kX2Ring; };
-    // prologue: conv rows ya - 1 .. ya + 2 with the x2 rows of output rows ya - 2 .. ya + 1 (the
-    // first two are never read); step oh then issues conv row oh + 3 and x2 row of oh + 2
 #pragma unroll
     for (int r = -1; r <= 2; ++r)
 #pragma unroll
       for (int k = 0; k < 4; ++k) piece(k, ya + r, m5(ya + r), m3(ya + r - 1));
+  };
+  bool more = idx < end;
+  if (more) begin_segment();
+  if constexpr (DRNMI_S2_LATEPIN) pin_weights();   // waits for the weights only: the fill stays in flight
+  while (more) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 
@@ -478,6 +541,8 @@ conv_s1x2row_kernel(const S1Params a) {
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    more = idx < end;
+    if (more) begin_segment();
   }
 }
 
@@ -612,3 +677,18 @@ int s2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t st) {
 }
 
 }  // namespace drnmi
+
+#if DRNMI_S2_STAMP
+// diagnostic builds: copy the per-workgroup stamps of the last conv_s2row_kernel launch to the host
+// ([wg][8]: realtime start, memtime start, after the first ring fill, after the first row step,
+// memtime end, rows walked, realtime end, segments)
+extern "C" int drnmi_diag_s2_stamps(unsigned long long* host, int wgs) {
+  if (host == nullptr || wgs <= 0 || wgs > drnmi::kStampWgs) return -1;
+  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(drnmi::g_s2_stamp), sizeof(unsigned long long) * 8 * wgs, 0,
+                                              hipMemcpyDeviceToHost));
+}
+extern "C" int drnmi_diag_s2_stamps_clear() {
+  static unsigned long long zero[drnmi::kStampWgs * 8] = {};
+  return static_cast<int>(hipMemcpyToSymbol(HIP_SYMBOL(drnmi::g_s2_stamp), zero, sizeof(zero), 0, hipMemcpyHostToDevice));
+}
+#endif
