@@ -57,6 +57,8 @@ CONV_CASES = [
     (1, 16, 16, 64, 128, 1, 2, 0, 1, False, "i8"),      # 1x1 stride-2 downsample
     (1, 12, 20, 512, 512, 3, 1, 4, 4, False, "bf16"),   # dilation 4, bf16 out
     (1, 10, 10, 512, 19, 1, 1, 0, 1, False, "f32"),     # seg head: cout 19, fp32 NCHW logits
+    (1, 10, 10, 512, 19, 1, 1, 0, 1, False, "f32rows20"),  # labels-head NHWC rows (y_sp 20)
+    (1, 10, 10, 512, 19, 1, 1, 0, 1, False, "f32slice28"),  # channel slice of a wider fp32 NHWC buffer
     (2, 32, 64, 256, 512, 1, 1, 0, 1, False, "i8"),     # layer6.0 downsample shape (occ2 1x1 tile)
     (1, 9, 17, 128, 256, 1, 1, 0, 1, True, "bf16"),     # ragged 1x1 with a residual
     (1, 8, 8, 256, 256, 3, 1, 1, 1, True, "f32"),
@@ -97,6 +99,10 @@ def test_conv_i8_matches_oracle(case):
     if out == "f32":
         y = torch.full((n, cout, ho, wo), float("nan"), device=DEV)
         a.y_sn, a.y_sp, a.y_sc, a.out_dtype = cout * ho * wo, 1, ho * wo, L.DRNMI_F32
+    elif out.startswith("f32"):                      # NHWC rows of ysp floats, sentinel in the rest
+        ysp = int(out[len("f32rows"):] if out.startswith("f32rows") else out[len("f32slice"):])
+        y = torch.full((n, ho, wo, ysp), 7.0, device=DEV)
+        a.y_sn, a.y_sp, a.y_sc, a.out_dtype = ho * wo * ysp, ysp, 1, L.DRNMI_F32
     else:
         y = torch.zeros((n, ho, wo, cout), dtype=torch.int8 if out == "i8" else torch.int16, device=DEV)
         a.y_sn, a.y_sp, a.y_sc = ho * wo * cout, cout, 1
@@ -104,7 +110,7 @@ def test_conv_i8_matches_oracle(case):
     a.y = y.data_ptr()
     a.n, a.h, a.w, a.cin, a.ho, a.wo, a.cout, a.cout_pad = n, h, w, cin, ho, wo, cout, cout_pad
     a.ks, a.stride, a.pad, a.dil, a.k, a.k_pad = ks, st, pad, dil, k, k
-    a.relu = 1 if out != "f32" or has_res else 0
+    a.relu = 1 if not out.startswith("f32") or has_res else 0
     a.dtype, a.tile, a.algo = L.DRNMI_I8, -1, L.ALGO_IGEMM
     a.res_scale, a.out_scale = res_scale, out_scale
     name = lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
@@ -116,11 +122,15 @@ def test_conv_i8_matches_oracle(case):
     L.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), _stream()), "conv i8")
     torch.cuda.synchronize()
     ref = Q.conv_i8(x, wpk, scale, shift, cout, ks, st, pad, dil, bool(a.relu), res, res_scale,
-                    {"i8": "i8", "bf16": "bf16", "f32": "f32"}[out], out_scale)
+                    "f32" if out.startswith("f32") else out, out_scale)
     got = y.cpu().numpy()
     if out == "f32":
         got = got.transpose(0, 2, 3, 1)
         np.testing.assert_array_equal(got, ref)
+    elif out.startswith("f32"):
+        np.testing.assert_array_equal(got[..., :cout], ref)
+        if out.startswith("f32slice"):               # a wider buffer's other channels stay untouched
+            assert bool((got[..., cout:] == 7.0).all())
     elif out == "bf16":
         np.testing.assert_array_equal(got.view(np.uint16), ref)
     else:

@@ -142,6 +142,38 @@ def test_seg_kernel_matches_bk32_tile_bit_identical(n, h, w, cin, cout, fold, nc
     assert (got - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("ysp", [20, 28, 64])
+def test_fp32_nhwc_store_stays_in_its_channels(ysp):
+    """bf16 in, fp32 NHWC out (conv_big's 16-B fp32 epilogue): rows of ysp floats.  ysp 20 =
+    round_up(19, 4) is the labels head's padded-row layout; 28 / 64 are channel slices of a wider
+    buffer, whose channels past cout must keep their sentinel."""
+    n, h, w, cin, cout = 2, 9, 14, 512, 19
+    g = torch.Generator().manual_seed(90 + ysp)
+    x = torch.randn(n, h, w, cin, generator=g).bfloat16()
+    wt = torch.randn(cout, cin, 1, 1, generator=g) * 0.05
+    b = torch.randn(cout, generator=g) * 0.1
+    wpk, k = ops.pack_conv_weight(wt.to(DEV), cin, torch.bfloat16)
+    sc = torch.ones(wpk.shape[0], device=DEV)
+    sh = torch.zeros(wpk.shape[0], device=DEV)
+    sh[:cout] = b.to(DEV)
+    y = torch.full((n, h, w, ysp), 7.0, device=DEV)
+    xd = x.to(DEV)
+    a = _lib.ConvArgs()
+    a.x, a.wgt, a.scale, a.shift, a.res, a.y = xd.data_ptr(), wpk.data_ptr(), sc.data_ptr(), sh.data_ptr(), None, \
+        y.data_ptr()
+    a.y_sn, a.y_sp, a.y_sc = h * w * ysp, ysp, 1
+    a.n, a.h, a.w, a.cin, a.ho, a.wo, a.cout, a.cout_pad = n, h, w, cin, h, w, cout, wpk.shape[0]
+    a.ks, a.stride, a.pad, a.dil, a.k, a.k_pad, a.relu = 1, 1, 0, 1, k, wpk.shape[1], 0
+    a.dtype, a.out_dtype, a.tile, a.algo = _lib.DRNMI_BF16, _lib.DRNMI_F32, -1, _lib.ALGO_IGEMM
+    _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "conv")
+    torch.cuda.synchronize()
+    got = y.cpu()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wt.bfloat16().float(), b).permute(0, 2, 3, 1)
+    assert (got[..., :cout] - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    if ysp > 20:
+        assert bool((got[..., cout:] == 7.0).all())
+
+
 def test_frame_ingest_bit_exact(golden_forward):
     for case in ["d22_1x64x128", "d22_1x300x300"]:
         frames = torch.from_numpy(golden_forward[case + "/frames"]).to(DEV)
@@ -244,6 +276,105 @@ def test_patch_conv_bf16(case):
     assert (got - ref).abs().max().item() <= 1.5e-2 * scale
     # the two bf16 algorithms agree to bf16 output rounding
     assert (got - y2.float().permute(0, 3, 1, 2).cpu()).abs().max().item() <= 1e-2 * scale
+
+
+F32_PATCH_CASES = [  # cin(stored), cout, ks, stride, h, w -- the exact-fp32 patch kernel shapes
+    (16, 16, 3, 1, 37, 131),
+    (16, 32, 3, 2, 41, 133),
+    (8, 16, 7, 1, 23, 77),
+    (16, 16, 3, 1, 1, 1),
+    (16, 32, 3, 2, 2, 3),
+    (8, 16, 7, 1, 70, 5),
+]
+
+
+@pytest.mark.parametrize("case", range(len(F32_PATCH_CASES)))
+def test_patch_conv_f32(case):
+    """patch_f32_kernel (f32-input MFMA = an fmaf chain per output, conv_igemm's K order) vs the f32
+    implicit GEMM it replaces in the fp32 mode (bit-identical) and vs the fp64 conv."""
+    cin, cout, ks, stride, h, w = F32_PATCH_CASES[case]
+    n, pad = 2, ks // 2
+    creal = 3 if cin == 8 else cin
+    x = torch.zeros(n, cin, h, w)
+    x[:, :creal] = _rand((n, creal, h, w), 131 + case)
+    wt = torch.zeros(cout, cin, ks, ks)
+    wt[:, :creal] = _rand((cout, creal, ks, ks), 141 + case, (2.0 / (ks * ks * cout)) ** 0.5)
+    sc = torch.rand(cout, generator=torch.Generator().manual_seed(11)) + 0.5
+    sh = torch.rand(cout, generator=torch.Generator().manual_seed(12)) - 0.5
+    ref = _ref_conv(x.double(), wt.double(), sc.double(), sh.double(), None, stride, pad, 1, True)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    name = ops_kernel_name(xd, wt, stride, pad, _lib.ALGO_PATCH)
+    assert name.startswith("patch_f32_kernel"), name
+    y = ops.conv2d_bn_act(xd, wt.to(DEV), sc.to(DEV), sh.to(DEV), None, stride, pad, 1, True, algo=_lib.ALGO_PATCH)
+    yi = ops.conv2d_bn_act(xd, wt.to(DEV), sc.to(DEV), sh.to(DEV), None, stride, pad, 1, True)
+    torch.cuda.synchronize()
+    got = y.permute(0, 3, 1, 2).cpu().double()
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    err_i = (yi.permute(0, 3, 1, 2).cpu().double() - ref).abs().max().item()
+    print(f"{name} {F32_PATCH_CASES[case]}: max-abs vs fp64 {err:.2e} (igemm {err_i:.2e}, |y| {scale:.2f})")
+    assert err <= 1e-5 * scale + 1e-6
+    assert torch.equal(y, yi)
+
+
+def ops_kernel_name(xd, wt, stride, pad, algo):
+    """drnmi_conv_kernel_name of the fp32 launch ops.conv2d_bn_act would make for these operands."""
+    n, h, w, cs = xd.shape
+    cout, _, ks, _ = wt.shape
+    wpk, k = ops.pack_conv_weight(wt, cs, torch.float32)
+    a = _lib.ConvArgs()
+    a.n, a.h, a.w, a.cin = n, h, w, cs
+    a.ks, a.stride, a.pad, a.dil = ks, stride, pad, 1
+    a.ho, a.wo = (h + 2 * pad - ks) // stride + 1, (w + 2 * pad - ks) // stride + 1
+    a.cout, a.cout_pad, a.k, a.k_pad = cout, wpk.shape[0], k, wpk.shape[1]
+    a.dtype = a.out_dtype = _lib.DRNMI_F32
+    a.y_sp, a.y_sc = cout, 1
+    a.tile, a.algo = -1, algo
+    return _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
+
+
+@pytest.mark.parametrize("hw", [(45, 83), (9, 301), (130, 67), (1, 1)])
+def test_stem_u8_f32_ingest_bit_exact(hw):
+    """Exact-fp32 stem from uint8 frames, centre-tap identity weights: the output is the normalised
+    frame itself, bit for bit equal to the reference ToTensor + Normalize (oracle preprocess_u8) and
+    to drnmi_frame_ingest_u8, zero padding at every edge."""
+    h, w = hw
+    frames = torch.randint(0, 256, (3, h, w, 3), dtype=torch.uint8, generator=torch.Generator().manual_seed(h + w))
+    wt = torch.zeros(16, 3, 7, 7)
+    for c in range(3):
+        wt[c, c, 3, 3] = 1.0
+    y = ops.stem_u8(frames.to(DEV), wt, torch.ones(16), torch.zeros(16), O.INFO_MEAN, O.INFO_STD, relu=False,
+                    dtype=torch.float32)
+    ref = O.preprocess_u8(frames.numpy())
+    assert torch.equal(y.cpu()[..., :3].permute(0, 3, 1, 2), ref)
+    assert torch.count_nonzero(y[..., 3:]).item() == 0
+
+
+@pytest.mark.parametrize("hw", [(45, 83), (33, 130), (64, 64)])
+def test_stem_u8_f32_conv(hw):
+    """Exact-fp32 fused-ingest stem vs the fp64 conv of the reference-normalised frame, and vs the
+    two-launch fp32 path (drnmi_frame_ingest_u8 + the NHWC8 stem); BGR flag."""
+    frames = torch.randint(0, 256, (2, hw[0], hw[1], 3), dtype=torch.uint8,
+                           generator=torch.Generator().manual_seed(6))
+    wt = _rand((16, 3, 7, 7), 51, 0.1)
+    sc = torch.rand(16, generator=torch.Generator().manual_seed(4)) + 0.5
+    sh = torch.rand(16, generator=torch.Generator().manual_seed(5)) - 0.5
+    x = O.preprocess_u8(frames.numpy())
+    ref = _ref_conv(x.double(), wt.double(), sc.double(), sh.double(), None, 1, 3, 1, True)
+    y = ops.stem_u8(frames.to(DEV), wt, sc.to(DEV), sh.to(DEV), O.INFO_MEAN, O.INFO_STD, dtype=torch.float32)
+    got = y.permute(0, 3, 1, 2).cpu().double()
+    scale = ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= 1e-5 * scale + 1e-6
+    # the NHWC8 form (SRC 1) stages the same normalised values in the same K order, and both are
+    # conv_igemm's order on drnmi_frame_ingest_u8's input: bit-identical to the two-launch path
+    xi = ops.frame_ingest(frames.to(DEV), O.INFO_MEAN, O.INFO_STD, dtype=torch.float32)
+    y2 = ops.conv2d_bn_act(xi, wt.to(DEV), sc.to(DEV), sh.to(DEV), None, 1, 3, 1, True, algo=_lib.ALGO_PATCH)
+    yi = ops.conv2d_bn_act(xi, wt.to(DEV), sc.to(DEV), sh.to(DEV), None, 1, 3, 1, True)
+    assert torch.equal(y2, y)
+    assert torch.equal(yi, y)
+    yb = ops.stem_u8(frames.flip(-1).contiguous().to(DEV), wt, sc.to(DEV), sh.to(DEV), O.INFO_MEAN,
+                     O.INFO_STD, bgr=True, dtype=torch.float32)
+    assert torch.equal(yb, y)
 
 
 @pytest.mark.parametrize("hw", [(45, 83), (64, 128), (9, 301), (130, 67)])

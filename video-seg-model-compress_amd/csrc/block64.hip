@@ -328,10 +328,11 @@ extern "C" int drnmi_basic_block64(const void* x, const void* pack, void* y, int
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    g_block_wgs = 2 * cus;                             // two workgroups per CU (79 KB LDS each)
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&block64_kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     if (e != hipSuccess) return static_cast<int>(e);
+    g_block_wgs = 2 * cus;                             // two workgroups per CU (79 KB LDS each); set only
+                                                       // once the LDS attribute is in place
   }
   BlockParams p;
   p.x = static_cast<const uint16_t*>(x);

@@ -280,10 +280,14 @@ __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4
   const int hw_o = p.ho * p.wo;
   const uint16_t* __restrict__ res = reinterpret_cast<const uint16_t*>(p.res);
   const bool nhwc16 = p.out_dtype == DRNMI_BF16 && p.y_sc == 1;
-  // fp32 NHWC rows with room for a whole 4-channel group (y_sp a multiple of 4): one 16-B store;
-  // channels past cout inside the row (the labels-only seg logits' padding) get the padded
-  // weight rows' values, which no reader uses
-  const bool nhwc32 = p.out_dtype == DRNMI_F32 && p.y_sc == 1 && p.y_sp % 4 == 0;
+  // fp32 NHWC rows, 16-B aligned: one 16-B store per whole 4-channel group inside cout.  A partial
+  // group is stored whole only into the pixel's own padding, i.e. when the row is exactly
+  // round_up(cout, 4) wide (the labels-only seg logits, SEG_NHWC_CS): those channels get the padded
+  // weight rows' values, which no reader uses.  A conv writing a channel slice of a wider buffer
+  // (y_sp > round_up(cout, 4)) never touches the channels past cout.
+  const bool nhwc32 = p.out_dtype == DRNMI_F32 && p.y_sc == 1 && p.y_sp % 4 == 0 && p.y_sn % 4 == 0 &&
+                      (reinterpret_cast<uintptr_t>(p.y) & 15) == 0;
+  const bool pad_row = p.y_sp == ((p.cout + 3) & ~3);
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
     const int m = cur_px0 + wp * PXW + fn * 16 + fr;
@@ -328,7 +332,7 @@ __device__ __forceinline__ void store_tile(const drnmi_conv_args& p, const f32x4
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
       }
-      if (nhwc32 && co + 4 <= p.y_sp) {
+      if (nhwc32 && (full || pad_row)) {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.y) + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
       } else if (nhwc16 && full) {
         uint2 o;
@@ -424,9 +428,12 @@ __device__ __forceinline__ void store_tile_i8(const drnmi_conv_args& p, const i3
             y[ybase + static_cast<int64_t>(co + j) * p.y_sc] = static_cast<int8_t>((o >> (8 * j)) & 0xff);
           }
         }
-      } else if (p.out_dtype == DRNMI_F32 && p.y_sc == 1 && (p.y_sp & 3) == 0 && co + 4 <= p.y_sp) {
-        // fp32 NHWC rows padded to y_sp (the labels head's logits, SEG_NHWC_CS): one 16-B store;
-        // the pad channels cout .. y_sp hold scale/shift padding values nobody reads
+      } else if (p.out_dtype == DRNMI_F32 && p.y_sc == 1 && (p.y_sp & 3) == 0 && (p.y_sn & 3) == 0 &&
+                 (reinterpret_cast<uintptr_t>(p.y) & 15) == 0 && (full || p.y_sp == ((p.cout + 3) & ~3))) {
+        // fp32 NHWC rows: one 16-B store per 4-channel group; a partial group only into the pixel's
+        // own padding (rows exactly round_up(cout, 4) wide: the labels head's logits, SEG_NHWC_CS,
+        // whose pad channels hold scale/shift padding values nobody reads), never into a wider
+        // buffer's neighbouring channels
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.y) + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
 #pragma unroll

@@ -10,6 +10,9 @@ bool big_conv_supported(const drnmi_conv_args& p);
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s);  // variant -1 = auto
 const char* big_conv_name(const drnmi_conv_args& p, int variant);
 const char* patch_conv_name(const drnmi_conv_args& p);
+// Exact-fp32 small-channel LDS-patch conv on the f32 MFMA (patch_f32.hip): layer0..layer2 shapes.
+int patch_f32_dispatch(const drnmi_conv_args& p, hipStream_t s);
+const char* patch_f32_name(const drnmi_conv_args& p);
 // Fused uint8 stem + the 3x3 16->16 conv after it (patch_conv.hip).
 bool stem_l1_ok(const drnmi_conv_args& p, const drnmi_conv_args& q);
 int stem_l1_dispatch(const drnmi_conv_args& p, const drnmi_conv_args& q, hipStream_t s);

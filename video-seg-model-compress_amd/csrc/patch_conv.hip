@@ -997,6 +997,7 @@ static int patch_x6_dispatch(const drnmi_conv_args& p, hipStream_t s) {
 
 int patch_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (p.dtype == DRNMI_F32X3) return patch_x6_dispatch(p, s);
+  if (p.dtype == DRNMI_F32) return patch_f32_dispatch(p, s);       // exact fp32 (patch_f32.hip)
   if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.dil != 1 || p.res != nullptr) return DRNMI_ENOTSUP;
   if (p.y_sc != 1 || p.y_sp != p.cout) return DRNMI_ENOTSUP;            // packed NHWC output
   hipError_t e;
@@ -1030,6 +1031,7 @@ const char* patch_conv_name(const drnmi_conv_args& p) {
     if (p.cin == 16 && p.cout == 32 && p.ks == 3) return "patch_conv_kernel<16, 32, 3, 2, 4, 32, false, true>";
     return nullptr;
   }
+  if (p.dtype == DRNMI_F32) return patch_f32_name(p);
   if (p.src_u8) return stem_dma_ok(p) ? "stem_dma_kernel" : "patch_conv_kernel<4, 16, 7, 1, 4, 64, true>";
   if (p.cin == 8 && p.cout == 16 && p.ks == 7) return "patch_conv_kernel<8, 16, 7, 1, 4, 64, false>";
   if (p.cin == 16 && p.cout == 16 && p.ks == 3 && p.stride == 1)

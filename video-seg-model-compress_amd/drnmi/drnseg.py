@@ -237,8 +237,9 @@ class DRNSeg(nn.Module):
             lib = _lib.load()
             amax = torch.empty(1, dtype=torch.float32, device=frames_u8.device)
             scales = {}
-            for v, buf in plan.bufs.items():
-                if v in ("input", "logits"):
+            values = set(plan.packed.graph.channels)             # graph values only (not the
+            for v, buf in plan.bufs.items():                      # head's logits_nhwc / seg_part buffers)
+                if v in ("input", "logits") or v not in values:
                     continue
                 _lib.check(lib.drnmi_absmax(buf.data_ptr(), _lib.DRNMI_BF16, buf.numel(), amax.data_ptr(),
                                             ctypes.c_void_p(stream)), "absmax")

@@ -53,6 +53,9 @@ INT8_MIN_COUT = int(os.environ.get("DRNMI_INT8_MIN_COUT", "256"))
 PATCH_SHAPES = {(8, 16, 7, 1, 1), (16, 16, 3, 1, 1), (16, 32, 3, 2, 1)}
 # fp32x: the same full-resolution layers on the split-bf16 patch kernel (fp32 in / out)
 X6_PATCH_SHAPES = PATCH_SHAPES
+# fp32: the same layers on the exact-fp32 patch kernel (csrc/patch_f32.hip, f32-input MFMA; the stem
+# reads the uint8 frame on the segment() path)
+F32_PATCH_SHAPES = PATCH_SHAPES
 STEM_U8_K = 224     # fused u8 stem: k = kh*32 + kw*4 + c
 
 
@@ -300,13 +303,14 @@ class PackedNet:
             self.stem_u8_w = None
             stem = self.graph.nodes[0]
             w = stem.conv.weight.detach().to(self.device, torch.float32)
-            if self.base in ("bf16", "fp32x") and tuple(w.shape[1:]) == (3, 7, 7) and \
+            if self.base in ("bf16", "fp32x", "fp32") and tuple(w.shape[1:]) == (3, 7, 7) and \
                     _uses_patch(stem, self.cstride["input"], self.base):
                 wp = torch.zeros(w.shape[0], 7, 8, 4, device=self.device, dtype=torch.float32)
                 wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
                 full = torch.zeros(stem.cout_pad, STEM_U8_K, device=self.device, dtype=torch.float32)
                 full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
                 self.stem_u8_w = split3_bf16(full) if self.base == "fp32x" else full.to(self.tdtype).contiguous()
+                # (fp32: the f32 weights in the same kh*32 + kw*4 + c layout, patch_f32.hip SRC 0)
             self._front_packs = {}
             self.front_eligible = self._front_shapes_ok()
             self.block64_pairs = self._block64_pairs()
@@ -499,7 +503,8 @@ def _uses_patch(nd: ConvNode, cin_stride: int, precision: str) -> bool:
     shape = (cin_stride, c.out_channels, c.kernel_size[0], c.stride[0], c.dilation[0])
     if nd.res is not None or nd.out_fp32_nchw:
         return False
-    return (precision == "bf16" and shape in PATCH_SHAPES) or (precision == "fp32x" and shape in X6_PATCH_SHAPES)
+    return (precision == "bf16" and shape in PATCH_SHAPES) or (precision == "fp32x" and shape in X6_PATCH_SHAPES) \
+        or (precision == "fp32" and shape in F32_PATCH_SHAPES)
 
 
 # bf16: fold 1x1 downsamples into the block's last conv (PackedNet._fuse_downsamples)
@@ -637,6 +642,7 @@ class Plan:
         self.stem_fused = self._stem_fusable(reads_of)
         self.front_fused = self._front_fusable(reads_of)
         self.front_pack_t = None
+        self._norm = None                          # (mean, std, bgr) of the last ingest_u8
         # fused 64-channel BasicBlocks: the first conv's output has no other reader
         self.block64 = {}
         lib = _lib.load()
@@ -667,16 +673,16 @@ class Plan:
             return
         cs = self.SEG_NHWC_CS
         lh, lw = self.shapes[nd.dst]
-        if "logits_nhwc" not in self.bufs:
-            self.bufs["logits_nhwc"] = torch.empty(self.n * lh * lw * cs, dtype=torch.float32,
-                                                   device=self.packed.device)
         a = _lib.ConvArgs()
         ctypes.pointer(a)[0] = a0
-        a.y = self.bufs["logits_nhwc"].data_ptr()
         a.y_sn, a.y_sp, a.y_sc = lh * lw * cs, cs, 1
-        name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
+        name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))   # (routing does not read a.y)
         if name is None or not name.decode().startswith(("conv_big_kernel", "conv_i8_kernel", "conv_i8_occ2_kernel")):
             return
+        if "logits_nhwc" not in self.bufs:      # only plans whose seg conv writes the NHWC rows
+            self.bufs["logits_nhwc"] = torch.empty(self.n * lh * lw * cs, dtype=torch.float32,
+                                                   device=self.packed.device)
+        a.y = self.bufs["logits_nhwc"].data_ptr()
         self.seg_idx, self.seg_nhwc_args = i, a
         self._setup_seg_fused(i)
 
@@ -810,7 +816,9 @@ class Plan:
             if i in self.skip:
                 continue
             self.args[i] = self._conv_args(nd)
-        self.front_pack_t = None                  # re-fetched (repacked) at the next ingest_u8
+        self.front_pack_t = None
+        if self._norm is not None and self.front_fused:   # a u8 plan may run again without a new ingest
+            self.front_pack_t = self.packed.front_pack(*self._norm)
         for i in list(self.block64):
             self.block64[i] = self.packed.block64_pack(i)
         self._setup_seg_nhwc()
@@ -896,8 +904,9 @@ class Plan:
                                           self.packed.code, ctypes.c_void_p(stream)), "nchw_to_nhwc")
 
     def ingest_u8(self, frames: torch.Tensor, mean, std, bgr: bool, stream: int):
-        """uint8 HWC frames in.  bf16: the stem kernel reads them directly (normalise fused);
-        fp32: a separate ingest kernel writes the normalised NHWC8 input."""
+        """uint8 HWC frames in.  The stem kernel reads them directly (normalisation fused) on every
+        precision whose stem runs on a patch kernel; otherwise a separate ingest kernel writes the
+        normalised NHWC8 input."""
         n, h, w, _ = frames.shape
         if (n, h, w) != (self.n, self.h, self.w):
             raise ValueError("frames shape does not match the plan")
@@ -910,6 +919,7 @@ class Plan:
                 a.std[i] = float(std[i])
             if self.front_fused:
                 self.front_pack_t = self.packed.front_pack(mean, std, bgr)
+            self._norm = (tuple(mean), tuple(std), bool(bgr))
             self.src = "u8"
             return
         self.src = "nchw"

@@ -116,8 +116,9 @@ def up8_logsoftmax_argmax(logits: torch.Tensor, up_plane: torch.Tensor, want_log
     return lp, lab
 
 
-def _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu):
-    """ConvArgs of the fused-ingest 7x7 stem (PATCH, src_u8) + the tensors they point into."""
+def _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu, dtype=torch.bfloat16):
+    """ConvArgs of the fused-ingest 7x7 stem (PATCH, src_u8) + the tensors they point into.
+    dtype: bf16 (stem_dma_kernel) or fp32 (the exact-fp32 patch_f32_kernel)."""
     from .engine import STEM_U8_K
     n, h, w, _ = frames_u8.shape
     cout = weight.shape[0]
@@ -126,7 +127,7 @@ def _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu):
     wp[:, :, :7, :3] = weight.float().to(dev).permute(0, 2, 3, 1)
     full = torch.zeros(_round_up(cout, COUT_ALIGN), STEM_U8_K, device=dev)
     full[:cout] = wp.reshape(cout, STEM_U8_K)
-    wpk = full.to(torch.bfloat16).contiguous()
+    wpk = full.to(dtype).contiguous()
     sc = torch.ones(wpk.shape[0], device=dev)
     sh = torch.zeros(wpk.shape[0], device=dev)
     sc[:cout] = scale.float()
@@ -139,7 +140,7 @@ def _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu):
     a.ks, a.stride, a.pad, a.dil = 7, 1, 3, 1
     a.k = a.k_pad = STEM_U8_K
     a.relu = 1 if relu else 0
-    a.dtype = a.out_dtype = _lib.DRNMI_BF16
+    a.dtype = a.out_dtype = _CODE[dtype]
     a.tile = -1
     a.algo = _lib.ALGO_PATCH
     a.src_u8 = 1
@@ -149,11 +150,13 @@ def _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu):
     return a, (wpk, sc, sh)
 
 
-def stem_u8(frames_u8: torch.Tensor, weight: torch.Tensor, scale, shift, mean, std, bgr=False, relu=True):
-    """Fused ingest + 7x7 stem (bf16 patch kernel): uint8 [N,H,W,3] -> bf16 NHWC [N,H,W,cout]."""
+def stem_u8(frames_u8: torch.Tensor, weight: torch.Tensor, scale, shift, mean, std, bgr=False, relu=True,
+            dtype=torch.bfloat16):
+    """Fused ingest + 7x7 stem: uint8 [N,H,W,3] -> NHWC [N,H,W,cout] in `dtype` (bf16 patch kernel, or
+    fp32: the exact-fp32 patch kernel)."""
     n, h, w, _ = frames_u8.shape
-    a, keep = _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu)
-    y = torch.empty(n, h, w, weight.shape[0], device=frames_u8.device, dtype=torch.bfloat16)
+    a, keep = _stem_u8_args(frames_u8, weight, scale, shift, mean, std, bgr, relu, dtype)
+    y = torch.empty(n, h, w, weight.shape[0], device=frames_u8.device, dtype=dtype)
     a.y = y.data_ptr()
     lib = _lib.load()
     _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr(frames_u8.device))), "stem_u8")
