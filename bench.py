@@ -13,8 +13,9 @@ timing barrier and the max-over-ranks of the elapsed time).
 
 `--gpus N` without a torchrun environment spawns the N rank processes itself (before any GPU
 call; one device each, RCCL rendezvous on 127.0.0.1); under torchrun WORLD_SIZE must equal N.
-The default bf16 line also carries `exact_mode`: the fp32-accurate (fp32x) engine on the same
-weights and frames, timed in the same process, with its own dominant-kernel roofline and parity.
+The default bf16 line also carries `exact_mode` (the fp32-accurate split-bf16 engine) and
+`exact_mode_fp32` (exact fp32 on the f32 MFMA): the exact-argmax modes on the same weights and
+frames, timed in the same process, each with its own dominant-kernel roofline and parity.
 
 Prints ONE JSON line (rank 0).
 """
@@ -540,30 +541,42 @@ def main(argv=None):
     out["network_roofline"] = network_block(m, args.steps, B)
     if host is not None:
         out["host_frames"] = host
-    exact = None
+    exact = {}                               # precision -> (sub-line, model)
     if (world == 1 and args.precision == "bf16" and not args.prune and not args.no_exact_mode
             and not args.no_kernel_events):
-        # exact-argmax mode (north star: labels bit-exact vs the reference): the fp32-accurate
-        # split-bf16 engine on the same weights and frames, timed in this process
-        xm = build(args.arch, 19, seed=0, device=dev, precision="fp32x")
-        mx = measure(args, xm, frames, args.exact_steps, 2, world, dev)
-        xroof, _ = roofline_block(args, mx, "fp32x")
-        exact = {"precision": "fp32x", "value": B * args.exact_steps / mx["el"], "unit": "frames/s",
-                 "steps": args.exact_steps, "warmup": 2, "ms_per_step": mx["el"] / args.exact_steps * 1e3,
-                 "roofline": xroof, "network_roofline": network_block(mx, args.exact_steps, B),
-                 "arithmetic": "fp32-accurate: exact 3-way bf16 split of weights and activations, the six "
-                               "products above 2^-24 on the bf16 MFMA, fp32 accumulation (peak 2.5 PF / 6)"}
-        out["exact_mode"] = exact
+        # exact-argmax modes (north star: labels bit-exact vs the reference), each on the same weights
+        # and frames, timed in this process: fp32x (split-bf16, fp32-accurate) and fp32 (the
+        # reference's own arithmetic on the f32-input MFMA)
+        for prec, arith in EXACT_MODES:
+            xm = build(args.arch, 19, seed=0, device=dev, precision=prec)
+            mx = measure(args, xm, frames, args.exact_steps, 2, world, dev)
+            xroof, xkern = roofline_block(args, mx, prec)
+            exact[prec] = ({"precision": prec, "value": B * args.exact_steps / mx["el"], "unit": "frames/s",
+                            "steps": args.exact_steps, "warmup": 2,
+                            "ms_per_step": mx["el"] / args.exact_steps * 1e3,
+                            "roofline": xroof, "network_roofline": network_block(mx, args.exact_steps, B),
+                            "kernels": xkern, "arithmetic": arith}, xm)
+            del mx
+        out["exact_mode"] = exact["fp32x"][0]
+        out["exact_mode_fp32"] = exact["fp32"][0]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], (bframes, blabels) = cpu_baseline(args, args.cpu_seconds)
         if not args.prune:                   # the oracle runs the unpruned synthetic weights
             out["parity_vs_ref"] = parity_vs_ref(args, model, bframes, blabels, dev)
-            if exact is not None:
-                exact["parity_vs_ref"] = parity_vs_ref(args, xm, bframes, blabels, dev, "fp32x")
+            for prec, (line, xm) in exact.items():
+                line["parity_vs_ref"] = parity_vs_ref(args, xm, bframes, blabels, dev, prec)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+EXACT_MODES = (
+    ("fp32x", "fp32-accurate: exact 3-way bf16 split of weights and activations, the six products above "
+              "2^-24 on the bf16 MFMA, fp32 accumulation (peak 2.5 PF / 6)"),
+    ("fp32", "exact fp32: f32-input MFMA (v_mfma_f32_16x16x4_f32 = an fmaf chain per output), fp32 "
+             "activations, the reference's arithmetic (peak 157.3 TF)"),
+)
 
 
 def host_frames_run(args, model, step, world, dev):

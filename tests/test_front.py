@@ -117,4 +117,4 @@ def test_front_network_labels():
     a_front = float((lab.cpu() == ref).float().mean())
     a_sep = float((lab2.cpu() == ref).float().mean())
     print(f"front vs separate launches {agree:.4f}; vs fp32 oracle: front {a_front:.4f}, separate {a_sep:.4f}")
-    assert agree >= 0.985 and a_front >= 0.98
+    assert agree >= 0.99 and a_front >= 0.99           # measured 0.9937 / 0.9951

@@ -97,6 +97,33 @@ def test_headline_1024x2048_exact_modes_vs_oracle(precision):
         assert int(diff.sum()) <= 4 and not np.any(diff & (margin > 1e-5))
 
 
+def test_headline_1024x2048_bf16_vs_oracle():
+    """Config C2, the headline path itself: bf16 DRNSeg.segment (the seg_video loop bench.py times:
+    uint8 frames -> labels, seg_video_old_no_plot.py:157-169, semantic_seg.py:445) on bench.py's
+    seed-0 weights and both of its 1024x2048 parity frames vs the fp32 oracle.  Gates just below
+    the measured values (round 4 bench: 99.945 % of 4,194,304 labels, mIoU vs ref 96.5)."""
+    from drnmi import metrics
+    from drnmi.drnseg import build
+    from drnmi.weights import synth_frames
+    m = build("drn_d_22", 19, seed=0, device=DEV, precision="bf16")
+    frames = synth_frames(7, 2, 1024, 2048)
+    lab = m.segment(torch.from_numpy(frames).to(DEV)).long()
+    torch.cuda.synchronize()
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref = []
+    for i in range(len(frames)):
+        ref_lp, _, _ = O.drnseg_forward(sd, "drn_d_22", O.preprocess_u8(frames[i:i + 1]))
+        ref.append(torch.max(ref_lp, 1)[1])
+        del ref_lp
+    ref = torch.cat(ref).to(DEV)
+    agree = float((lab == ref).float().mean())
+    hist = metrics.fast_hist(lab.flatten(), ref.flatten(), 19)
+    miou = float(metrics.miou(hist.cpu().numpy()))
+    print(f"headline D-22 2x1024x2048 bf16 segment: labels agree {agree:.6f} "
+          f"({int((lab != ref).sum())} of {lab.numel()} differ), mIoU vs ref {miou:.2f}")
+    assert agree >= 0.999 and miou >= 96.0
+
+
 @pytest.mark.parametrize("precision", ["fp32", "fp32x"])
 def test_c4_d54_rmb75_finetune_step(golden_masks, precision):
     from drnmi.drnseg import DRNSeg

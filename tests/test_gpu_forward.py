@@ -95,7 +95,9 @@ def test_bf16_forward_agreement(case, golden_forward):
     agree = (labels == golden_forward[case + "/labels"]).mean()
     print(f"{case} bf16: logit rel err {rel:.3e}, argmax agreement {agree:.4f}")
     assert rel <= 0.03
-    assert agree >= 0.98
+    # just below the measured agreement (round 4: 0.9939 / 0.9919 / 0.9894): a regression that
+    # doubles the mismatch rate fails
+    assert agree >= {"d22_2x128x256": 0.990, "d38_1x64x128": 0.988, "d54_1x64x128": 0.985}[case]
 
 
 def test_weights_repack_after_mask_apply(golden_forward, tmp_path):
@@ -150,7 +152,7 @@ def test_bf16_segment_matches_bf16_forward_labels(golden_forward):
     ref = torch.from_numpy(golden_forward[case + "/labels"]).long().to(DEV)
     agree_ref = (lab_seg == ref).float().mean().item()
     print(f"bf16 segment vs predict agreement {agree:.4f}, vs reference {agree_ref:.4f}")
-    assert agree >= 0.98 and agree_ref >= 0.98
+    assert agree >= 0.99 and agree_ref >= 0.99        # measured 0.9938 / 0.9944
 
 
 @pytest.mark.parametrize("case", CASES)

@@ -81,13 +81,14 @@ def test_segment_labels_nhwc_identical(arch, hw):
     assert torch.equal(ref, got)
 
 
-@pytest.mark.parametrize("n", [1, 2])
-def test_segment_seg_fused_into_last_conv(n):
-    """D-22 at 1024 x 2048 (layer8 on the staggered tile): the seg classifier folded into layer8's
+@pytest.mark.parametrize("arch,n", [("drn_d_22", 1), ("drn_d_22", 2), ("drn_d_38", 1), ("drn_d_54", 1)])
+def test_segment_seg_fused_into_last_conv(arch, n):
+    """DRN-D at 1024 x 2048 (layer8 on the staggered tile): the seg classifier folded into layer8's
     epilogue (drnmi_conv_stag_seg) + the SEG2 head against the separate seg conv + NHWC head.  The
     logits differ only by fp32 summation order (two 256-channel partials): bound 2^-16 max|logit|;
-    labels may flip only at near ties."""
-    m = drnseg.build("drn_d_22", 19, seed=4, device=torch.device(DEV), precision="bf16").eval()
+    labels may flip only at near ties.  Every architecture whose plan routes the fusion is covered
+    (D-38 / D-54 share D-22's 512-channel layer8)."""
+    m = drnseg.build(arch, 19, seed=4, device=torch.device(DEV), precision="bf16").eval()
     g = torch.Generator(device=DEV).manual_seed(2)
     frames = torch.randint(0, 256, (n, 1024, 2048, 3), dtype=torch.uint8, device=DEV, generator=g)
     old = engine.SEG_FUSE
@@ -108,7 +109,7 @@ def test_segment_seg_fused_into_last_conv(n):
     err = (fused - logits).abs().max().item()
     assert err <= 2 ** -16 * logits.abs().max().item() + 1e-6, err
     agree = (got == ref).float().mean().item()
-    print(f"seg-fused labels agreement {agree:.6f}, logits max |diff| {err:.3e}")
+    print(f"{arch} seg-fused labels agreement {agree:.6f}, logits max |diff| {err:.3e}")
     assert agree >= 0.9995
 
 
