@@ -1,4 +1,4 @@
-"""Row-walking stride-2 3x3 conv (csrc/conv_s2row.hip, tile id 21): the BasicBlock conv1 of DRN-D
+"""Row-walking stride-2 3x3 conv (csrc/conv_s2row.hip, tile id 20): the BasicBlock conv1 of DRN-D
 layer3.0 (32 -> 64) and layer4.0 (64 -> 128), lmodels/drn.py:27-29 conv3x3 + :49-52 (stride 2),
 BN folded (scale into the bf16 weights, shift as the accumulator start), ReLU.
 
@@ -57,11 +57,11 @@ def test_s2row_bit_identical_to_conv_big(cin, shape, relu):
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     lib = _lib.load()
     outs = {}
-    for tile in (-1, 21, 6 if cin == 32 else 7):    # auto, forced s2row, conv_big BK-32 / BK-64 64-wide tile
+    for tile in (-1, 20, 6 if cin == 32 else 7):    # auto, forced s2row, conv_big BK-32 / BK-64 64-wide tile
         y = torch.full((n, ho, wo, cout), float("nan"), device=DEV, dtype=torch.bfloat16)
         a = _args(x, wpk, k, sh, y, cin, cout, relu, tile)
         name = lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
-        if tile in (-1, 21):
+        if tile in (-1, 20):
             assert name.startswith(f"conv_s2row_kernel<{cin}, "), name
         else:
             assert name.startswith("conv_big_kernel<3, 64, 1"), name
@@ -69,10 +69,10 @@ def test_s2row_bit_identical_to_conv_big(cin, shape, relu):
         torch.cuda.synchronize()
         outs[tile] = y
     ref_tile = 6 if cin == 32 else 7
-    assert not torch.isnan(outs[21].float()).any()
-    assert torch.equal(outs[-1], outs[21])
-    assert torch.equal(outs[21], outs[ref_tile]), \
-        f"{int((outs[21] != outs[ref_tile]).sum())} of {outs[21].numel()} differ"
+    assert not torch.isnan(outs[20].float()).any()
+    assert torch.equal(outs[-1], outs[20])
+    assert torch.equal(outs[20], outs[ref_tile]), \
+        f"{int((outs[20] != outs[ref_tile]).sum())} of {outs[20].numel()} differ"
     # fp32 torch restatement (bf16 tolerance: the folded weights and the output are bf16-rounded)
     if n * h * w <= 3 * 64 * 248:
         wf = wpk[:cout, :k].float().view(cout, 3, 3, cin).permute(0, 3, 1, 2)
@@ -80,7 +80,7 @@ def test_s2row_bit_identical_to_conv_big(cin, shape, relu):
         if relu:
             r = torch.relu(r)
         r = r.permute(0, 2, 3, 1)
-        err = (outs[21].float() - r).abs()
+        err = (outs[20].float() - r).abs()
         assert bool((err <= 2 ** -7 * r.abs() + 1e-3 * r.abs().max()).all())
 
 
@@ -89,7 +89,7 @@ def test_s2row_refuses_other_shapes():
     wpk, k = ops.pack_conv_weight(torch.zeros(64, 64, 3, 3, device=DEV), 64, torch.bfloat16)   # 64 -> 64: not taken
     sh = torch.zeros(wpk.shape[0], device=DEV)
     y = torch.empty(1, 4, 4, 64, device=DEV, dtype=torch.bfloat16)
-    a = _args(x, wpk, k, sh, y, 64, 64, True, 21)
+    a = _args(x, wpk, k, sh, y, 64, 64, True, 20)
     lib = _lib.load()
     assert lib.drnmi_conv_kernel_name(ctypes.byref(a)) is None
     assert lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())) == -2
@@ -97,7 +97,7 @@ def test_s2row_refuses_other_shapes():
 
 @pytest.mark.parametrize("shape", [(1, 3, 5), (2, 17, 70), (1, 40, 130), (3, 33, 200), (8, 256, 512)])
 def test_s1x2row_bit_identical_to_halo(shape):
-    """Layer3.0 conv2 + the folded 1x1 stride-2 downsample (conv_s1x2row_kernel, tile 22) against
+    """Layer3.0 conv2 + the folded 1x1 stride-2 downsample (conv_s1x2row_kernel, tile 21) against
     conv_halo's x2 form (tile 17): same packed [W2 | W_ds | 0] rows, K order, start and epilogue."""
     n, h, w = shape
     h2, w2 = 2 * h, 2 * w
@@ -115,7 +115,7 @@ def test_s1x2row_bit_identical_to_halo(shape):
     sh[:64] = (torch.randn(64, generator=g) * 0.3).to(DEV)
     lib = _lib.load()
     outs = {}
-    for tile in (-1, 22, 17):
+    for tile in (-1, 21, 17):
         y = torch.full((n, h, w, 64), float("nan"), device=DEV, dtype=torch.bfloat16)
         a = _lib.ConvArgs()
         a.x, a.wgt, a.scale, a.shift, a.res, a.y = x.data_ptr(), wpk.data_ptr(), None, sh.data_ptr(), None, y.data_ptr()
@@ -130,12 +130,12 @@ def test_s1x2row_bit_identical_to_halo(shape):
         _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "s1x2row")
         torch.cuda.synchronize()
         outs[tile] = y
-    assert not torch.isnan(outs[22].float()).any()
-    assert torch.equal(outs[-1], outs[22])
-    assert torch.equal(outs[22], outs[17]), f"{int((outs[22] != outs[17]).sum())} of {outs[22].numel()} differ"
+    assert not torch.isnan(outs[21].float()).any()
+    assert torch.equal(outs[-1], outs[21])
+    assert torch.equal(outs[21], outs[17]), f"{int((outs[21] != outs[17]).sum())} of {outs[21].numel()} differ"
     if n * h * w <= 3 * 33 * 200:
         r = F.conv2d(x.float().permute(0, 3, 1, 2), wt.float().to(DEV), padding=1) \
             + F.conv2d(x2.float().permute(0, 3, 1, 2), wd.float().to(DEV), stride=2) + sh[:64].view(1, -1, 1, 1)
         r = torch.relu(r).permute(0, 2, 3, 1)
-        err = (outs[22].float() - r).abs()
+        err = (outs[21].float() - r).abs()
         assert bool((err <= 2 ** -7 * r.abs() + 1e-3 * r.abs().max()).all())

@@ -42,12 +42,6 @@ constexpr int kTSlot = kTW * kRowB;    // 8192
 constexpr int kTRing = 4;
 constexpr int kTBase = kXRing * kXSlot;                  // 46080
 constexpr int kLds = kTBase + kTRing * kTSlot + 512;     // + slack: conv2 reads t pixels 64, 65 (unstored columns); two workgroups per CU
-#ifndef DRNMI_B64_LATEPIN
-#define DRNMI_B64_LATEPIN 1    // pin the weights after the first ring fill is issued (0: before)
-#endif
-#ifndef DRNMI_B64_PF
-#define DRNMI_B64_PF 4         // B fragment reads in flight ahead of their MFMAs
-#endif
 constexpr int kChunks = 18;            // 9 taps x 2 chunks of 32 channels
 constexpr int kSlices = 2 * kChunks;   // A fragments per wave: (chunk, 16-row tile)
 constexpr int kFragB = 16;             // bytes per lane per A fragment
@@ -95,13 +89,11 @@ block64_kernel(const BlockParams a) {
 #pragma unroll
     for (int s = 0; s < kSlices; ++s) wf[s] = pk[s * 64];
   }
-  // the pins wait for every weight load: with DRNMI_B64_LATEPIN they follow the first segment's
-  // ring-fill DMA, so the two latencies overlap (conv_s2row.hip, scripts/s2row_stamps.py)
+  // the pins wait for every weight load: they follow the first segment's ring-fill DMA, so the two latencies overlap (conv_s2row.hip, scripts/s2row_stamps.py)
   auto pin_weights = [&]() {
 #pragma unroll
     for (int s = 0; s < kSlices; ++s) asm volatile("" : "+a"(wf[s]));
   };
-  if constexpr (!DRNMI_B64_LATEPIN) pin_weights();
   // accumulator start: the conv's shift for the 16 D rows this lane holds
   f32x4 cinit[2];
   {
@@ -170,7 +162,7 @@ block64_kernel(const BlockParams a) {
   };
   bool more = idx < end;
   if (more) begin_segment();
-  if constexpr (DRNMI_B64_LATEPIN) pin_weights();   // waits for the weights only: the fill stays in flight
+  pin_weights();                                     // waits for the weights only: the fill stays in flight
   while (more) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -192,7 +184,7 @@ block64_kernel(const BlockParams a) {
       }
       // entries (chunk ks = tap * 2 + sb, pixel tile fn): one B read, two MFMAs (row tiles); reads
       // run PF entries ahead with counted lgkmcnt
-      constexpr int NE = kChunks * 4, PF = DRNMI_B64_PF;
+      constexpr int NE = kChunks * 4, PF = 4;   // B reads in flight
       u32x4_t bq[PF + 1];
       auto issue_rd = [&](auto e_c) {
         constexpr int E = decltype(e_c)::value;

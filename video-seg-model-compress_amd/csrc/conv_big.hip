@@ -33,26 +33,10 @@
 #include "conv_tile.h"
 #include "kernels.h"
 
-// Diagnostic-only ablation builds (never the shipped library): DRNMI_ABLATE bit 0 drops the
-// in-loop DMA (MFMAs consume stale LDS), bit 1 drops the MFMAs (loads only).
-#ifndef DRNMI_ABLATE
-#define DRNMI_ABLATE 0
-#endif
-// LDS fragment prefetch distance in MFMA groups (1 or 2)
-#ifndef DRNMI_PFD
-#define DRNMI_PFD 1
-#endif
-// Pin the main-loop schedule: fragment reads for group q+PFD go out before group q's MFMAs
-// (sched_barrier between groups) and the next step's DMA pieces are issued without a branch
-// (the last steps re-fetch a clamped step into the idle stage).  Without the pins the compiler
-// sinks each read next to its MFMAs and waits lgkmcnt(0) on it (no LDS latency hiding).
-#ifndef DRNMI_PRIO
-#define DRNMI_PRIO 0   // diagnostic: 1 raises wave priority across each MFMA group, 2 across
-                       // each group's fragment reads and DMA issue (both measured slower)
-#endif
-#ifndef DRNMI_PIN
-#define DRNMI_PIN 1
-#endif
+// The main-loop schedule is pinned: fragment reads for group q+1 go out before group q's MFMAs
+// (sched_barrier between groups) and the next step's DMA pieces are issued without a branch (the
+// last steps re-fetch a clamped step into the idle stage).  Without the pins the compiler sinks
+// each read next to its MFMAs and waits lgkmcnt(0) on it (no LDS latency hiding).
 
 namespace drnmi {
 namespace {
@@ -281,10 +265,9 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
       constexpr int GL = STRIP ? C::A_INSTR + 2 : C::GLDS;
       constexpr int NG = C::SUB * C::GR;
       constexpr int PPG = (GL + C::GR - 1) / C::GR;   // DMA pieces per group (first substep)
-      const bool nxt = (DRNMI_ABLATE & 1) ? false : (DRNMI_PIN ? true : t + NST - 1 < nlive);
       const StepP sp = step_params(kt_at(t + NST - 1 < nlive ? t + NST - 1 : nlive - 1));
       const int nst = (t + NST - 1) % NST;
-      constexpr int PFD = DRNMI_PFD;
+      constexpr int PFD = 1;                     // fragment prefetch distance in MFMA groups
       constexpr int NAF = PFD + 1;               // A-fragment ring depth
       typename K::frag af[NAF][C::FPG], bfr[2][C::FN];
       auto load_a = [&](typename K::frag (&dst)[C::FPG], int q) {
@@ -320,21 +303,11 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         // group q's fragments (issued a group ago) land before the next reads go out, so the
         // compiler's wait in front of the MFMAs does not also cover the fresh reads
         // (s_waitcnt lgkmcnt(0) with vmcnt/expcnt at their maxima: LDS-DMA stays in flight)
-        if constexpr (DRNMI_PIN >= 2) __builtin_amdgcn_s_waitcnt(0xC07F);
-        if constexpr (DRNMI_PRIO == 2) if (q == 0) __builtin_amdgcn_s_setprio(1);
         if (q + PFD < NG) {
           load_a(af[(q + PFD) % NAF], q + PFD);
           if ((q + PFD) % C::GR == 0) load_b(bfr[((q + PFD) / C::GR) & 1], (q + PFD) / C::GR);
         }
-        if constexpr (DRNMI_PIN) __builtin_amdgcn_sched_barrier(0);
-        if constexpr (DRNMI_PRIO == 1) { __builtin_amdgcn_s_setprio(1); __builtin_amdgcn_sched_barrier(0); }
-        if constexpr (DRNMI_PRIO == 2) { __builtin_amdgcn_s_setprio(0); __builtin_amdgcn_sched_barrier(0); }
-        if constexpr ((DRNMI_ABLATE & 2) != 0) {
-#pragma unroll
-          for (int h = 0; h < C::FPG; ++h)
-#pragma unroll
-            for (int fn = 0; fn < C::FN; ++fn) asm volatile("" :: "v"(af[q % NAF][h]), "v"(bfr[(q / C::GR) & 1][fn]));
-        } else {
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int h = 0; h < C::FPG; ++h) {
 #pragma unroll
@@ -342,10 +315,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
             acc[(q % C::GR) * C::FPG + h][fn] = K::mma(
                 af[q % NAF][h], bfr[(q / C::GR) & 1][fn], acc[(q % C::GR) * C::FPG + h][fn]);
         }
-        }
-        if constexpr (DRNMI_PRIO == 1) { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_setprio(0); }
-        if constexpr (DRNMI_PRIO == 2) { __builtin_amdgcn_sched_barrier(0); __builtin_amdgcn_s_setprio(1); }
-        if (q < C::GR && nxt) {
+        if (q < C::GR) {
 #pragma unroll
           for (int k = 0; k < PPG; ++k)
             if constexpr (STRIP) {
@@ -356,7 +326,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
               if (q * PPG + k < C::GLDS) issue_piece(sp, nst, q * PPG + k);
             }
         }
-        if constexpr (DRNMI_PIN) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 
@@ -370,7 +340,7 @@ __device__ __forceinline__ void conv_big_body(const drnmi_conv_args& p) {
         tile = xcd_remap2(tl, ntiles);
         px0 = (tile / nco) * kBPX;
         co0 = (tile % nco) * C::BCO;
-        // every wave done with the ring, and (DRNMI_PIN) the clamped re-fetches have landed
+        // every wave done with the ring, and the clamped re-fetches have landed
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         setup(px0, co0);
@@ -554,13 +524,6 @@ conv_pp_kernel(const drnmi_conv_args p) {
   };
   f32x4 acc[8][4];
   auto mfma = [&](const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2], int hh, int g) {
-    if constexpr ((DRNMI_ABLATE & 2) != 0) {
-#pragma unroll
-      for (int f = 0; f < 4; ++f) asm volatile("" :: "v"(a[f][0]), "v"(a[f][1]));
-#pragma unroll
-      for (int e = 0; e < 2; ++e) asm volatile("" :: "v"(b[e][0]), "v"(b[e][1]));
-      return;
-    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub)
@@ -592,7 +555,7 @@ conv_pp_kernel(const drnmi_conv_args p) {
   bf16x8 a_f[4][2], b0[2][2], b1[2][2];
   for (int s = 0; s < nk; ++s) {
     const char* sa = smem + (s & 1) * STAGE;
-    const bool n1 = (DRNMI_ABLATE & 1) ? false : s + 1 < nk, n2 = (DRNMI_ABLATE & 1) ? false : s + 2 < nk;
+    const bool n1 = s + 1 < nk, n2 = s + 2 < nk;
     // phase 0: quadrant (channels 0-63, pixels 0-31); retire the second half of step s
     load_a(a_f, sa, 0);
     load_b(b0, sa, 0);
@@ -697,26 +660,9 @@ hipError_t launch_strip(const drnmi_conv_args& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// auto-picked strip launches run conv_stag_kernel when cin % 128 == 0 (measured 5-6 % faster,
-// bit-identical); DRNMI_STAG=0 keeps them on conv_strip_kernel (A/B runs)
-bool stag_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("DRNMI_STAG");
-    on = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  return on == 1;
-}
-
-// DRNMI_STRIP=0 keeps every launch on the per-tap B gather (A/B runs)
-bool strip_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("DRNMI_STRIP");
-    on = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  return on == 1;
-}
+// Routing is fixed (no environment switches): auto-picked strip launches run conv_stag_kernel
+// when cin % 128 == 0 (measured 5-6 % faster, bit-identical), else conv_strip_kernel; the other
+// tiles stay reachable through an explicit drnmi_conv_args.tile for the bit-identity tests.
 
 // a 256-pixel tile is a run of one output row, the strip of 256 + 2 dil rows fits its buffer
 bool strip_ok(const drnmi_conv_args& p) {
@@ -734,15 +680,8 @@ bool stag_ok(const drnmi_conv_args& p) {
 }
 
 // 128-channel convs (D-22 layer4) go to the staggered 128-channel tile instead of the halo
-// kernel when both apply; DRNMI_HALO=1 keeps them on conv_halo_kernel (A/B runs)
-bool halo_preferred(const drnmi_conv_args& p) {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("DRNMI_HALO");
-    on = (e != nullptr && e[0] == '1') ? 1 : 0;
-  }
-  return on == 1 || !(stag_enabled() && strip_enabled() && big_conv_supported(p) && stag_ok(p));
-}
+// kernel when both apply (88-96 vs 102-107 us, profiles/r4c_stag128_vs_halo)
+bool halo_preferred(const drnmi_conv_args& p) { return !(big_conv_supported(p) && stag_ok(p)); }
 
 struct Variant {
   int bco, bk;
@@ -770,35 +709,15 @@ constexpr int kPingPong = 12;
 constexpr int kHalo = 13;   // conv_halo.hip (tile id 17)
 constexpr int kStrip = 14;  // conv_strip_kernel (tile id 18); auto routes variant 1 there when strip_ok
 constexpr int kStag = 15;   // conv_stag_kernel (tile id 19): the strip tile with staggered SIMD partners
-constexpr int kSeg = 16;    // conv_seg_kernel (tile id 20): the seg classifier, 1x1 to <= 32 classes
-constexpr int kS2Row = 17;  // conv_s2row_kernel (tile id 21): stride-2 3x3 32 -> 64 / 64 -> 128, row walk
-constexpr int kS1X2Row = 18;  // conv_s1x2row_kernel (tile id 22): stride-1 3x3 64 -> 64 + 1x1 s2 downsample 32 -> 64
-constexpr int kRow128 = 19;   // conv_row128_kernel (tile id 23): stride-1 3x3 128 -> 128 (+ residual), row walk
+constexpr int kS2Row = 16;  // conv_s2row_kernel (tile id 20): stride-2 3x3 32 -> 64 / 64 -> 128, row walk
+constexpr int kS1X2Row = 17;  // conv_s1x2row_kernel (tile id 21): stride-1 3x3 64 -> 64 + 1x1 s2 downsample 32 -> 64
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
-
-// the seg classifier (1x1, cout <= 32) stays on conv_big's BK-32 tile by default: conv_seg_kernel
-// (bit-identical) measured 80-84 vs 72 us on the D-22 batch-8 map (profiles/r5e_ab); DRNMI_SEG=1
-// routes it there (A/B runs)
-bool seg_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("DRNMI_SEG");
-    on = (e != nullptr && e[0] == '1') ? 1 : 0;
-  }
-  return on == 1;
-}
 
 template <int KS, bool PERSIST>
 hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
   switch (base) {
     case 0: return launch_big<KS, 128, 1, 3, 64, PERSIST>(p, s);   // 128 x 256 tile, 4 waves, 3 x 48 KB
-#if defined(DRNMI_WIDE_TEST)   // diagnostic builds only: 4 waves of 128 x 128
-    case 1: return launch_big<KS, 128, 2, 2, 64, PERSIST, 2>(p, s);
-#elif defined(DRNMI_W16_TEST)  // diagnostic builds only: 16 waves of 64 x 64
-    case 1: return launch_big<KS, 64, 4, 2, 64, PERSIST, 4>(p, s);
-#else
     case 1: return launch_big<KS, 128, 2, 2, 64, PERSIST>(p, s);   // 256 x 256 tile, 8 waves, 2 x 64 KB
-#endif
     case 2: return launch_big<KS, 64, 1, 4, 32, PERSIST>(p, s);    //  64 x 256 tile, 4 waves, 4 x 20 KB
     case 3: return launch_big<KS, 64, 1, 2, 64, PERSIST>(p, s);    //  64 x 256 tile, 4 waves, 2 x 40 KB
     case 4: return launch_big<KS, 128, 2, 4, 32, PERSIST>(p, s);   // 256 x 256 tile, 8 waves, 4 x 32 KB
@@ -846,26 +765,11 @@ constexpr I8Variant kI8Variants[] = {
 };
 constexpr int kI8Occ2 = 4;   // 128 x 256 / 64-B rows, 2 stages, two workgroups per CU
 
-// DRNMI_I8_V1 / DRNMI_I8_V3 = 0..4: force the 1x1 / 3x3 tile variant where it fits (A/B runs;
-// every variant accumulates in int32 and shares store_tile_i8, so the outputs are identical)
-static int i8_variant_override(int ks) {
-  static int ov[2] = {-2, -2};
-  int& o = ov[ks == 3 ? 1 : 0];
-  if (o == -2) {
-    const char* e = getenv(ks == 3 ? "DRNMI_I8_V3" : "DRNMI_I8_V1");
-    o = (e != nullptr && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : -1;
-  }
-  return o;
-}
-
 int i8_variant(const drnmi_conv_args& p) {
   const int wide = p.cout % 256 == 0 ? 0 : 1;
   // 1x1: the two-workgroups-per-CU tile (71.6-73.5 vs 86.7-86.9 us for layer5.0 / layer6.0's
   // downsample, 65.6-67.0 for the seg conv: profiles/r6_int8_fusions/occ2_ab.txt)
-  const int v = p.ks == 1 && p.cout_pad % kI8Variants[kI8Occ2].bco == 0 ? kI8Occ2 : (p.cin >= 128 ? 0 : 2) + wide;
-  const int o = i8_variant_override(p.ks);
-  if (o >= 0 && (o >= 2 || p.cin % 128 == 0) && p.cout_pad % kI8Variants[o].bco == 0) return o;
-  return v;
+  return p.ks == 1 && p.cout_pad % kI8Variants[kI8Occ2].bco == 0 ? kI8Occ2 : (p.cin >= 128 ? 0 : 2) + wide;
 }
 
 template <int KS>
@@ -904,23 +808,8 @@ const char* sparse_name(int ks, int base) {
   return ks == 3 ? n3[base] : n1[base];
 }
 
-#ifndef DRNMI_AUTO_PERSIST
-#define DRNMI_AUTO_PERSIST 0
-#endif
-// DRNMI_SEG_VARIANT=v: the seg classifier (1x1, cout <= 32) on conv_big variant v (A/B runs only)
-int seg_variant_override() {
-  static int v = -2;
-  if (v == -2) {
-    const char* e = getenv("DRNMI_SEG_VARIANT");
-    v = e != nullptr ? atoi(e) : -1;
-  }
-  return v;
-}
-
 int auto_variant(const drnmi_conv_args& p) {
-  if (p.ks == 1 && p.cout <= 32 && seg_variant_override() >= 0) return seg_variant_override();
   if (p.cin < 64) return p.cout % 256 == 0 ? 4 : p.cout % 128 == 0 ? 5 : 2;   // K steps of 32
-  if (DRNMI_AUTO_PERSIST && p.cout % 256 == 0) return 7;
   // cout <= 32 (the seg 1x1) also takes the 64-wide BK-32 tile: 57 vs 66 us on the D-22 seg conv
   // at batch 8 (scripts/conv_micro.py) — two workgroups fit per CU where the 32-wide 3 x 36 KB ring fits one
   // 64 -> 128 (D-22 layer4.0 conv1 / downsample, stride 2): the 64-wide BK-32 tile too, two
@@ -976,7 +865,7 @@ bool i8_conv_supported(const drnmi_conv_args& p) {
 }
 
 bool i8_strip_ok(const drnmi_conv_args& p) {
-  return i8_variant(p) == 0 && p.cin % 128 == 0 && strip_enabled() && strip_ok(p);
+  return i8_variant(p) == 0 && p.cin % 128 == 0 && strip_ok(p);
 }
 
 hipError_t launch_i8_strip(const drnmi_conv_args& p, hipStream_t s) {
@@ -996,7 +885,7 @@ hipError_t launch_i8_strip(const drnmi_conv_args& p, hipStream_t s) {
 // int8 staggered strip tile (conv_stag.hip): 128-channel K steps, so cin % 256 == 0 gives the
 // even number of 3-step tap groups the kernel walks in pairs
 bool i8_stag_ok(const drnmi_conv_args& p) {
-  return i8_strip_ok(p) && stag_enabled() && p.cin % 256 == 0 && p.x2 == nullptr;
+  return i8_strip_ok(p) && p.cin % 256 == 0 && p.x2 == nullptr;
 }
 
 int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
@@ -1043,15 +932,13 @@ bool big_conv_supported(const drnmi_conv_args& p) {
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   if (variant == kS2Row || (variant < 0 && s2row_auto(p))) return s2row_conv_dispatch(p, s);
   if (variant == kS1X2Row || (variant < 0 && s1x2row_auto(p))) return s1x2row_conv_dispatch(p, s);
-  if (variant == kRow128 || (variant < 0 && row128_auto(p))) return row128_conv_dispatch(p, s);
-  if (variant == kSeg || (variant < 0 && seg_enabled() && seg_conv_supported(p))) return seg_conv_dispatch(p, s);
   // the halo kernel (cin/cout 64-128) stays dense: it beats unit skipping on those shapes
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_dispatch(p, s);
   if (!big_conv_supported(p)) return DRNMI_ENOTSUP;
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
-  if (auto_pick && strip_enabled()) {
-    if (stag_enabled() && stag_ok(p)) variant = kStag;
+  if (auto_pick) {
+    if (stag_ok(p)) variant = kStag;
     else if (variant == 1 && strip_ok(p)) variant = kStrip;
   }
   if (variant == kStrip || variant == kStag) {
@@ -1093,14 +980,11 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   if (variant == kS2Row || (variant < 0 && s2row_auto(p))) return s2row_conv_name(p);
   if (variant == kS1X2Row || (variant < 0 && s1x2row_auto(p))) return s1x2row_conv_name(p);
-  if (variant == kRow128 || (variant < 0 && row128_auto(p))) return row128_conv_name(p);
-  if (variant == kSeg || (variant < 0 && seg_enabled() && seg_conv_supported(p)))
-    return seg_conv_supported(p) ? "conv_seg_kernel" : nullptr;
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_name(p);
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
-  if (auto_pick && strip_enabled()) {
-    if (stag_enabled() && stag_ok(p)) variant = kStag;
+  if (auto_pick) {
+    if (stag_ok(p)) variant = kStag;
     else if (variant == 1 && strip_ok(p)) variant = kStrip;
   }
   if (variant == kStag) {
@@ -1166,7 +1050,7 @@ extern "C" int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, 
     return DRNMI_EINVAL;
   if (seg_k_pad < p.cout || seg_k_pad % 8 != 0 || seg_rows < 32 || (reinterpret_cast<uintptr_t>(partials) & 15) != 0)
     return DRNMI_EINVAL;
-  if (!(big_conv_supported(p) && strip_enabled() && stag_enabled() && stag_ok(p)) || p.x2 != nullptr ||
+  if (!(big_conv_supported(p) && stag_ok(p)) || p.x2 != nullptr ||
       p.scale != nullptr || p.res != nullptr || p.cout % 256 != 0 || p.cout_pad < p.cout)
     return DRNMI_ENOTSUP;
   const hipError_t e = launch_stag_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream));

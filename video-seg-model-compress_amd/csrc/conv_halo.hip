@@ -33,9 +33,6 @@ typedef __attribute__((address_space(1))) const void g_void_t;
 __device__ uint4 g_halo_zero[64];   // zero-initialised source of padded pixels
 
 constexpr int kTR = 4, kTC = 64;     // output block: rows x columns
-#ifndef DRNMI_HALO_ABL
-#define DRNMI_HALO_ABL 0             // diagnostic builds only: bit 0 skips the patch DMA
-#endif
 constexpr int kNST = 3;              // weight ring stages (4-5 stages cost a workgroup per CU: slower)
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
@@ -168,7 +165,7 @@ conv_halo_kernel(const drnmi_conv_args p) {
     const char* zero_src = reinterpret_cast<const char*>(g_halo_zero) + lane * 16;
     const int lr = lane / CPR, ls = lane % CPR;
     const int64_t img = static_cast<int64_t>(n) * H;
-    for (int pc = wave; pc < ((DRNMI_HALO_ABL & 1) ? 0 : npieces); pc += NW) {
+    for (int pc = wave; pc < npieces; pc += NW) {
       const int row = pc * RPP + lr;
       const int pr = row / PW;
       const int ih = oh0 - p.pad + pr;
@@ -370,12 +367,9 @@ conv_halo_kernel(const drnmi_conv_args p) {
   }
 }
 
-// output-block width.  32 columns for the 64 -> 64 conv (three workgroups per CU instead of two)
-// measured the same as 64 (128.0 vs 128.3 us, D-22 layer3, 8 frames)
-#ifndef DRNMI_HALO_TC_64_64
-#define DRNMI_HALO_TC_64_64 64
-#endif
-constexpr int halo_tc(int cin, int cout) { return cin == 64 && cout == 64 ? DRNMI_HALO_TC_64_64 : 64; }
+// output-block width: 64 columns (32 for the 64 -> 64 conv, three workgroups per CU instead of two,
+// measured the same: 128.0 vs 128.3 us, D-22 layer3, 8 frames)
+constexpr int halo_tc(int /*cin*/, int /*cout*/) { return 64; }
 
 template <int CIN, int WC>
 hipError_t launch_halo(const drnmi_conv_args& p, hipStream_t s) {
@@ -423,11 +417,9 @@ int halo_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   return static_cast<int>(e);
 }
 
-#define DRNMI_STR2(x) #x
-#define DRNMI_STR(x) DRNMI_STR2(x)
 const char* halo_conv_name(const drnmi_conv_args& p) {
   if (p.cin == 64)
-    return p.cout == 64 ? "conv_halo_kernel<64, 1, " DRNMI_STR(DRNMI_HALO_TC_64_64) ">" : "conv_halo_kernel<64, 2, 64>";
+    return p.cout == 64 ? "conv_halo_kernel<64, 1, 64>" : "conv_halo_kernel<64, 2, 64>";
   return p.cout == 64 ? "conv_halo_kernel<128, 1, 64>" : "conv_halo_kernel<128, 2, 64>";
 }
 

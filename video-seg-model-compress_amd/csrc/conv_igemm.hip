@@ -264,10 +264,8 @@ constexpr TileDesc kTiles[] = {
     {128, 128, "halo"},                                    // conv_halo.hip, 4x64 pixel block
     {256, 256, "strip256"},                                // conv_big.hip, strip-staged B (3x3, wo % 256 == 0)
     {256, 256, "stag256"},                                 // the strip tile, SIMD partners half a K step apart
-    {32, 32, "seg32"},                                     // conv_seg.hip: the seg classifier (1x1, cout <= 32)
     {64, 64, "s2row"},                                     // conv_s2row.hip: stride-2 3x3 32->64 / 64->128 row walk
     {64, 64, "s1x2row"},                                   // conv_s2row.hip: stride-1 3x3 64->64 + 1x1 s2 downsample
-    {128, 64, "row128"},                                   // conv_row128.hip: stride-1 3x3 128->128 (+res) row walk
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 

@@ -30,40 +30,9 @@ namespace {
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
-#ifndef DRNMI_S2_ABL
-#define DRNMI_S2_ABL 0         // diagnostic builds only: bit 0 drops the MFMAs, bit 1 the in-loop DMA,
-#endif                         // bit 2 the output stores, bit 3 the fragment reads, bit 4 the step barrier
-#ifndef DRNMI_S2_LATEPIN
-#define DRNMI_S2_LATEPIN 1     // pin the weights into AGPRs after the first ring fill is issued (0: before)
-#endif
-#ifndef DRNMI_S2_STAMP
-#define DRNMI_S2_STAMP 0       // diagnostic builds only: per-workgroup clock stamps (drnmi_diag_s2_stamps)
-#endif
-#if DRNMI_S2_STAMP
-constexpr int kStampWgs = 8192;
-__device__ unsigned long long g_s2_stamp[kStampWgs * 8];
-// lanes 0..7 of wave 0 store one value each (per-lane addresses: plain vector stores)
-__device__ __forceinline__ void s2_stamp_store(const unsigned long long (&v)[8]) {
-  if (threadIdx.x < 8 && blockIdx.x < kStampWgs) {
-    unsigned long long x = v[0];
-#pragma unroll
-    for (int i = 1; i < 8; ++i) x = threadIdx.x == static_cast<unsigned>(i) ? v[i] : x;
-    g_s2_stamp[blockIdx.x * 8 + threadIdx.x] = x;
-  }
-}
-#endif
-#ifndef DRNMI_S2_RING32
-#define DRNMI_S2_RING32 7      // input-row slots for cin 32: 3 in use + 2 per step of DMA lead
-#endif
-#ifndef DRNMI_S2_WGS32
-#define DRNMI_S2_WGS32 2       // workgroups per CU for cin 32
-#endif
-#ifndef DRNMI_S2_RING64
-#define DRNMI_S2_RING64 7
-#endif
-#ifndef DRNMI_S2_WGS64
-#define DRNMI_S2_WGS64 2
-#endif
+// ring depth (input-row slots: 3 in use + 2 per step of DMA lead) and workgroups per CU of the
+// cin 32 / cin 64 instantiations
+constexpr int kRing32 = 7, kWgs32 = 2, kRing64 = 7, kWgs64 = 2;
 
 constexpr int kSlotB = 9 * 1024;       // input row slot: <= 8448 B used, whole 1-KB DMA pieces
 constexpr int kPieces = kSlotB / 1024;
@@ -112,10 +81,6 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-__device__ __forceinline__ void fake_rd(u32x4_t& dst, uint32_t addr) {   // DRNMI_S2_ABL bit 3
-  asm volatile("" : "+v"(dst) : "v"(addr));
-}
-
 template <int OFF>
 __device__ __forceinline__ void ds_rd16(u32x4_t& dst, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF));
@@ -125,9 +90,6 @@ template <int CIN, int RING, int WGS>
 __global__ void __launch_bounds__(256, WGS) __attribute__((amdgpu_waves_per_eu(WGS, WGS)))
 conv_s2row_kernel(const S2Params a) {
   using C = S2Cfg<CIN>;
-#if DRNMI_S2_STAMP
-  unsigned long long stamp[8] = {__builtin_amdgcn_s_memrealtime(), __builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0};
-#endif
   constexpr int D = (RING - 3) / 2;                  // steps of DMA lead
   static_assert(RING == 3 + 2 * D && D >= 1 && D <= 2, "ring");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -145,8 +107,8 @@ conv_s2row_kernel(const S2Params a) {
     for (int fm = 0; fm < 2; ++fm)
       wf[ks][fm] = *reinterpret_cast<const u32x4_t*>(a.wgt + static_cast<int64_t>(32 * wc + 16 * fm + fr) * a.k_pad +
                                                      32 * ks + 8 * fq);
-  // the AGPR pins wait for every weight load: with DRNMI_S2_LATEPIN they come after the first
-  // segment's ring-fill DMA is issued, so the weight and input-row latencies overlap (stamps:
+  // the AGPR pins wait for every weight load: they come after the first segment's ring-fill DMA
+  // is issued, so the weight and input-row latencies overlap (stamps:
   // the fill was 12.2 us of a 40 us workgroup with the pins first, scripts/s2row_stamps.py)
   auto pin_weights = [&]() {
 #pragma unroll
@@ -154,7 +116,6 @@ conv_s2row_kernel(const S2Params a) {
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm) asm volatile("" : "+a"(wf[ks][fm]));
   };
-  if constexpr (!DRNMI_S2_LATEPIN) pin_weights();
   f32x4 cinit[2];
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm) {
@@ -233,14 +194,10 @@ conv_s2row_kernel(const S2Params a) {
   };
   bool more = idx < end;
   if (more) begin_segment();
-  if constexpr (DRNMI_S2_LATEPIN) pin_weights();   // waits for the weights only: the fill stays in flight
+  pin_weights();                                   // waits for the weights only: the fill stays in flight
   while (more) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-#if DRNMI_S2_STAMP
-    if (stamp[2] == 0) stamp[2] = __builtin_amdgcn_s_memtime();   // weights + first ring landed
-    stamp[5] += yb - ya;                                            // rows walked
-#endif
 
     int s_lo = mod_ring(2 * ya - 1);                   // slot of row 2 oh - 1
     int s_dma = mod_ring(2 * ya + 2 * D);              // slot of row 2 oh + 2 D
@@ -259,8 +216,7 @@ conv_s2row_kernel(const S2Params a) {
         constexpr int E = decltype(e_c)::value;
         constexpr int KS = E / 2, FN = E % 2;
         constexpr int TAP = KS / C::SUBS, SB = KS % C::SUBS;
-        if constexpr ((DRNMI_S2_ABL & 8) != 0) fake_rd(bq[E % (PF + 1)], rb[TAP / 3] + boff[FN][TAP % 3][SB]);
-        else ds_rd16<0>(bq[E % (PF + 1)], rb[TAP / 3] + boff[FN][TAP % 3][SB]);
+        ds_rd16<0>(bq[E % (PF + 1)], rb[TAP / 3] + boff[FN][TAP % 3][SB]);
       };
       static_for<0, PF>(issue_rd);
       auto entry = [&](auto e_c) {
@@ -271,13 +227,9 @@ conv_s2row_kernel(const S2Params a) {
         asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(AHEAD) : "memory");
         __builtin_amdgcn_sched_barrier(0);
         const bf16x8 bv = __builtin_bit_cast(bf16x8, bq[E % (PF + 1)]);
-        if constexpr ((DRNMI_S2_ABL & 1) != 0) {
-          asm volatile("" :: "v"(bv), "a"(wf[KS][0]), "a"(wf[KS][1]));
-        } else {
-          acc[0][FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[KS][0]), bv, acc[0][FN], 0, 0, 0);
-          acc[1][FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[KS][1]), bv, acc[1][FN], 0, 0, 0);
-        }
-        if constexpr (E < 5 && (DRNMI_S2_ABL & 2) == 0) piece(E, r_dma, sl_dma);   // this step's DMA, one piece per MFMA pair
+        acc[0][FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[KS][0]), bv, acc[0][FN], 0, 0, 0);
+        acc[1][FN] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[KS][1]), bv, acc[1][FN], 0, 0, 0);
+        if constexpr (E < 5) piece(E, r_dma, sl_dma);   // this step's DMA, one piece per MFMA pair
         __builtin_amdgcn_sched_barrier(0);
       };
       static_for<0, C::NE>(entry);
@@ -302,36 +254,22 @@ conv_s2row_kernel(const S2Params a) {
         swap_halves(o);
         const int ow = ow0 + 32 * wp + 16 * fn + fr;
         const unsigned ob = ow < a.wo ? static_cast<unsigned>(((obase + ow) * C::COUT + 32 * wc + chunk_of_row(fq) * 8) * 2) : kOob;
-        if constexpr ((DRNMI_S2_ABL & 4) == 0) __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o.x, o.y, o.z, o.w}, ys, ob, 0, 0);
-        else asm volatile("" :: "v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w), "v"(ob));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o.x, o.y, o.z, o.w}, ys, ob, 0, 0);
       }
       // retire the DMA pieces of rows 2 oh + 2, 2 oh + 3 (issued D - 1 steps ago; younger ops stay
       // in flight: the 2 stores, and with D = 2 this step's pieces), then publish them and free
       // the slots of 2 oh - 1, 2 oh
-      if ((DRNMI_S2_ABL & 16) != 0) asm volatile("s_waitcnt vmcnt(7)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-      else if ((DRNMI_S2_ABL & 4) != 0) asm volatile("s_waitcnt vmcnt(5)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else if (D == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (D == 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(7)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-#if DRNMI_S2_STAMP
-      if (stamp[3] == 0) stamp[3] = __builtin_amdgcn_s_memtime();   // first row step done
-#endif
       s_lo = s_lo + 2 >= RING ? s_lo + 2 - RING : s_lo + 2;
       s_dma = s_dma + 2 >= RING ? s_dma + 2 - RING : s_dma + 2;
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-#if DRNMI_S2_STAMP
-    stamp[7] += 1;                                                  // segments (ring refills)
-#endif
     more = idx < end;
     if (more) begin_segment();
   }
-#if DRNMI_S2_STAMP
-  stamp[4] = __builtin_amdgcn_s_memtime();
-  stamp[6] = __builtin_amdgcn_s_memrealtime();
-  s2_stamp_store(stamp);
-#endif
 }
 
 // --- Stride-1 3x3 64 -> 64 with the block's 1x1 stride-2 downsample folded in (x2, 32 channels):
@@ -379,7 +317,6 @@ conv_s1x2row_kernel(const S1Params a) {
 #pragma unroll
       for (int fm = 0; fm < 2; ++fm) asm volatile("" : "+a"(wf[ks][fm]));
   };
-  if constexpr (!DRNMI_S2_LATEPIN) pin_weights();
   f32x4 cinit[2];
 #pragma unroll
   for (int fm = 0; fm < 2; ++fm) {
@@ -470,7 +407,7 @@ conv_s1x2row_kernel(const S1Params a) {
   };
   bool more = idx < end;
   if (more) begin_segment();
-  if constexpr (DRNMI_S2_LATEPIN) pin_weights();   // waits for the weights only: the fill stays in flight
+  pin_weights();                                   // waits for the weights only: the fill stays in flight
   while (more) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -547,18 +484,8 @@ conv_s1x2row_kernel(const S1Params a) {
 }
 
 int g_cus = 0;
-constexpr auto kern32 = &conv_s2row_kernel<32, DRNMI_S2_RING32, DRNMI_S2_WGS32>;
-constexpr auto kern64 = &conv_s2row_kernel<64, DRNMI_S2_RING64, DRNMI_S2_WGS64>;
-
-// DRNMI_S2ROW=0 keeps these convs on conv_big (A/B runs)
-bool s2row_enabled() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("DRNMI_S2ROW");
-    on = (e != nullptr && e[0] == '0') ? 0 : 1;
-  }
-  return on == 1;
-}
+constexpr auto kern32 = &conv_s2row_kernel<32, kRing32, kWgs32>;
+constexpr auto kern64 = &conv_s2row_kernel<64, kRing64, kWgs64>;
 
 }  // namespace
 
@@ -573,7 +500,7 @@ bool s2row_conv_supported(const drnmi_conv_args& p) {
          static_cast<int64_t>(p.n) * p.ho * p.wo * p.cout * 2 < (int64_t(1) << 31);
 }
 
-bool s2row_auto(const drnmi_conv_args& p) { return s2row_enabled() && s2row_conv_supported(p); }
+bool s2row_auto(const drnmi_conv_args& p) { return s2row_conv_supported(p); }
 
 bool s1x2row_conv_supported(const drnmi_conv_args& p) {
   return p.dtype == DRNMI_BF16 && p.out_dtype == DRNMI_BF16 && p.cin == 64 && p.cout == 64 && p.ks == 3 &&
@@ -585,7 +512,7 @@ bool s1x2row_conv_supported(const drnmi_conv_args& p) {
          static_cast<int64_t>(p.n) * p.h2 * p.w2 * 64 < (int64_t(1) << 31);
 }
 
-bool s1x2row_auto(const drnmi_conv_args& p) { return s2row_enabled() && s1x2row_conv_supported(p); }
+bool s1x2row_auto(const drnmi_conv_args& p) { return s1x2row_conv_supported(p); }
 
 const char* s1x2row_conv_name(const drnmi_conv_args& p) {
   return s1x2row_conv_supported(p) ? "conv_s1x2row_kernel" : nullptr;
@@ -629,10 +556,8 @@ int s1x2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t st) {
 
 const char* s2row_conv_name(const drnmi_conv_args& p) {
   if (!s2row_conv_supported(p)) return nullptr;
-#define DRNMI_S2_STR2(x) #x
-#define DRNMI_S2_STR(x) DRNMI_S2_STR2(x)
-  return p.cin == 32 ? "conv_s2row_kernel<32, " DRNMI_S2_STR(DRNMI_S2_RING32) ", " DRNMI_S2_STR(DRNMI_S2_WGS32) ">"
-                     : "conv_s2row_kernel<64, " DRNMI_S2_STR(DRNMI_S2_RING64) ", " DRNMI_S2_STR(DRNMI_S2_WGS64) ">";
+  static_assert(kRing32 == 7 && kWgs32 == 2 && kRing64 == 7 && kWgs64 == 2, "kernel names below");
+  return p.cin == 32 ? "conv_s2row_kernel<32, 7, 2>" : "conv_s2row_kernel<64, 7, 2>";
 }
 
 int s2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t st) {
@@ -643,15 +568,15 @@ int s2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t st) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern32), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       s2_lds_bytes<DRNMI_S2_RING32>());
+                                       s2_lds_bytes<kRing32>());
     if (e == hipSuccess)
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern64), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              s2_lds_bytes<DRNMI_S2_RING64>());
+                              s2_lds_bytes<kRing64>());
     if (e != hipSuccess) return static_cast<int>(e);
     g_cus = cus;
   }
   const bool c32 = p.cin == 32;
-  const int wgs = g_cus * (c32 ? DRNMI_S2_WGS32 : DRNMI_S2_WGS64);   // persistent: WGS workgroups per CU
+  const int wgs = g_cus * (c32 ? kWgs32 : kWgs64);   // persistent: WGS workgroups per CU
   S2Params a;
   a.x = static_cast<const uint16_t*>(p.x);
   a.wgt = static_cast<const uint16_t*>(p.wgt);
@@ -671,24 +596,9 @@ int s2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t st) {
   a.total = static_cast<int>(total);
   a.per_wg = (a.total + wgs - 1) / wgs;
   const int grid = (a.total + a.per_wg - 1) / a.per_wg;
-  if (c32) hipLaunchKernelGGL(kern32, dim3(grid), dim3(256), s2_lds_bytes<DRNMI_S2_RING32>(), st, a);
-  else hipLaunchKernelGGL(kern64, dim3(grid), dim3(256), s2_lds_bytes<DRNMI_S2_RING64>(), st, a);
+  if (c32) hipLaunchKernelGGL(kern32, dim3(grid), dim3(256), s2_lds_bytes<kRing32>(), st, a);
+  else hipLaunchKernelGGL(kern64, dim3(grid), dim3(256), s2_lds_bytes<kRing64>(), st, a);
   return static_cast<int>(hipGetLastError());
 }
 
 }  // namespace drnmi
-
-#if DRNMI_S2_STAMP
-// diagnostic builds: copy the per-workgroup stamps of the last conv_s2row_kernel launch to the host
-// ([wg][8]: realtime start, memtime start, after the first ring fill, after the first row step,
-// memtime end, rows walked, realtime end, segments)
-extern "C" int drnmi_diag_s2_stamps(unsigned long long* host, int wgs) {
-  if (host == nullptr || wgs <= 0 || wgs > drnmi::kStampWgs) return -1;
-  return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(drnmi::g_s2_stamp), sizeof(unsigned long long) * 8 * wgs, 0,
-                                              hipMemcpyDeviceToHost));
-}
-extern "C" int drnmi_diag_s2_stamps_clear() {
-  static unsigned long long zero[drnmi::kStampWgs * 8] = {};
-  return static_cast<int>(hipMemcpyToSymbol(HIP_SYMBOL(drnmi::g_s2_stamp), zero, sizeof(zero), 0, hipMemcpyHostToDevice));
-}
-#endif

@@ -5,39 +5,6 @@
 #include "conv_tile.h"
 #include "kernels.h"
 
-#ifndef DRNMI_STAG_LGKM
-#define DRNMI_STAG_LGKM 0   // diagnostic: explicit counted lgkmcnt before each MFMA group
-#endif
-#ifndef DRNMI_STAG_ASM
-#define DRNMI_STAG_ASM 1    // fragment reads as inline-asm ds_read_b128 with hand-counted lgkmcnt (hipcc's
-                            // own waits drain every second group: 0.6-0.8 % slower, profiles/r4a_stag_ab)
-#endif
-#ifndef DRNMI_STAG_ABL
-#define DRNMI_STAG_ABL 0    // diagnostic builds only: bit 0 drops the in-loop DMA, bit 1 the MFMAs,
-                            // bit 2 the fragment reads (registers keep stale values), bit 3 the
-                            // MFMAs of 2 of the 8 16-row blocks per wave (the 25 % of 16 x 32
-                            // weight units a 16 x 16 BlockPruner mask at 50 % leaves all-zero),
-                            // bit 4 the MFMAs of a pseudo-random 25 % of those units
-#endif
-#ifndef DRNMI_STAG_OLDINIT
-#define DRNMI_STAG_OLDINIT 0  // diagnostic: residual loaded and added before the prologue DMA (A/B)
-#endif
-#ifndef DRNMI_STAG_MAP
-#define DRNMI_STAG_MAP 0    // tile deal: 0 XCD-major rows x both channel blocks; 1 XCD-stationary channel
-#endif                      // block (XCD x keeps block x % 2, XCD pairs split the pixel tiles)
-#ifndef DRNMI_STAG_XAUX
-#define DRNMI_STAG_XAUX 0   // cache policy of the input-strip DMA (2 = nt: streaming)
-#endif
-#ifndef DRNMI_STAG_WAUX
-#define DRNMI_STAG_WAUX 0   // cache policy of the weight DMA
-#endif
-#ifndef DRNMI_STAG_SERP
-#define DRNMI_STAG_SERP 0   // diagnostic: odd rounds of tiles (blockIdx / 256) walk the tap groups in reverse
-#endif                      // order, so a round starts on the weight slices the previous one ended on (L2)
-#ifndef DRNMI_STAG_PRIO
-#define DRNMI_STAG_PRIO 0   // diagnostic: s_setprio 1 for the lagging half (waves 4-7)
-#endif
-
 namespace drnmi {
 namespace {
 
@@ -76,17 +43,10 @@ namespace {
 //
 // WCO = channels per wave (tile = 2 WCO output channels x 256 pixels): 128 (the 256-channel tile
 // of layer5-8) or 64 (128-channel convs: D-22 layer4); GR = WCO / 32 MFMA groups per substep.
-// Tile deal (workgroups go to XCD bid % 8).  Default: XCD-major -- XCD x takes a contiguous run of
-// (pixel tile, channel block) tiles, i.e. its rows x both channel blocks.  DRNMI_STAG_MAP 1: with
-// two channel blocks, XCD x keeps block x % 2 for its whole share and XCD pair x / 2 takes a
-// quarter of the pixel tiles, in the same row order on both XCDs of the pair.
-__device__ __forceinline__ int stag_tile(int bid, int ntiles, int nco) {
-  if (DRNMI_STAG_MAP == 1 && nco == 2 && ntiles % 8 == 0) {
-    const int xcd = bid & 7, j = bid >> 3;
-    return ((xcd >> 1) * (ntiles / 8) + j) * 2 + (xcd & 1);
-  }
-  return xcd_remap2(bid, ntiles);
-}
+// Tile deal (workgroups go to XCD bid % 8): XCD-major -- XCD x takes a contiguous run of (pixel
+// tile, channel block) tiles, i.e. its rows x both channel blocks (an XCD-stationary channel block
+// fetched 19 % more at the same time).
+__device__ __forceinline__ int stag_tile(int bid, int ntiles, int /*nco*/) { return xcd_remap2(bid, ntiles); }
 
 // SEGF (the labels-only video path's last conv, drnmi_conv_stag_seg): the conv's own output is not
 // stored; its epilogue feeds the seg classifier (1x1 512 -> 19 + bias, lmodels/drnseg.py:278-284)
@@ -148,14 +108,11 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
   const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.wgt), 0, p.cout_pad * p.k_pad * K::ESZ, 0x00020000);
   typedef __attribute__((address_space(3))) void lds_t;
-  bool in_loop = false;                              // DRNMI_STAG_ABL bit 0: no DMA once the loop runs
   auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, int soff, int lds_byte) {   // weights
-    if ((DRNMI_STAG_ABL & 1) && in_loop) return;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, DRNMI_STAG_WAUX);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, 0);
   };
   auto dma_x = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, int soff, int lds_byte) { // input strips
-    if ((DRNMI_STAG_ABL & 1) && in_loop) return;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, DRNMI_STAG_XAUX);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, 0);
   };
   // weight rows (wave*4 + i)*8 + lrow: the swizzle depends on i only through its parity
   uint32_t a_off[2];
@@ -167,9 +124,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
   constexpr uint32_t kOOB = 0x80000000u;             // beyond every buffer (sizes < 2^31)
 
   // weight piece i (rows (wave*4 + i)*8 .. +8) of K step kt into A stage `stage`
-  const bool serp = DRNMI_STAG_SERP != 0 && ((blockIdx.x >> 8) & 1) != 0;
   auto issue_a = [&](int kt, int stage, int i) {
-    if (serp && kt < nk) kt = 3 * (ngroups - 1 - kt / 3) + kt % 3;
     const int cb = kt / 9;
     const int tap = kt - cb * 9;
     const int k0 = (X2 && kt >= nk) ? 9 * cin + (kt - nk) * BK : (tap << lc) + cb * BK;
@@ -177,7 +132,6 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
   };
   // strip share sh of group g (channel block g / 3, tap row g % 3) into strip buffer `buf`
   auto issue_strip = [&](int g, int buf, int sh) {
-    if (serp) g = ngroups - 1 - g;
     const int j = wave + 8 * sh;
     if (j >= kStripPieces) return;                   // wave-uniform
     const int R = j * 8 + lrow;
@@ -227,17 +181,12 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
 
   typename K::acc acc[FM][4];
   typename K::frag af[2][2], bfr[2][4];
+  // fragment reads: inline-asm ds_read_b128 with compile-time offsets and hand-counted lgkmcnt
+  // (hipcc's own waits drained every second group: 0.6-0.8 % slower, profiles/r4a_stag_ab)
   auto rd = [&](typename K::frag& dst, uint32_t base, auto off_c) {
     constexpr int OFF = decltype(off_c)::value;
-    if constexpr ((DRNMI_STAG_ABL & 4) != 0) {
-      if (in_loop) { asm volatile("" : "+v"(dst)); return; }
-    }
-#if DRNMI_STAG_ASM
     // base: a byte offset into smem, which is LDS address 0 (the kernel's only LDS object)
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(OFF));
-#else
-    dst = *reinterpret_cast<const typename K::frag*>(smem + base + OFF);
-#endif
   };
   auto load_a = [&](typename K::frag (&dst)[2], auto stage_c, auto u_c, auto qg_c) {
     constexpr int ST = decltype(stage_c)::value, U_ = decltype(u_c)::value, QG = decltype(qg_c)::value;
@@ -264,9 +213,6 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
   uint4 rv[FM / 2][4];
   float4 shv[FM];
   if constexpr (K::ESZ == 2) {
-#if DRNMI_STAG_OLDINIT
-    init_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
-#else
     if (split_init) {
       // only loads here: a register written from a pending load before the DMA issue would make
       // the compiler wait (vmcnt(0) at the join) ahead of it
@@ -276,7 +222,6 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
     } else {
       init_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
     }
-#endif
   } else {
     zero_tile(acc);
   }
@@ -284,7 +229,6 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
   for (int i = 0; i < AI; ++i) issue_a(0, 0, i);
 #pragma unroll
   for (int sh = 0; sh < 5; ++sh) issue_strip(0, 0, sh);
-#if !DRNMI_STAG_OLDINIT
   if constexpr (K::ESZ == 2) {
     if (split_init) {
 #pragma unroll
@@ -294,16 +238,11 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
       if (has_res) add_residual(acc, rv, fr);
     }
   }
-#endif
   asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  in_loop = true;
   if (wc == 1) {                                     // the stagger: waves 4-7 sit out phase 0
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-#if DRNMI_STAG_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
   }
 
   // one phase = substep U of K step t = 3 g + KW; GP = g & 1 (strip buffer), stage = t & 1
@@ -324,10 +263,6 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
       load_b(bfr[0], IG{}, IK{}, Z{});
       load_a(af[0], IS{}, Z{}, Z{});
     }
-    // DRNMI_STAG_ABL bit 4: a pseudo-random 25 % of the (16-row block, substep) units per wave
-    // skip their MFMAs (the dead-unit pattern of a random 50 % 16 x 16 BlockPruner mask)
-    const uint32_t abl_hash = __builtin_amdgcn_readfirstlane(
-        (static_cast<uint32_t>(wave + 1) * 2654435761u) ^ (static_cast<uint32_t>(t) * 40503u + U * 977u + 0x9e3779b9u) * 2246822519u);
     auto group_reads = [&](auto qg_c) {
       constexpr int QG = decltype(qg_c)::value;
       if constexpr (QG < GR - 1) {
@@ -343,23 +278,16 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
       if (qg == 1) group_reads(std::integral_constant<int, 1>{});
       if (qg == 2) group_reads(std::integral_constant<int, 2>{});
       if (qg == 3) group_reads(std::integral_constant<int, 3>{});
-#if DRNMI_STAG_LGKM || DRNMI_STAG_ASM
       // this group's fragments: everything but the reads issued after them (the next group's
       // 2, or 6 when the second substep's B and first A went out)
       if (qg < GR - 1) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
       else if (U == 0) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int fn = 0; fn < 4; ++fn)
-          if constexpr ((DRNMI_STAG_ABL & 2) != 0) asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
-          else if ((DRNMI_STAG_ABL & 8) != 0 && h == 1 && (qg & 1) == 0) asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
-          else if ((DRNMI_STAG_ABL & 16) != 0 && ((abl_hash >> ((qg * 2 + h) * 2)) & 3u) == 0u)
-            asm volatile("" :: "v"(af[qg & 1][h]), "v"(bfr[U][fn]));
-          else acc[qg * 2 + h][fn] = K::mma(af[qg & 1][h], bfr[U][fn], acc[qg * 2 + h][fn]);
+        for (int fn = 0; fn < 4; ++fn) acc[qg * 2 + h][fn] = K::mma(af[qg & 1][h], bfr[U][fn], acc[qg * 2 + h][fn]);
       if constexpr (U == 0) { if (qg < AI) issue_a(ta, STAGE ^ 1, qg); }
       if constexpr (KW == 0 && U == 1) { if (qg < 2) issue_next_strip(g, GP ^ 1, qg); }
       if constexpr (KW == 1 && U == 0) { if (qg == 1) issue_next_strip(g, GP ^ 1, 2); }
@@ -399,9 +327,6 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
   }
-#if DRNMI_STAG_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   if constexpr (X2) {
     // x2 steps, all waves aligned: step nk + e reads A stage (nk + e) & 1 and strip buffer
     // (ngroups + e) & 1 (both landed: the last phases waited vmcnt(0) before their barriers)
@@ -504,7 +429,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
     return;
   }
   if constexpr (K::ESZ == 2) {
-    if (fast_epi && !DRNMI_STAG_OLDINIT) store_tile_x4<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
+    if (fast_epi) store_tile_x4<FM, WCO, 4>(p, acc, px0, co0, wc, wp, fr, fq);
     else store_tile<FM, WCO, 4, false>(p, acc, px0, co0, wc, wp, fr, fq);
   } else {
     // whole tile of a dense int8 NHWC output (M % 256 == 0 here): 16-B pieces

@@ -151,9 +151,6 @@ __device__ __forceinline__ void init_tile(const drnmi_conv_args& p, f32x4 (&acc)
 // the low halves and quad 4 + fq (fragment 2 f2 + 1) in the high halves, and back.  Half the
 // instructions, 64 contiguous bytes per pixel; the values are the same, so the sums are.
 // (chunk_of_row, swap_halves: common.h)
-#ifndef DRNMI_EPI128
-#define DRNMI_EPI128 1   // store_tile_x4 writes whole 128-B lines (0: 64-B pieces, A/B)
-#endif
 template <int FM, int WCO, int FN>
 __device__ __forceinline__ void load_residual(const drnmi_conv_args& p, uint4 (&rq)[FM / 2][FN], int px0, int co0, int wc,
                                               int wp, int fr, int fq) {
@@ -162,7 +159,6 @@ __device__ __forceinline__ void load_residual(const drnmi_conv_args& p, uint4 (&
 #pragma unroll
   for (int fn = 0; fn < FN; ++fn) {
     const int64_t m = px0 + wp * 16 * FN + fn * 16 + fr;
-#if DRNMI_EPI128
     // whole 128-B lines, the mirror of store_tile_x4: rq[2 L] / rq[2 L + 1] hold the pieces of
     // pixels 0-7 / 8-15 of groups (2 L, 2 L + 1); add_residual trades them back (lanes fr ^ 8)
     static_assert((FM / 2) % 2 == 0, "line pairs");
@@ -174,15 +170,10 @@ __device__ __forceinline__ void load_residual(const drnmi_conv_args& p, uint4 (&
       rq[2 * L][fn] = *reinterpret_cast<const uint4*>(res + m0 * p.cout + ca + (lo ? 0 : 32));
       rq[2 * L + 1][fn] = *reinterpret_cast<const uint4*>(res + m1 * p.cout + ca + (lo ? 32 : 0));
     }
-#else
-#pragma unroll
-    for (int f2 = 0; f2 < FM / 2; ++f2) rq[f2][fn] = *reinterpret_cast<const uint4*>(res + m * p.cout + c + f2 * 32);
-#endif
   }
 }
 template <int FM, int FN>
 __device__ __forceinline__ void add_residual(f32x4 (&acc)[FM][FN], uint4 (&rq)[FM / 2][FN], int fr) {
-#if DRNMI_EPI128
   const bool lo = fr < 8;
 #pragma unroll
   for (int L = 0; L < FM / 4; ++L)
@@ -199,7 +190,6 @@ __device__ __forceinline__ void add_residual(f32x4 (&acc)[FM][FN], uint4 (&rq)[F
       rq[2 * L][fn] = own;
       rq[2 * L + 1][fn] = r;
     }
-#endif
 #pragma unroll
   for (int f2 = 0; f2 < FM / 2; ++f2)
 #pragma unroll
@@ -244,7 +234,6 @@ __device__ __forceinline__ void store_tile_x4(const drnmi_conv_args& p, const f3
       o[f2] = make_uint4(w[0], w[1], w[2], w[3]);
       swap_halves(o[f2]);
     }
-#if DRNMI_EPI128
     // whole 128-B lines: lanes fr and fr ^ 8 (DPP row_ror:8) trade their odd-group chunks, so one
     // instruction writes groups (2 L, 2 L + 1) of pixels 0-7 and the next those of pixels 8-15
     const bool lo = fr < 8;
@@ -266,10 +255,6 @@ __device__ __forceinline__ void store_tile_x4(const drnmi_conv_args& p, const f3
       *reinterpret_cast<uint4*>(y1) = d1;
     }
     if constexpr ((FM / 2) % 2 == 1) *reinterpret_cast<uint4*>(y + m * p.cout + c + (FM / 2 - 1) * 32) = o[FM / 2 - 1];
-#else
-#pragma unroll
-    for (int f2 = 0; f2 < FM / 2; ++f2) *reinterpret_cast<uint4*>(y + m * p.cout + c + f2 * 32) = o[f2];
-#endif
   }
 }
 template <int FM, int WCO, int FN = 4, bool DEFER = false>
@@ -463,7 +448,7 @@ __device__ __forceinline__ void store_tile_i8_x4(const drnmi_conv_args& p, const
   const bool lo = fr < 8;
   // 128-B lines when the wave's channels span whole lines (NG even): groups (2 L, 2 L + 1) of
   // pixels 0-7, then of pixels 8-15, lanes fr and fr ^ 8 trading the odd group (DPP row_ror:8)
-  constexpr bool LINES = DRNMI_EPI128 && NG % 2 == 0;
+  constexpr bool LINES = NG % 2 == 0;
   auto trade = [](uint4 v) {
     uint4 r;
     r.x = __builtin_amdgcn_update_dpp(0u, v.x, 0x128, 0xf, 0xf, false);

@@ -37,9 +37,6 @@ typedef __attribute__((address_space(1))) const void g_void_t;
 
 __device__ uint4 g_x6_zero[64];   // zero-initialised: the source of padded taps / rows
 
-#ifndef DRNMI_X6_PIPE
-#define DRNMI_X6_PIPE 1     // 0: the round-3 step (A planes read right before their MFMA group, B split up front)
-#endif
 
 constexpr int kBPX = 256;   // pixels per tile
 constexpr int kBK = 32;     // input channels per K step
@@ -188,7 +185,6 @@ conv_x6_kernel(const drnmi_conv_args p) {
 
   for (int t = 0; t < C::NST - 1 && t < nk; ++t) issue(t, t);
 
-#if DRNMI_X6_PIPE
   const uint32_t a_lane = static_cast<uint32_t>((wc * WCO + fr) * 64 + swz64(fr, fq) * 16);
   const uint32_t b_lane0 = static_cast<uint32_t>((wp * 64 + fr) * 128 + swz128(fr, 2 * fq) * 16);
   const uint32_t b_lane1 = static_cast<uint32_t>((wp * 64 + fr) * 128 + swz128(fr, 2 * fq + 1) * 16);
@@ -308,86 +304,6 @@ conv_x6_kernel(const drnmi_conv_args p) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last step's re-fetch
-#else
-  // per step: B fragments read and split once; then per channel fragment fm, its three A
-  // planes are read and the next step's DMA pieces go out between the MFMA groups (PPF per
-  // group, behind the A reads), pinned with sched_barrier (a one-group-ahead A prefetch needs
-  // 12 more VGPRs than the 2-waves-per-SIMD budget leaves: it spilled)
-  constexpr int PPF = (C::GLDS + C::FM - 1) / C::FM;
-  for (int t = 0; t < nk; ++t) {
-    const int newer = ((nk - 1) < (t + C::NST - 2) ? (nk - 1) : (t + C::NST - 2)) - t;
-    if (C::NST >= 3 && newer >= 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(C::GLDS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    // the stage read at step t-1 is free for every wave: refill it with step t + NST - 1
-    const bool nxt = t + C::NST - 1 < nk;
-    const StepP spn = step_params(nxt ? t + C::NST - 1 : t);
-    const int nst = (t + C::NST - 1) % C::NST;
-
-    const char* sa = smem + (t % C::NST) * C::STAGE;
-    const char* sb = sa + C::A_BYTES;
-    // B: all fragments read now; fn 0, 1 split now, fn 2, 3 inside the first MFMA group so
-    // their VALU work overlaps the MFMAs of fn 0, 1 (each accumulator keeps its product order)
-    bf16x8 b1[C::FN], b2[C::FN], b3[C::FN];
-    float4 blo[C::FN], bhi[C::FN];
-#pragma unroll
-    for (int fn = 0; fn < C::FN; ++fn) {
-      const int r = wp * 64 + fn * 16 + fr;
-      blo[fn] = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq) * 16);
-      bhi[fn] = *reinterpret_cast<const float4*>(sb + r * 128 + swz128(r, 2 * fq + 1) * 16);
-    }
-#pragma unroll
-    for (int fn = 0; fn < C::FN / 2; ++fn) split3(blo[fn], bhi[fn], b1[fn], b2[fn], b3[fn]);
-    auto load_a = [&](bf16x8 (&dst)[3], int fm) {
-      const int r = wc * WCO + fm * 16 + fr;
-      const char* ar = sa + r * 64 + swz64(r, fq) * 16;
-      dst[0] = *reinterpret_cast<const bf16x8*>(ar);
-      dst[1] = *reinterpret_cast<const bf16x8*>(ar + C::A_PLANE);
-      dst[2] = *reinterpret_cast<const bf16x8*>(ar + 2 * C::A_PLANE);
-    };
-    // the six products of fragments fn0 <= fn < fn1, smallest terms first, independent
-    // accumulators between dependent MFMAs
-    auto mfma6 = [&](int fm, const bf16x8 (&af)[3], int fn0, int fn1) {
-      const bf16x8& a1 = af[0];
-      const bf16x8& a2 = af[1];
-      const bf16x8& a3 = af[2];
-#pragma unroll
-      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, b1[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b2[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b3[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b1[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b2[fn], acc[fm][fn], 0, 0, 0);
-#pragma unroll
-      for (int fn = fn0; fn < fn1; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[fn], acc[fm][fn], 0, 0, 0);
-    };
-#pragma unroll
-    for (int fm = 0; fm < C::FM; ++fm) {
-      bf16x8 af[3];
-      load_a(af, fm);
-      // the group's DMA pieces go out while its three A reads are in flight
-      if (nxt) {
-#pragma unroll
-        for (int k = 0; k < PPF; ++k)
-          if (fm * PPF + k < C::GLDS) issue_piece(spn, nst, fm * PPF + k);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (fm == 0) {
-        mfma6(0, af, 0, C::FN / 2);
-#pragma unroll
-        for (int fn = C::FN / 2; fn < C::FN; ++fn) split3(blo[fn], bhi[fn], b1[fn], b2[fn], b3[fn]);
-        mfma6(0, af, C::FN / 2, C::FN);
-      } else {
-        mfma6(fm, af, 0, C::FN);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#endif
 
   // --- split-K: raw fp32 partial sums [split][m][cout]; x6_splitk_epilogue_kernel finishes
   if (gridDim.y > 1) {

@@ -72,49 +72,14 @@ constexpr int kRowB = 1040;              // ring row: image byte o at o (copy A)
 constexpr int kCopyB = 516;              //   (copy B: 8-B aligned where o % 8 == 4)
 constexpr int kXSp = 34 * 16;            // exchange: [plane 2][sp 2][pair slot 34][16 B], pair r at r + 1
 constexpr int kXSlot = 4 * kXSp;
-constexpr int kXSlots = 6;               // exchange rows per activation (row mod 6)
-constexpr int kLdsZero = kRing * kRowB + 2 * kXSlots * kXSlot;
-constexpr int kLds = kLdsZero + kCTabB;                 // + the stem shift table
-constexpr uint32_t kF16Hi = 0x64646464u;
-#ifndef DRNMI_FR_PIN
-#define DRNMI_FR_PIN 0          // 1: keep the step's LDS operand reads ahead of its MFMAs (measured slower: 360 vs 342 us)
-#endif
-#ifndef DRNMI_FR_AGPRW
-#define DRNMI_FR_AGPRW 1        // weight fragments pinned to AGPRs
-#endif
-#ifndef DRNMI_FR_ILV
-#define DRNMI_FR_ILV 1          // v3: pin the MFMA / epilogue interleave (sched_barrier between groups)
-#endif
-#if DRNMI_FR_ILV
+constexpr uint32_t kF16Hi = 0x64646464u;            // v_perm source of the f16 exponent byte 0x64
+// front3_kernel's pinned MFMA / epilogue interleave: a sched_barrier between groups, epilogue
+// values kept where they are computed (else they sink to their first use, out of the MFMA shadow)
+// and their inputs read there (else the packing hoists to where they are ready, ahead of MFMAs)
 #define FR_SB() __builtin_amdgcn_sched_barrier(0)
-// keep an epilogue value where it is computed (else it sinks to its first use, out of the MFMA shadow)
 #define FR_PINV(x) ({ uint32_t _v = (x); asm volatile("" : "+v"(_v)); _v; })
-// ... and read its inputs there (else the packing hoists to where they are ready, ahead of MFMAs)
-#ifndef DRNMI_FR_PINF
-#define DRNMI_FR_PINF 1
-#endif
-#if DRNMI_FR_PINF
 #define FR_PINF(x) ({ float _f = (x); asm volatile("" : "+v"(_f)); _f; })
-#else
-#define FR_PINF(x) (x)
-#endif
-#else
-#define FR_SB() do {} while (0)
-#define FR_PINV(x) (x)
-#define FR_PINF(x) (x)
-#endif
-#ifndef DRNMI_FR_CSREG
-#define DRNMI_FR_CSREG 0          // 1: interior walks keep the stem's row-case-3 offsets in registers
-#endif
-#ifndef DRNMI_FR_FETCH
-#define DRNMI_FR_FETCH 8          // layer2 MFMA after which the next step's operands are fetched
-#endif
-#ifndef DRNMI_FR_V
-#define DRNMI_FR_V 3            // 3: front3_kernel (register-carried windows), 2: front_kernel
-#endif
-#ifndef DRNMI_FR_ABL
-#define DRNMI_FR_ABL 0          // diagnostic builds only: bit 0/1/2 skip the stem/layer1/layer2 MFMAs
-#endif                          // (operands still read), bit 3 the output stores               // v_perm source of the f16 exponent byte 0x64
+constexpr int kFetchAt = 8;               // layer2 MFMA after which the next step's operands are fetched
 
 struct FrontParams {
   const uint8_t* x;
@@ -139,268 +104,14 @@ __device__ __forceinline__ f16x8 ld_frag_f16(const char* row, int off) {
 __device__ __forceinline__ bf16x8 ld_frag_bf16(const char* p) {
   return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
 }
-template <int ABL = 0>
 __device__ __forceinline__ f32x16 mfma_f16(const uint4& a, const f16x8& b, const f32x16& c) {
-  if constexpr ((DRNMI_FR_ABL & ABL) != 0) {
-    asm volatile("" :: "v"(__builtin_bit_cast(u32x4_t, a)), "v"(__builtin_bit_cast(u32x4_t, b)));
-    return c;
-  } else {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), b, c, 0, 0, 0);
-  }
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), b, c, 0, 0, 0);
 }
-template <int ABL = 0>
 __device__ __forceinline__ f32x16 mfma_bf16(const uint4& a, const bf16x8& b, const f32x16& c) {
-  if constexpr ((DRNMI_FR_ABL & ABL) != 0) {
-    asm volatile("" :: "v"(__builtin_bit_cast(u32x4_t, a)), "v"(__builtin_bit_cast(u32x4_t, b)));
-    return c;
-  } else {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
-  }
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
-front_kernel(const FrontParams a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const ring = smem;
-  char* const xs0 = smem + kRing * kRowB;                 // stem rows (slot = row mod 6)
-  char* const xs1 = xs0 + kXSlots * kXSlot;               // layer1 rows (slot = row mod 6)
-  float* const ctab = reinterpret_cast<float*>(xs1 + kXSlots * kXSlot);   // [7][7][16] stem shifts
-  const int lane = threadIdx.x;
-  const int r = lane & 31, hh = lane >> 5;
-
-  const uint4* pk = reinterpret_cast<const uint4*>(a.pack);
-  uint4 as[kFS], a1[kF1], a2[kF2];
-#pragma unroll
-  for (int m = 0; m < kFS; ++m) as[m] = pk[m * 64 + lane];
-#pragma unroll
-  for (int m = 0; m < kF1; ++m) a1[m] = pk[(kFS + m) * 64 + lane];
-#pragma unroll
-  for (int m = 0; m < kF2; ++m) a2[m] = pk[(kFS + kF1 + m) * 64 + lane];
-  if constexpr (DRNMI_FR_AGPRW) {
-    // keep the 32 weight fragments in AGPRs (MFMA A operands may be AGPRs): the VGPRs are left to
-    // the operand fragments and the accumulators, whose epilogue VALU would otherwise copy them out
-#pragma unroll
-    for (int m = 0; m < kFS; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, as[m]); asm volatile("" : "+a"(t)); as[m] = __builtin_bit_cast(uint4, t); }
-#pragma unroll
-    for (int m = 0; m < kF1; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, a1[m]); asm volatile("" : "+a"(t)); a1[m] = __builtin_bit_cast(uint4, t); }
-#pragma unroll
-    for (int m = 0; m < kF2; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, a2[m]); asm volatile("" : "+a"(t)); a2[m] = __builtin_bit_cast(uint4, t); }
-  }
-  const float* c1t = reinterpret_cast<const float*>(a.pack + kOffC1);
-  const float* c2t = reinterpret_cast<const float*>(a.pack + kOffC2);
-  f32x16 c1, c2;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    c1[j] = c1t[j];
-    c2[j] = c2t[(j & 3) + 8 * (j >> 2) + 4 * hh];      // 32x32 D row (j&3) + 8(j>>2) + 4h = channel
-  }
-  for (int i = lane * 16; i < kLdsZero; i += 64 * 16) *reinterpret_cast<uint4*>(smem + i) = make_uint4(0, 0, 0, 0);
-  for (int i = lane * 4; i < kCTabB; i += 64 * 4)
-    *reinterpret_cast<float*>(reinterpret_cast<char*>(ctab) + i) =
-        *reinterpret_cast<const float*>(a.pack + kOffC0 + i);
-
-  const int H = a.h, W = a.w;
-  const int rowb = 3 * W;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.x), 0, a.n * H * rowb, 0x00020000);
-  const __amdgpu_buffer_rsrc_t ys =
-      __builtin_amdgcn_make_buffer_rsrc(a.y, 0, a.n * a.h2 * a.w2 * 64, 0x00020000);
-  constexpr unsigned kOob = 0x80000000u;                 // buffer offset past num_records: loads 0, stores dropped
-
-  int idx = blockIdx.x * a.per_wave;
-  const int end = min(idx + a.per_wave, a.total);
-  while (idx < end) {
-    const int seg = idx / a.h2;
-    const int ya = idx - seg * a.h2;
-    const int yb = min(a.h2, ya + (end - idx));
-    idx += yb - ya;
-    const int n = seg / a.ns, s = seg - n * a.ns;
-
-    const int X0 = kCols * s;
-    const int S0 = 2 * X0 - 3;                       // stem / layer1 column of pair 0, sub-pixel 0
-    const int col = S0 + 2 * r + hh;                 // this lane's stem / layer1 pixel
-    const uint32_t cmask = static_cast<unsigned>(col) < static_cast<unsigned>(W) ? 0xffffffffu : 0u;
-    const int ccl = col < 3 ? col : (col >= W - 3 ? 6 - (W - 1 - col) : 3);
-    const int cc = ccl < 0 ? 0 : (ccl > 6 ? 6 : ccl);
-    // frame bytes: image byte t <-> row byte fb0 + t (fb0 % 4 == 0); lane l converts t = 4l .. 4l+3
-    const int fb0 = 6 * X0 - 20;
-    const int cb = fb0 + 4 * lane;
-    auto bv = [&](int k) { return static_cast<unsigned>(cb + k) < static_cast<unsigned>(rowb); };
-    const uint32_t fm0 = (bv(0) ? 0x0000ffffu : 0u) | (bv(1) ? 0xffff0000u : 0u);
-    const uint32_t fm1 = (bv(2) ? 0x0000ffffu : 0u) | (bv(3) ? 0xffff0000u : 0u);
-    // stem B: pair r's window chunk j at image byte 4 + 12 r + 16 j (f16 image = 2 B per byte)
-    const int oP = 4 + 12 * r + 16 * hh;             // P fragments: chunk j = lane half
-    const int oX = 36 + 12 * r;                      // X fragments: chunk 2 of rows fr + lane half
-    const int rdP = (r & 1) ? oP : kCopyB + oP;
-    const int rdX = ((r & 1) ? oX : kCopyB + oX) + hh * kRowB;     // lane half h reads row fr + h
-    // exchange offsets (plane 1 = +2 kXSp)
-    const int xo_own = hh * kXSp + (r + 1) * 16;
-    const int xo_lr = hh ? (r + 2) * 16 : kXSp + r * 16;     // half 0: pixel 2r-1, half 1: 2r+2
-    const int xo_r = hh * 2 * kXSp + (r + 2) * 16;          // layer2: pixel 2r+2, channels 8h..
-    const int x2 = X0 - 1 + r;
-    const bool st_ok = r >= 1 && r <= kCols && x2 < a.w2;
-    const int frame_row0 = n * H;
-    const float* ctl = ctab + cc * 16;               // this lane's column case (row stride 8 cases)
-
-    auto row_ok = [&](int q) { return static_cast<unsigned>(q) < static_cast<unsigned>(H); };
-    auto load_row = [&](int fr) -> uint32_t {        // OOB offset for rows outside the frame: 0
-      const unsigned off = row_ok(fr) ? static_cast<unsigned>((frame_row0 + fr) * rowb + cb) : kOob;
-      return __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
-    };
-    auto ring_put = [&](int fr, uint32_t raw) {
-      const bool ok = row_ok(fr);
-      const uint32_t f0 = __builtin_amdgcn_perm(kF16Hi, raw, 0x04010400u) & (ok ? fm0 : 0u);
-      const uint32_t f1 = __builtin_amdgcn_perm(kF16Hi, raw, 0x04030402u) & (ok ? fm1 : 0u);
-      char* row = ring + (fr & (kRing - 1)) * kRowB;
-      *reinterpret_cast<uint2*>(row + 8 * lane) = make_uint2(f0, f1);
-      *reinterpret_cast<uint32_t*>(row + kCopyB + 8 * lane) = f0;
-      *reinterpret_cast<uint32_t*>(row + kCopyB + 8 * lane + 4) = f1;
-    };
-    auto slot6 = [](int row) { return (row + 12) % 6; };   // rows >= -12
-    auto put_x = [&](char* base, int row, const uint32_t (&v)[8]) {
-      char* p = base + slot6(row) * kXSlot + xo_own;
-      *reinterpret_cast<uint4*>(p) = make_uint4(v[0], v[1], v[2], v[3]);
-      *reinterpret_cast<uint4*>(p + 2 * kXSp) = make_uint4(v[4], v[5], v[6], v[7]);
-    };
-    auto row_case = [&](int q) { const int v = q < 3 ? q : (q >= H - 3 ? 6 - (H - 1 - q) : 3); return v < 0 ? 0 : (v > 6 ? 6 : v); };
-    auto cinit = [&](int q) -> f32x16 {
-      const float4* ct = reinterpret_cast<const float4*>(ctl + row_case(q) * 8 * 16);
-      f32x16 c;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float4 v = ct[i];
-        c[4 * i] = v.x; c[4 * i + 1] = v.y; c[4 * i + 2] = v.z; c[4 * i + 3] = v.w;
-      }
-      return c;
-    };
-
-    // Skewed walk: step j computes stem rows 2j+3, 2j+4, layer1 rows 2j, 2j+1 and layer2 row j-1,
-    // each from rows the PREVIOUS steps wrote, so the three MFMA chains of a step are independent
-    // and the stem / layer1 epilogues run under the later chains' MFMAs.  Steps ya-3 .. yb cover
-    // layer2 rows ya .. yb-1 (edge steps compute rows nobody stores).  The frame rows step j reads
-    // (2j .. 2j+7) were converted by the end of step j-1.
-    const int j0 = ya - 3;
-    {
-      uint32_t raw[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) raw[i] = load_row(2 * j0 + i);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ring_put(2 * j0 + i, raw[i]);
-    }
-    uint32_t raw0 = load_row(2 * j0 + 8), raw1 = load_row(2 * j0 + 9);
-    for (int j = j0; j <= yb; ++j) {
-      const int q = 2 * j + 3;                       // stem rows q, q+1
-      // ---- operand reads (all from rows written by earlier steps)
-      f16x8 bp[8], bx[4], bx2[4];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) bp[i] = ld_frag_f16(ring + ((2 * j + i) & (kRing - 1)) * kRowB, rdP);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        // X term t of stem row q: chunk 2 of rows q-3+2t+h = 2j+2t+h; of row q+1: 2j+1+2t+h
-        // (the kh = 7 half of t = 3 has zero weights; its row aliases a live ring slot)
-        bx[t] = ld_frag_f16(ring + ((2 * j + 2 * t) & (kRing - 1)) * kRowB, rdX - ((((2 * j + 2 * t) & (kRing - 1)) == kRing - 1) ? hh * kRing * kRowB : 0));
-        bx2[t] = ld_frag_f16(ring + ((2 * j + 1 + 2 * t) & (kRing - 1)) * kRowB, rdX - ((((2 * j + 1 + 2 * t) & (kRing - 1)) == kRing - 1) ? hh * kRing * kRowB : 0));
-      }
-      const f32x16 ci0 = cinit(q), ci1 = cinit(q + 1);
-      bf16x8 o1a[4], o1b[4], lr1a[4], lr1b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const char* sl = xs0 + slot6(2 * j - 1 + i) * kXSlot;
-        o1a[i] = ld_frag_bf16(sl + xo_own);
-        o1b[i] = ld_frag_bf16(sl + 2 * kXSp + xo_own);
-        lr1a[i] = ld_frag_bf16(sl + xo_lr);
-        lr1b[i] = ld_frag_bf16(sl + 2 * kXSp + xo_lr);
-      }
-      bf16x8 o2a[3], o2b[3], rr2[3];
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const char* sl = xs1 + slot6(2 * j - 3 + kh) * kXSlot;
-        o2a[kh] = ld_frag_bf16(sl + xo_own);
-        o2b[kh] = ld_frag_bf16(sl + 2 * kXSp + xo_own);
-        rr2[kh] = ld_frag_bf16(sl + xo_r);
-      }
-      // every operand of the step is in flight before the first MFMA waits on one
-      if constexpr (DRNMI_FR_PIN) __builtin_amdgcn_sched_barrier(0);
-      // ---- stem (2 x 11 MFMAs)
-      f32x16 s0 = ci0, s1 = ci1;
-#pragma unroll
-      for (int kh = 0; kh < 7; ++kh) {
-        s0 = mfma_f16<1>(as[kh], bp[kh], s0);
-        s1 = mfma_f16<1>(as[kh], bp[kh + 1], s1);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s0 = mfma_f16<1>(as[7 + t], bx[t], s0);
-        s1 = mfma_f16<1>(as[7 + t], bx2[t], s1);
-      }
-      // ---- layer1 (2 x 12 MFMAs)
-      f32x16 l0 = c1, l1 = c1;
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        l0 = mfma_bf16<2>(a1[4 * kh + 0], o1a[kh], l0);
-        l1 = mfma_bf16<2>(a1[4 * kh + 0], o1a[kh + 1], l1);
-        l0 = mfma_bf16<2>(a1[4 * kh + 1], o1b[kh], l0);
-        l1 = mfma_bf16<2>(a1[4 * kh + 1], o1b[kh + 1], l1);
-        l0 = mfma_bf16<2>(a1[4 * kh + 2], lr1a[kh], l0);
-        l1 = mfma_bf16<2>(a1[4 * kh + 2], lr1a[kh + 1], l1);
-        l0 = mfma_bf16<2>(a1[4 * kh + 3], lr1b[kh], l0);
-        l1 = mfma_bf16<2>(a1[4 * kh + 3], lr1b[kh + 1], l1);
-      }
-      // ---- stem epilogue (overlaps the layer1 / layer2 MFMAs)
-      {
-        const uint32_t m0 = row_ok(q) ? cmask : 0u, m1 = row_ok(q + 1) ? cmask : 0u;
-        uint32_t v0[8], v1[8];
-#pragma unroll
-        for (int d = 0; d < 8; ++d) {
-          v0[d] = relu_pk(s0[2 * d], s0[2 * d + 1]) & m0;
-          v1[d] = relu_pk(s1[2 * d], s1[2 * d + 1]) & m1;
-        }
-        put_x(xs0, q, v0);
-        put_x(xs0, q + 1, v1);
-      }
-      // ---- layer2 (9 MFMAs): row j - 1
-      f32x16 t2 = c2;
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        t2 = mfma_bf16<4>(a2[3 * kh + 0], o2a[kh], t2);
-        t2 = mfma_bf16<4>(a2[3 * kh + 1], o2b[kh], t2);
-        t2 = mfma_bf16<4>(a2[3 * kh + 2], rr2[kh], t2);
-      }
-      // ---- layer1 epilogue
-      {
-        const int p = 2 * j;
-        const uint32_t m0 = row_ok(p) ? cmask : 0u, m1 = row_ok(p + 1) ? cmask : 0u;
-        uint32_t v0[8], v1[8];
-#pragma unroll
-        for (int d = 0; d < 8; ++d) {
-          v0[d] = relu_pk(l0[2 * d], l0[2 * d + 1]) & m0;
-          v1[d] = relu_pk(l1[2 * d], l1[2 * d + 1]) & m1;
-        }
-        put_x(xs1, p, v0);
-        put_x(xs1, p + 1, v1);
-      }
-      // ---- layer2 epilogue: NHWC bf16 stores, lane half h holds channels 8g + 4h .. + 3
-      {
-        const int y = j - 1;
-        const bool store = st_ok && y >= ya && y < yb && (DRNMI_FR_ABL & 8) == 0;
-        const unsigned off =
-            store ? static_cast<unsigned>(((static_cast<int>(n) * a.h2 + y) * a.w2 + x2) * 64 + 8 * hh) : kOob;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint2 v = make_uint2(relu_pk(t2[4 * g], t2[4 * g + 1]), relu_pk(t2[4 * g + 2], t2[4 * g + 3]));
-          __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{v.x, v.y}, ys, off, 16 * g, 0);
-        }
-      }
-      // ---- frame rows 2j+8, 2j+9 into the ring (over rows 2j, 2j+1: read above), next loads
-      ring_put(2 * j + 8, raw0);
-      ring_put(2 * j + 9, raw1);
-      raw0 = load_row(2 * j + 10);
-      raw1 = load_row(2 * j + 11);
-    }
-  }
-}
-
-// ---- v3: register-carried rolling windows.  Step j's operands are mostly rows earlier steps already
+// ---- front3_kernel: register-carried rolling windows.  Step j's operands are mostly rows earlier steps already
 // hold in registers: the stem's P / X fragments shift by two frame rows per step (only rows 2j+6,
 // 2j+7 are read from the ring), layer1's own-pixel operands are the stem outputs S(j-2), S(j-1)
 // kept as bf16 registers and only their left/right neighbours come from the LDS exchange, and
@@ -433,14 +144,14 @@ front3_kernel(const FrontParams a) {
   for (int m = 0; m < kF1; ++m) a1[m] = pk[(kFS + m) * 64 + lane];
 #pragma unroll
   for (int m = 0; m < kF2; ++m) a2[m] = pk[(kFS + kF1 + m) * 64 + lane];
-  if constexpr (DRNMI_FR_AGPRW) {
+  // the 32 weight fragments live in AGPRs (MFMA A operands may be AGPRs): the VGPRs are left to
+  // the operand fragments and the accumulators, whose epilogue VALU would otherwise copy them out
 #pragma unroll
     for (int m = 0; m < kFS; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, as[m]); asm volatile("" : "+a"(t)); as[m] = __builtin_bit_cast(uint4, t); }
 #pragma unroll
     for (int m = 0; m < kF1; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, a1[m]); asm volatile("" : "+a"(t)); a1[m] = __builtin_bit_cast(uint4, t); }
 #pragma unroll
     for (int m = 0; m < kF2; ++m) { u32x4_t t = __builtin_bit_cast(u32x4_t, a2[m]); asm volatile("" : "+a"(t)); a2[m] = __builtin_bit_cast(uint4, t); }
-  }
   // layer1 / layer2 starting values live in LDS next to the stem table (re-read every step: the
   // walk's registers are full): c1l[0] = layer1 shift, c1l[1] = -1e30 (pixel outside the image),
   // c2l[h] = layer2 shift of 32x32 D row (j&3) + 8(j>>2) + 4h = channel
@@ -654,7 +365,7 @@ front3_kernel(const FrontParams a) {
     // layer2 epilogue of row y from its sums: NHWC bf16, lane half h holds channels 8g + 4h .. + 3;
     // piece g of 0..3 (8 B) -- or the packing of piece g (stores issued separately)
     auto l2_store = [&](int y, const uint32_t (&o)[8]) {
-      const bool store = st_ok && y >= ya && y < yb && (DRNMI_FR_ABL & 8) == 0;
+      const bool store = st_ok && y >= ya && y < yb;
       const unsigned off = store ? st_base + static_cast<unsigned>(y * a.w2 * 64) : kOob;
 #pragma unroll
       for (int g = 0; g < 4; ++g)
@@ -665,8 +376,7 @@ front3_kernel(const FrontParams a) {
     // (2 PH + k) & 3).  Pipelined over the step boundary: the previous step's layer2 epilogue runs
     // in the shadows of this step's stem MFMAs, the stem epilogue under the layer1 MFMAs, the
     // layer1 epilogue and the next step's operand fetch under the layer2 MFMAs; the instruction
-    // order is pinned (DRNMI_FR_ILV).
-    f32x16 cs_int;                                   // interior stem rows: row case 3 (DRNMI_FR_CSREG)
+    // order is pinned (FR_SB).
     auto step = [&](int j, auto ph_, auto border_) {
       constexpr int PH = decltype(ph_)::value;
       constexpr bool BORDER = decltype(border_)::value != 0;
@@ -680,25 +390,20 @@ front3_kernel(const FrontParams a) {
       for (int i = 0; i < 22; ++i) {
         const int kh = i >> 1;
         if (kh < 7) {
-          if ((i & 1) == 0) s0 = mfma_f16<1>(as[kh], P[kh], s0);
-          else s1 = mfma_f16<1>(as[kh], P[kh + 1], s1);
+          if ((i & 1) == 0) s0 = mfma_f16(as[kh], P[kh], s0);
+          else s1 = mfma_f16(as[kh], P[kh + 1], s1);
         } else {
           const int t = kh - 7;
-          if ((i & 1) == 0) s0 = mfma_f16<1>(as[7 + t], X[t], s0);
-          else s1 = mfma_f16<1>(as[7 + t], X2[t], s1);
+          if ((i & 1) == 0) s0 = mfma_f16(as[7 + t], X[t], s0);
+          else s1 = mfma_f16(as[7 + t], X2[t], s1);
         }
         if (i < 8) o2[i] = FR_PINV(relu_pk(FR_PINF(t2p[2 * i]), FR_PINF(t2p[2 * i + 1])));
         if (i == 9) l2_store(j - 2, o2);
         // later stages' LDS operands, issued a stage ahead: layer1 starting values, the stem rows'
         // border-case offsets (interior segments: row case 3)
         if (i == 12) l0 = ld16(c1m);
-        if constexpr (BORDER || !DRNMI_FR_CSREG) {
-          if (i == 14) cs0 = BORDER ? cinit(p + 3) : cinit_case(3);
-          if (i == 16) cs1 = BORDER ? cinit(p + 4) : cinit_case(3);
-        } else if (i == 14) {
-          cs0 = cs_int;
-          cs1 = cs_int;
-        }
+        if (i == 14) cs0 = BORDER ? cinit(p + 3) : cinit_case(3);
+        if (i == 16) cs1 = BORDER ? cinit(p + 4) : cinit_case(3);
         FR_SB();
       }
       // ---- C: layer1 rows p, p+1 from stem rows p-1 .. p+2 (2 x 12 MFMAs); the stem epilogue
@@ -722,8 +427,8 @@ front3_kernel(const FrontParams a) {
         const uint32_t* src = f < 2 ? V[kh + odd] : LR[kh + odd];
         const int o = (f & 1) * 4;
         const bf16x8 b = tobf({src[o], src[o + 1], src[o + 2], src[o + 3]});
-        if (odd) l1 = mfma_bf16<2>(a1[4 * kh + f], b, l1);
-        else l0 = mfma_bf16<2>(a1[4 * kh + f], b, l0);
+        if (odd) l1 = mfma_bf16(a1[4 * kh + f], b, l1);
+        else l0 = mfma_bf16(a1[4 * kh + f], b, l0);
         if (i >= 2 && i < 18) {
           const int d = (i - 2) >> 1;
           if ((i & 1) == 0) vq0[d] = FR_PINV(relu_pk(FR_PINF(s0[2 * d]) + cs0[2 * d], FR_PINF(s0[2 * d + 1]) + cs0[2 * d + 1]));
@@ -740,7 +445,7 @@ front3_kernel(const FrontParams a) {
       for (int i = 0; i < 9; ++i) {
         const int kh = i / 3, f = i % 3;
         const uint32_t* src = f < 2 ? Wl[kh] + f * 4 : Rl[kh];
-        t2 = mfma_bf16<4>(a2[i], tobf({src[0], src[1], src[2], src[3]}), t2);
+        t2 = mfma_bf16(a2[i], tobf({src[0], src[1], src[2], src[3]}), t2);
         if (i >= 1) {
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
@@ -750,7 +455,7 @@ front3_kernel(const FrontParams a) {
             else wp1[d] = FR_PINV(relu_pk(FR_PINF(l1[2 * d]), FR_PINF(l1[2 * d + 1])));
           }
         }
-        if (i == DRNMI_FR_FETCH) {
+        if (i == kFetchAt) {
           // the next step's operands: the frame windows roll by one step (the stem is done with
           // them) and take the new rows; V[2], V[3] = this step's stem rows
 #pragma unroll
@@ -791,7 +496,6 @@ front3_kernel(const FrontParams a) {
     // interior segments skip all row checks: every frame row a stem row reads (<= 2jl+7) is inside
     // and every stem row is of row case 3 (rows fetch() converts past 2jl+7 are never read)
     auto walk = [&](auto border_) {
-      if constexpr (decltype(border_)::value == 0 && DRNMI_FR_CSREG) cs_int = cinit_case(3);
       fetch(jb, ic<0>{}, border_);
       for (int j = jb; j <= jl; j += 4) {
         step(j + 0, ic<0>{}, border_);
@@ -961,9 +665,6 @@ extern "C" int drnmi_video_front_u8(const uint8_t* frames, const void* pack, voi
   const int waves = p.total < g_front_waves ? p.total : g_front_waves;
   p.per_wave = (p.total + waves - 1) / waves;
   const int grid = (p.total + p.per_wave - 1) / p.per_wave;
-  if (DRNMI_FR_V == 3)
-    hipLaunchKernelGGL(front3_kernel, dim3(grid), dim3(64), kLds3, static_cast<hipStream_t>(stream), p);
-  else
-    hipLaunchKernelGGL(front_kernel, dim3(grid), dim3(64), kLds, static_cast<hipStream_t>(stream), p);
+  hipLaunchKernelGGL(front3_kernel, dim3(grid), dim3(64), kLds3, static_cast<hipStream_t>(stream), p);
   return static_cast<int>(hipGetLastError());
 }

@@ -36,12 +36,8 @@ hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s);
 // conv_stag_kernel with the seg classifier in its epilogue (drnmi_conv_stag_seg): no activation store,
 // partial logits per 256-channel block into part[cout / 256][n ho wo][20].
 hipError_t launch_stag_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_pad, float* part, hipStream_t s);
-// The seg classifier (1x1, cout <= 32, cin % 256 == 0; conv_seg.hip), bit-identical to conv_big's
-// BK-32 tile.
-bool seg_conv_supported(const drnmi_conv_args& p);
-int seg_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
 // Row-walking stride-2 3x3 conv, 32 -> 64 / 64 -> 128 (conv_s2row.hip), bit-identical to conv_big's
-// BK-32 / BK-64 tiles; s2row_auto: supported and not disabled by DRNMI_S2ROW=0.
+// BK-32 / BK-64 tiles; s2row_auto: routed by default where supported.
 bool s2row_conv_supported(const drnmi_conv_args& p);
 bool s2row_auto(const drnmi_conv_args& p);
 int s2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
@@ -52,9 +48,4 @@ bool s1x2row_conv_supported(const drnmi_conv_args& p);
 bool s1x2row_auto(const drnmi_conv_args& p);
 int s1x2row_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
 const char* s1x2row_conv_name(const drnmi_conv_args& p);
-// Row-walking stride-1 3x3 128 -> 128 (+ residual) with K split over wave pairs (conv_row128.hip).
-bool row128_conv_supported(const drnmi_conv_args& p);
-bool row128_auto(const drnmi_conv_args& p);
-int row128_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
-const char* row128_conv_name(const drnmi_conv_args& p);
 }  // namespace drnmi

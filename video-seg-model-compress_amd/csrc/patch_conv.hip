@@ -632,14 +632,8 @@ constexpr int kSLLDS = 3 * kSLRawB + kSLPatchB + kSLStemB + 3 * 256 * 2;
 static_assert(kSLPatchB % 16 == 0 && kSLStemB % 16 == 0, "16-B aligned LDS regions");
 static_assert(kSLPR % 4 == 0 && 2 * kSLSR <= 32 && kSLSR % 2 == 0, "raw rows over 4 waves; edge columns in two groups");
 
-#ifndef DRNMI_SL_WAVES
-#define DRNMI_SL_WAVES 3      // waves per SIMD the fused stem is register-allocated for
-#endif
-#ifndef DRNMI_SL_ABL
-#define DRNMI_SL_ABL 0        // diagnostic builds only: bit 0 converts without the table, bit 1 skips
-                              // the stem MFMAs, bit 2 the layer1 MFMAs, bit 3 the output stores
-#endif
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(DRNMI_SL_WAVES)))
+// register-allocated for 3 waves per SIMD (4 spills and runs 10 % slower)
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(3)))
 stem_l1_kernel(const drnmi_conv_args p, const drnmi_conv_args q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* raw = smem;
@@ -730,13 +724,8 @@ stem_l1_kernel(const drnmi_conv_args p, const drnmi_conv_args q) {
           const unsigned char* px = rowp + pc * 3;
           int c0 = px[0], c1 = px[1], c2 = px[2];
           if (p.bgr) { const int t = c0; c0 = c2; c2 = t; }
-          if constexpr ((DRNMI_SL_ABL & 1) != 0) {
-            v.x = static_cast<uint32_t>(c0 << 7) | (static_cast<uint32_t>(c1 << 7) << 16);
-            v.y = static_cast<uint32_t>(c2 << 7);
-          } else {
           v.x = static_cast<uint32_t>(lut[c0]) | (static_cast<uint32_t>(lut[256 + c1]) << 16);
           v.y = static_cast<uint32_t>(lut[512 + c2]);
-          }
         }
         *reinterpret_cast<uint2*>(patch + (r * kSLPC + pc) * 4) = v;
       }
@@ -810,11 +799,7 @@ stem_l1_kernel(const drnmi_conv_args p, const drnmi_conv_args q) {
 #pragma unroll
         for (int kh = 0; kh < NK0; ++kh) {
           const int q = r - kh;
-          if constexpr ((DRNMI_SL_ABL & 2) != 0) {
-            if (q >= 0 && q < HR) asm volatile("" :: "v"(bv), "v"(wa0[kh]));
-          } else {
           if (q >= 0 && q < HR) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa0[kh], bv, acc[q], 0, 0, 0);
-          }
         }
       }
 #pragma unroll
@@ -846,8 +831,7 @@ stem_l1_kernel(const drnmi_conv_args p, const drnmi_conv_args q) {
       for (int ks = 0; ks < NK1; ++ks) {
         bf16x8 bv = __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
         if (boff[ks] >= 0) bv = *reinterpret_cast<const bf16x8*>(stile + boff[ks] + (r * kSLSC + c) * 32);
-        if constexpr ((DRNMI_SL_ABL & 4) != 0) asm volatile("" :: "v"(bv), "v"(wa1[ks]));
-        else acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[ks], bv, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa1[ks], bv, acc, 0, 0, 0);
       }
       const int oh = oh0 + r, ow = ow0 + c;
       const bool ok = oh < q.ho && ow < q.wo;
@@ -861,8 +845,7 @@ stem_l1_kernel(const drnmi_conv_args p, const drnmi_conv_args q) {
       o.x = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
       o.y = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
       const unsigned pix = static_cast<unsigned>((n * q.ho + oh) * q.wo + ow);
-      if constexpr ((DRNMI_SL_ABL & 8) != 0) asm volatile("" :: "v"(o), "v"(pix));
-      else __builtin_amdgcn_raw_buffer_store_b64(o, ys, ok ? (pix * 16 + kq * 4) * 2 : 0xffffffffu, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(o, ys, ok ? (pix * 16 + kq * 4) * 2 : 0xffffffffu, 0, 0);
     }
   }
 }

@@ -124,9 +124,6 @@ pack_batched_kernel(const int64_t* __restrict__ tab, int n, int64_t total) {
 // grid = (G splits, C / (4 * TPR) channel chunks).  Partials ws[2][G][C] (S1, S2).
 enum { RED_STATS = 0, RED_BNBWD = 1, RED_SUM = 2 };
 
-#ifndef DRNMI_RED_BATCH
-#define DRNMI_RED_BATCH 4    // column-reduction rows loaded ahead per thread (1: one load in flight)
-#endif
 
 struct RedArgs {
   const float* a;       // STATS: y ; BNBWD: dz ; SUM: x
@@ -151,9 +148,9 @@ __global__ void __launch_bounds__(kThreads) colred_kernel(const RedArgs r) {
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * r.rows_per_split;
   const int64_t r1 = (r0 + r.rows_per_split) < r.rows ? (r0 + r.rows_per_split) : r.rows;
   double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
-  // DRNMI_RED_BATCH rows' loads go out before their (in-order) fp64 accumulation: the same sums,
-  // with that many loads in flight per thread instead of one
-  constexpr int RB = DRNMI_RED_BATCH;
+  // RB rows' loads go out before their (in-order) fp64 accumulation: the same sums, with that many
+  // loads in flight per thread instead of one
+  constexpr int RB = 4;
   int64_t row = r0 + tr;
   for (; row + (RB - 1) * rg < r1; row += RB * rg) {
     float4 av[RB], zv[RB], yv[RB];
@@ -443,12 +440,6 @@ struct WgradP {
   int64_t pix_per_split;
 };
 
-#ifndef DRNMI_WGRAD_BIG
-#define DRNMI_WGRAD_BIG 1    // fp32x: the 128 x 128 wgrad tile where cout and K >= 128 (0: 64 x 64 only, A/B)
-#endif
-#ifndef DRNMI_WGRAD_MAP
-#define DRNMI_WGRAD_MAP 1    // 0: the 8-pixels-per-wave staging map (A/B)
-#endif
 constexpr int kWT = 64;      // tile rows / cols
 constexpr int kWM = 32;      // pixels per chunk
 constexpr int kWLD = kWM + 4;
@@ -471,17 +462,12 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4
   const int64_t m_begin = static_cast<int64_t>(blockIdx.z) * p.pix_per_split;
   int64_t m_end = m_begin + p.pix_per_split;
   if (m_end > p.M) m_end = p.M;
-#if DRNMI_WGRAD_MAP
   // the transposed LDS writes As[8 lv + j][lm] hit bank (4 j + lm) % 32 whatever lv is (rows are
   // 36 floats, 8 rows = 288 = 0 mod 32): with 8 pixels x 8 column groups per wave every write was
   // 8-way conflicted; 32 pixels per 32-lane half (lm = t % 32) makes them conflict-free, at 64 B
   // per pixel per load instruction pair instead of 256 B
   const int lm = t & 31;      // pixel row of the chunk this thread loads
   const int lv = t >> 5;      // 8-column group
-#else
-  const int lm = t >> 3;      // pixel row of the chunk this thread loads
-  const int lv = t & 7;       // 8-column group
-#endif
   const int hw = p.ho * p.wo;
   // B column group: (tap, ci) fixed for the whole loop
   const int kcol = kc0 + 8 * lv;
@@ -797,16 +783,13 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
     }
 }
 
-// ---- fp32x weight gradient, dy pre-split (DRNMI_WGRAD_PRE) ---------------------------------
+// ---- fp32x weight gradient, dy pre-split -----------------------------------------------------
 // The 128 x 128 tile above splits every dy and x value in each of the two waves that read it
 // (~4.4 VALU instructions per MFMA: VALU-bound, MFMA busy 0.31, profiles/r5r_wgrad_pmc).  Here dy
 // is split once per launch into three transposed bf16 planes [plane][co][m] (one HBM pass,
 // wgrad_dy_split_kernel) that the tile stages with LDS-DMA like conv_x6's weight planes: the
 // kernel splits only x.  Same split3 (RNE) of the same values and the same MFMA order per
 // accumulator as wgrad_x6_big_kernel, so the partial sums are bit-identical to it.
-#ifndef DRNMI_WGRAD_PRE
-#define DRNMI_WGRAD_PRE 1
-#endif
 constexpr int kPreRows = kWT2;   // dyT rows padded to a multiple of the tile (zero rows)
 
 __global__ void __launch_bounds__(kThreads)
@@ -1039,7 +1022,7 @@ wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin,
 // second round 1/8 full, 4.6 ms of a 52.8 ms fine-tune step).  Every split holds >= 512 pixels.
 static bool wgrad_big_ok(const drnmi_wgrad_args& a) {
   const int K = a.ks * a.ks * a.cin_stride;
-  return DRNMI_WGRAD_BIG && a.cout >= kWT2 && K >= kWT2 && a.cin_stride % 16 == 0;
+  return a.cout >= kWT2 && K >= kWT2 && a.cin_stride % 16 == 0;
 }
 
 static void wgrad_plan(const drnmi_wgrad_args& a, bool big, int* splits, int64_t* per) {
@@ -1496,7 +1479,7 @@ static int64_t wgrad_partials_bytes(const drnmi_wgrad_args& a, int splits) {
 // the dy split pass costs ~10 B of HBM per dy element against 2 K flops per element of the tile:
 // it pays where K >= 1024 (layer7.0: 3.78 -> 2.72 ms; a 1x1 256 -> 1024 wgrad: 128 -> 234 us)
 static bool wgrad_pre_ok(const drnmi_wgrad_args& a) {
-  return DRNMI_WGRAD_PRE && wgrad_big_ok(a) && a.ks * a.ks * a.cin_stride >= 1024;
+  return wgrad_big_ok(a) && a.ks * a.ks * a.cin_stride >= 1024;
 }
 static int64_t wgrad_pre_bytes(const drnmi_wgrad_args& a) {
   if (!wgrad_pre_ok(a)) return 0;

@@ -28,7 +28,7 @@ CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE,
 # per-source extra flags.  front.hip: MFMA results in VGPRs (the weights are pinned to AGPRs in the
 # source), so the epilogues read the accumulators without v_accvgpr_read copies
 EXTRA = {"front.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"], "block64.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-         "conv_s2row.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"], "conv_row128.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+         "conv_s2row.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def sources():

@@ -18,7 +18,6 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
-import os
 from dataclasses import dataclass, field
 
 import torch
@@ -45,8 +44,8 @@ INT8_MIN_CIN = 64
 # ... and whose output has at least this many channels.  256: D-22's 128-channel layer4 stays on
 # the bf16 row / staggered kernels (s2row, stag128 with the downsample folded in), which beat the
 # int8 tiles there (cin 128 gives the int8 staggered tile an odd tap-group count): 1786-1788 vs
-# 1750-1755 fps interleaved (profiles/r6_int8_fusions); DRNMI_INT8_MIN_COUT=128 restores it.
-INT8_MIN_COUT = int(os.environ.get("DRNMI_INT8_MIN_COUT", "256"))
+# 1750-1755 fps interleaved (profiles/r6_int8_fusions).
+INT8_MIN_COUT = 256
 
 # (cin_stride, cout, ks, stride, dil) served by the LDS-patch kernel (bf16 only; include/drnmi.h)
 # (32 -> 64 stride 2 runs faster on the K-32 LDS-DMA implicit GEMM: 67 vs 108 us per 4 frames)
@@ -569,9 +568,9 @@ def _conv_out(h, k, s, p, d):
 
 
 # segment(): NHWC logits rows for the labels head, and the seg classifier folded into the last conv
-# (drnmi_conv_stag_seg); DRNMI_LABELS_NHWC=0 / DRNMI_SEG_FUSE=0 switch them off (A/B runs)
-LABELS_NHWC = os.environ.get("DRNMI_LABELS_NHWC", "1") != "0"
-SEG_FUSE = os.environ.get("DRNMI_SEG_FUSE", "1") != "0"
+# (drnmi_conv_stag_seg); tests switch these module flags off to compare with the unfused path
+LABELS_NHWC = True
+SEG_FUSE = True
 
 
 class Plan:

@@ -38,8 +38,8 @@ from . import _lib
 from .engine import COUT_ALIGN, K_ALIGN, X6_PATCH_SHAPES, _conv_out, _pow2_at_least, _round_up
 
 F32 = _lib.DRNMI_F32
-# TrainRunner default (tests compare against the per-layer packs; DRNMI_BATCHED_PACK=0: A/B runs)
-BATCHED_PACK = os.environ.get("DRNMI_BATCHED_PACK", "1") != "0"
+# TrainRunner default (tests switch it off to compare against the per-layer packs)
+BATCHED_PACK = True
 
 
 def _vp(t):
