@@ -337,7 +337,7 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
 
     def launched_name(i):
         if front and i <= 2:                 # layer0..layer2 in one launch (drnmi_video_front_u8)
-            return "" if i else "front_kernel"
+            return "" if i else "front3_kernel"
         if i in blocks:                      # a 64-channel BasicBlock in one launch (drnmi_basic_block64)
             return "block64_kernel"
         if i - 1 in blocks:

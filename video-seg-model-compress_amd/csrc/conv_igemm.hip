@@ -101,7 +101,7 @@ conv_igemm_kernel(const drnmi_conv_args p) {
   const int M = p.n * p.ho * p.wo;
   const int hw_o = p.ho * p.wo;
   const int mt_count = (M + BM - 1) / BM;
-  const int nt_count = p.cout_pad / BN;
+  const int nt_count = (p.cout + BN - 1) / BN;      // column tiles past cout would be all padding
   const int tile = xcd_remap(blockIdx.x, mt_count * nt_count);
   const int bm0 = (tile / nt_count) * BM;
   const int bn0 = (tile % nt_count) * BN;
@@ -272,7 +272,7 @@ constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 template <typename T, int BM, int BN, int WM, int WN, int KS>
 hipError_t launch_conv(const drnmi_conv_args& p, hipStream_t stream) {
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
-  const int64_t blocks = ((M + BM - 1) / BM) * (p.cout_pad / BN);
+  const int64_t blocks = ((M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);   // (as the kernel's nt_count)
   hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, WM, WN, KS>), dim3(static_cast<unsigned>(blocks)),
                      dim3(kThreads), 0, stream, p);
   return hipGetLastError();
