@@ -351,9 +351,13 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
         return lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
 
     names = [launched_name(i) for i in range(len(plan.args))]
-    if plan.labels_path() == "seg2":           # the seg classifier in the last conv's epilogue (drnmi_conv_stag_seg)
-        names[plan.seg_fused["conv"]] = "conv_stag_seg_kernel"
+    path = plan.labels_path()
+    if path == "seg2":                         # the seg classifier in the last conv's epilogue (drnmi_conv_stag_seg)
+        names[plan.seg_fused["conv"]] = "conv_i8_stag_seg_kernel" if plan.seg_fused["i8"] else "conv_stag_seg_kernel"
         names[plan.seg_idx] = ""
+    # the head launch (index len(nodes), DRNSeg._segment_impl): up x8 + argmax -> uint8 labels
+    names.append({"seg2": "up8_labels_oct_kernel<19, U8, NHWC, SEG2>", "nhwc": "up8_labels_oct_kernel<19, U8, NHWC>"}
+                 .get(path, "up8_labels_oct_kernel<19, U8>"))
     nodes = plan.packed.graph.nodes
     # per-launch work (roofline.launch_work): a folded downsample's FLOPs and input run inside its
     # block's last conv, the fused stem launch carries layer1; useful work of a pruned layer
@@ -386,16 +390,21 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
         model.timing_hook = hook if (timed and kernel_events) else None
         return model.segment(x, INFO_MEAN, INFO_STD, False)
 
+    launches = []         # (node index, seconds) of the last collect(), in launch order
+
     def collect():
         """per-kernel durations of the recorded launches (the events list is then reset)"""
         torch.cuda.synchronize()
         per_, pend = {}, {}
+        launches.clear()
         for i, before, ev in events:
             if before:
                 pend[i] = ev
             else:
+                d = pend.pop(i).elapsed_time(ev) * 1e-3
+                launches.append((i, d))
                 g_ = per_.setdefault(names[i], {"d": [], "f": [], "b": [], "fd": []})
-                g_["d"].append(pend.pop(i).elapsed_time(ev) * 1e-3)
+                g_["d"].append(d)
                 g_["f"].append(works[i][1])
                 g_["fd"].append(dense_flops[i])
                 g_["b"].append(works[i][2])
@@ -417,11 +426,16 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
     watch[0] = None
     step(True)
     per = collect()
+    # per launch of that step, keyed by the node that opens it (the conv_stag family's launches
+    # differ in K and tile count: the weakest shows here, not in the per-kernel average)
+    layers = [{"node": nodes[i].name if i < len(nodes) else "head", "kernel": names[i], "us": round(d * 1e6, 1),
+               "gflop": round(works[i][1] / 1e9, 2), "tflops": round(works[i][1] / d / 1e12, 1),
+               "gbps": round(works[i][2] / d / 1e9, 1)} for i, d in launches]
     if dominant in timed_per:
         per[dominant] = timed_per[dominant]
     model.timing_hook = None
     return {"el": el, "own": own, "plan": plan, "names": names, "density": density, "per": per,
-            "dominant": dominant, "timed": timed_per.get(dominant), "step": step}
+            "dominant": dominant, "timed": timed_per.get(dominant), "step": step, "layers": layers}
 
 
 def roofline_block(args, m, precision):
@@ -538,6 +552,7 @@ def main(argv=None):
         out["kernels_source"] = ("dominant kernel: HIP events around its launches in the timed region; "
                                  "the others: one fully instrumented step after it")
         out["kernels"] = kernels
+        out["layers"] = m["layers"]
     out["network_roofline"] = network_block(m, args.steps, B)
     if host is not None:
         out["host_frames"] = host

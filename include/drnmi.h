@@ -265,14 +265,26 @@ int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const float* up_w, vo
  * 256-channel block's partial logits go to partials[cout / 256][n*ho*wo][20] (fp32, 16-B aligned):
  * partial_b[m][k] = sum over the block's channels c of seg_w[k][c] * bf16(relu(conv)[m][c]).
  * seg_w: packed bf16 [seg_rows >= 32][seg_k_pad] (rows 19.. zero).  DRNMI_ENOTSUP if the conv does
- * not take the staggered tile. */
+ * not take the staggered tile.
+ * int8 nets (a->dtype DRNMI_I8, out_dtype DRNMI_I8, the W8A8 epilogue of drnmi_conv2d_bn_act, no
+ * residual): seg_w is the int8 seg conv's packed weights and the partials are int32,
+ * partial_b[m][k] = sum over the block's channels c of seg_w[k][c] * q8[m][c], q8 = the int8 value
+ * the conv would store; the int8 seg conv's fp32 output is then (float)(partial_0 + partial_1) *
+ * seg_scale[k] + seg_shift[k] (drnmi_up8_labels_seg2_i8). */
 int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, int32_t seg_k_pad, int32_t seg_rows,
-                        float* partials, void* stream);
+                        void* partials, void* stream);
 
 /* Labels from those partials: logit[k] = (bias[k] + partial_0[k]) + partial_1[k] (bias: >= cs
  * floats), then the labels-only head's arithmetic (drnmi_up8_labels_nhwc).  partials: [2][n][h][w][cs]. */
 int drnmi_up8_labels_seg2(const float* partials, int32_t cs, const float* bias, const float* up_w, void* labels,
                           int32_t label_dtype, int32_t n, int32_t c, int32_t h, int32_t w, void* stream);
+
+/* int8 nets: logit[k] = (float)(partial_0[k] + partial_1[k]) * scale[k] + shift[k] (fmul then fadd,
+ * the int8 seg conv's epilogue: identical logits), then the same head.  partials: int32
+ * [2][n][h][w][cs]; scale, shift: >= cs floats. */
+int drnmi_up8_labels_seg2_i8(const int32_t* partials, int32_t cs, const float* scale, const float* shift,
+                             const float* up_w, void* labels, int32_t label_dtype, int32_t n, int32_t c, int32_t h,
+                             int32_t w, void* stream);
 
 /* Same head for DRNSeg(use_torch_up=True): nn.UpsamplingBilinear2d(scale_factor=8) (bilinear,
  * align_corners=True; lmodels/drnseg.py:285-287) + LogSoftmax + argmax.  Source index and

@@ -1,6 +1,7 @@
 """conv_x6 (fp32x) micro-benchmark on the exact-mode / fine-tune shapes: HIP-event time per launch,
 fp32-accurate TFLOP/s (peak 2.5 PF / 6) and a SHA-1 of the output bytes (bit-identity across
-library builds: DRNMI_LIB=...).  python scripts/x6_micro.py"""
+variants: VARIANTS=auto,3 forces conv_x6 variants through drnmi_conv_args.tile).
+python scripts/x6_micro.py"""
 import ctypes
 import hashlib
 import os
@@ -20,7 +21,15 @@ SHAPES = [  # name, n, h, w, cin, cout, ks, stride, pad, dil, res, split
     ("l5 256 d2 +res b8", 8, 128, 256, 256, 256, 3, 1, 2, 2, True, False),
     ("l6 ds 1x1 b8", 8, 128, 256, 256, 512, 1, 1, 0, 1, False, False),
     ("ft l6 512 d4 split", 2, 128, 96, 512, 512, 3, 1, 4, 4, False, True),
+    ("l3 64 +res b8", 8, 256, 512, 64, 64, 3, 1, 1, 1, True, False),
+    ("l4 128 +res b8", 8, 128, 256, 128, 128, 3, 1, 1, 1, True, False),
+    ("l4.0 ds 1x1 s2 b8", 8, 256, 512, 64, 128, 1, 2, 0, 1, False, False),
+    ("l5.0 ds 1x1 b8", 8, 128, 256, 128, 256, 1, 1, 0, 1, False, False),
 ]
+SEL = os.environ.get("SHAPES")
+if SEL:
+    SHAPES = [sh for sh in SHAPES if any(k in sh[0] for k in SEL.split(","))]
+VARIANTS = [(-1 if v == "auto" else int(v)) for v in os.environ.get("VARIANTS", "auto").split(",")]
 lib = _lib.load()
 for name, n, h, w, cin, cout, ks, s, pad, dil, res, split in SHAPES:
     g = torch.Generator(device=DEV).manual_seed(cin + cout + ks)
@@ -45,13 +54,20 @@ for name, n, h, w, cin, cout, ks, s, pad, dil, res, split in SHAPES:
     a.k, a.k_pad = k, wpk.shape[1]
     a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_F32X3, _lib.DRNMI_F32, -1, _lib.ALGO_IGEMM
     ws = None
+    if split and VARIANTS != [-1]:
+        continue                      # (split-K workspaces are sized for the auto variant)
     if split:
         nb = lib.drnmi_conv_workspace_bytes(ctypes.byref(a))
         ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=DEV)
         a.ws, a.ws_bytes = ws.data_ptr(), nb
     st = ctypes.c_void_p(_lib.stream_ptr())
-    best = None
-    for rep in range(3):
+    for var in VARIANTS:
+      a.tile = var
+      kname = lib.drnmi_conv_kernel_name(ctypes.byref(a))
+      if kname is None:
+        continue
+      best = None
+      for rep in range(3):
         for _ in range(2):
             _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), st), "x6")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,7 +78,7 @@ for name, n, h, w, cin, cout, ks, s, pad, dil, res, split in SHAPES:
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / 5 * 1e3
         best = us if best is None else min(best, us)
-    flops = 2.0 * n * ho * wo * cout * cin * ks * ks
-    sha = hashlib.sha1(y.cpu().numpy().tobytes()).hexdigest()[:12]
-    print(f"{name:22s} {best:9.1f} us  {flops / best / 1e6:6.1f} TF  ({flops / best / 1e6 / (2500 / 6):.3f} of 417)  sha {sha}",
-          flush=True)
+      flops = 2.0 * n * ho * wo * cout * cin * ks * ks
+      sha = hashlib.sha1(y.cpu().numpy().tobytes()).hexdigest()[:12]
+      print(f"{name:22s} {kname.decode():28s} {best:9.1f} us  {flops / best / 1e6:6.1f} TF  "
+            f"({flops / best / 1e6 / (2500 / 6):.3f} of 417)  sha {sha}", flush=True)

@@ -52,6 +52,73 @@ def test_labels_nhwc_match_nchw_head(shape, ldt):
     assert torch.equal(a, b)
 
 
+def _smooth_logits(n, h, w, seed):
+    """Spatially smooth logits (bilinearly enlarged coarse noise): large same-argmax regions, the
+    fast path of up8_labels_fast_kernel, with engineered top-2 margins around its guard."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(seed)
+    coarse = torch.randn(n, 19, h // 6 + 2, w // 6 + 2, generator=g) * 4
+    x = F.interpolate(coarse, size=(h, w), mode="bilinear", align_corners=True)
+    top2 = torch.topk(x, 2, dim=1)
+    # every 7th pixel: runner-up moved to best - d with d around the guard (2^-16 .. 2^-13)
+    sel = torch.zeros(h, w, dtype=torch.bool)
+    sel.view(-1)[::7] = True
+    d = torch.tensor([2 ** -17, 2 ** -16, 1.1 * 2 ** -16, 2 ** -15, 1.5 * 2 ** -15, 2 ** -13, 2 ** -12])
+    dd = d[torch.arange(h * w) % len(d)].view(h, w)
+    i2 = top2.indices[:, 1]
+    newv = top2.values[:, 0] - dd
+    x.scatter_(1, i2.unsqueeze(1), torch.where(sel, newv, top2.values[:, 1]).unsqueeze(1))
+    return x
+
+
+@pytest.mark.parametrize("shape", [(2, 40, 64), (1, 128, 256), (3, 9, 130)])
+@pytest.mark.parametrize("up", ["bilinear", "random", "negative"])
+@pytest.mark.parametrize("seg2", [False, True])
+def test_labels_fast_path_identical(shape, up, seg2):
+    """up8_labels_fast_kernel (NHWC / SEG2 entry points): blocks whose 4 taps share an argmax with a
+    margin above the guard are written without per-pixel work; labels must equal the oct head's
+    (NCHW) bit for bit, with margins engineered around the guard, non-bilinear up weights and a
+    negative weight (which disables the fast path)."""
+    n, h, w = shape
+    logits = _smooth_logits(n, h, w, h * 7 + w + (1 if seg2 else 0))
+    if up == "bilinear":
+        upw = _up_plane()
+    else:
+        g = torch.Generator().manual_seed(5)
+        upw = (torch.rand(16, 16, generator=g) * 0.3).float()
+        if up == "negative":
+            upw[3, 5] = -0.01
+        upw = upw.contiguous().to(DEV)
+    cs = 20
+    lib = _lib.load()
+    st = ctypes.c_void_p(_lib.stream_ptr())
+    a = torch.empty(n, 8 * h, 8 * w, dtype=torch.uint8, device=DEV)
+    b = torch.empty_like(a)
+    if seg2:   # the head sums (bias + partial 0) + partial 1: feed the NCHW head that same sum
+        g = torch.Generator().manual_seed(9)
+        bias = torch.randn(20, generator=g) * 0.1
+        p0 = torch.randn(n, h, w, cs, generator=g)
+        p1 = logits.permute(0, 2, 3, 1).contiguous()
+        p1 = torch.cat([p1, torch.zeros(n, h, w, 1)], dim=3) - p0
+        summed = ((bias.view(1, 1, 1, cs) + p0) + p1)[..., :19].permute(0, 3, 1, 2).contiguous().to(DEV)
+        parts = torch.stack([p0, p1]).contiguous().to(DEV)
+        bias = bias.to(DEV)
+        _lib.check(lib.drnmi_up8_logsoftmax_argmax(summed.data_ptr(), upw.data_ptr(), None, a.data_ptr(),
+                                                   _lib.DRNMI_U8, n, 19, h, w, st), "nchw head")
+        _lib.check(lib.drnmi_up8_labels_seg2(parts.data_ptr(), cs, bias.data_ptr(), upw.data_ptr(), b.data_ptr(),
+                                             _lib.DRNMI_U8, n, 19, h, w, st), "seg2 head")
+    else:
+        lg = logits.to(DEV)
+        nhwc = torch.full((n, h, w, cs), float("nan"), device=DEV)
+        nhwc[..., :19] = lg.permute(0, 2, 3, 1)
+        _lib.check(lib.drnmi_up8_logsoftmax_argmax(lg.data_ptr(), upw.data_ptr(), None, a.data_ptr(), _lib.DRNMI_U8,
+                                                   n, 19, h, w, st), "nchw head")
+        _lib.check(lib.drnmi_up8_labels_nhwc(nhwc.data_ptr(), cs, upw.data_ptr(), b.data_ptr(), _lib.DRNMI_U8,
+                                             n, 19, h, w, st), "nhwc head")
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), f"{int((a != b).sum())} labels differ"
+
+
 def test_labels_nhwc_rejects_bad_args():
     lib = _lib.load()
     x = torch.zeros(1, 4, 4, 20, device=DEV)
@@ -132,3 +199,37 @@ def test_segment_labels_nhwc_identical_int8():
     finally:
         engine.LABELS_NHWC = old
     assert torch.equal(ref, got)
+
+
+def test_segment_seg_fused_int8_exact():
+    """int8 nets (C5): the int8 seg conv folded into layer8's int8 epilogue (conv_i8_stag_seg_kernel:
+    the int8 values layer8 would store times the int8 seg weights, int32 partials per 256-channel
+    block) + drnmi_up8_labels_seg2_i8.  Integer sums are exact, so (float)(p0 + p1) * scale + shift
+    must equal the separate int8 seg conv's fp32 logits bit for bit, and the labels must be equal."""
+    m = drnseg.build("drn_d_22", 19, seed=6, device=torch.device(DEV))
+    g = torch.Generator(device=DEV).manual_seed(12)
+    frames = torch.randint(0, 256, (2, 256, 2048, 3), dtype=torch.uint8, device=DEV, generator=g)
+    m.calibrate_int8(frames[:1])
+    m.set_precision("int8")
+    old = engine.SEG_FUSE
+    try:
+        engine.SEG_FUSE = False
+        ref = m.segment(frames, INFO_MEAN, INFO_STD, False).clone()
+        plan = [p for k, p in m._plans.items() if k[0] == "int8"][0]
+        assert plan.labels_path() == "nhwc"
+        lh, lw = plan.shapes["logits"]
+        logits = plan.bufs["logits_nhwc"].view(2, lh, lw, 20)[..., :19].clone()
+        engine.SEG_FUSE = True
+        plan.refresh_weight_ptrs()
+        assert plan.labels_path() == "seg2" and plan.seg_fused["i8"]
+        got = m.segment(frames, INFO_MEAN, INFO_STD, False)
+    finally:
+        engine.SEG_FUSE = old
+    torch.cuda.synchronize()
+    part = plan.bufs["seg_part"].view(2, 2, lh, lw, 20)
+    seg = plan.packed.graph.nodes[plan.seg_idx]
+    acc = (part[0] + part[1])[..., :19]
+    rebuilt = acc.float() * seg.scale[:19].view(1, 1, 1, 19)
+    rebuilt = rebuilt + seg.shift[:19].view(1, 1, 1, 19)
+    assert torch.equal(rebuilt, logits)
+    assert torch.equal(got, ref)

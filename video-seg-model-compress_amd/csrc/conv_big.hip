@@ -1040,11 +1040,27 @@ using namespace drnmi;
 // epilogue (conv_stag.hip SEGF): same launch geometry and MFMA work as conv_stag_kernel, the
 // activation is never stored.  Validated like the conv it replaces plus the seg operands.
 extern "C" int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, int32_t seg_k_pad, int32_t seg_rows,
-                                   float* partials, void* stream) {
+                                   void* partials, void* stream) {
   if (a == nullptr || seg_w == nullptr || partials == nullptr) return DRNMI_EINVAL;
   const drnmi_conv_args& p = *a;
   if (p.x == nullptr || p.wgt == nullptr || p.shift == nullptr) return DRNMI_EINVAL;
-  if (p.algo != DRNMI_ALGO_IGEMM || p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16 || p.src_u8) return DRNMI_EINVAL;
+  if (p.algo != DRNMI_ALGO_IGEMM || p.src_u8) return DRNMI_EINVAL;
+  if (p.dtype == DRNMI_I8) {
+    // int8 nets: the conv's int8 output (out_dtype I8, quantised with out_scale) feeds int8 seg
+    // weights; int32 partials
+    if (p.out_dtype != DRNMI_I8 || p.scale == nullptr) return DRNMI_EINVAL;
+    if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
+        p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
+      return DRNMI_EINVAL;
+    if (seg_k_pad < p.cout || seg_k_pad % 16 != 0 || seg_rows < 32 || (reinterpret_cast<uintptr_t>(partials) & 15) != 0)
+      return DRNMI_EINVAL;
+    if (!(i8_conv_supported(p) && p.ks == 3 && i8_stag_ok(p)) || p.res != nullptr || p.cout % 256 != 0 ||
+        p.cout_pad < p.cout)
+      return DRNMI_ENOTSUP;
+    const hipError_t e = launch_stag_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream));
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
+  if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16) return DRNMI_EINVAL;
   if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
       p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
     return DRNMI_EINVAL;

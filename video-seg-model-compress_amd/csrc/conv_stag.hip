@@ -53,11 +53,94 @@ __device__ __forceinline__ int stag_tile(int bid, int ntiles, int /*nco*/) { ret
 // instead -- per tile, the partial logits over its 256 channels go to part[channel block][pixel][20]
 // and the head adds bias + block 0 + block 1 in that order.
 struct SegFuse {
-  const uint16_t* w;    // seg weights, packed [>= 32 rows][k_pad] bf16 (scale folded; rows 19.. zero)
+  const void* w;        // seg weights, packed [>= 32 rows][k_pad]: bf16 (scale folded) or int8; rows 19.. zero
   int k_pad;
-  float* part;          // [nco][n ho wo][kSegCS] fp32
+  void* part;           // [nco][n ho wo][kSegCS]: fp32 (bf16 nets) or int32 (int8 nets)
 };
 constexpr int kSegCS = 20;
+
+// int8 nets (C5): the seg classifier on the int8 copy of the last conv's output.  Each output
+// value is quantised exactly as store_tile_i8 stores it (fmul, fadd, ReLU, rint(v * out_scale)
+// clamped to +-127; no contraction) and becomes the B operand of v_mfma_i32_16x16x64_i8 whose A
+// fragments are the int8 seg weights.  Lane (fr, fq) holds channels 16 fm + 4 fq .. + 3 of
+// pixel fr; for the 64-channel group g its 16 bytes are channels 64 g + 16 m + 4 fq + e (m, e =
+// 0..3) in that order, and the A fragment takes the seg weights of the same channels: a fixed
+// permutation of K, so the int32 sums are exact -- the separate int8 seg conv's accumulators,
+// split into per-tile (256-channel) partials whose integer sum is order-free.
+template <int FM>
+__device__ __forceinline__ void stag_seg_i8(const drnmi_conv_args& p, const int (&acc)[FM][4][4], int px0, int co0, int wc,
+                                            int wp, int fr, int fq, const SegFuse& sf, char* smem) {
+#pragma clang fp contract(off)
+  static_assert(FM % 4 == 0, "64-channel groups");
+  constexpr int NG = FM / 4;
+  const int8_t* sw = static_cast<const int8_t*>(sf.w);
+  const int cw = co0 + wc * 16 * FM;                 // the wave's first channel
+  i32x4 aw[2][NG];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        aw[mt][g][m] = *reinterpret_cast<const int*>(sw + static_cast<int64_t>(16 * mt + fr) * sf.k_pad + cw + 64 * g +
+                                                     16 * m + 4 * fq);
+  const bool relu = p.relu != 0;
+  i32x4 pacc[2][4];
+#pragma unroll
+  for (int fn = 0; fn < 4; ++fn) {
+    pacc[0][fn] = i32x4{0, 0, 0, 0};
+    pacc[1][fn] = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      i32x4 b;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int fm = 4 * g + m;
+        const int co = cw + 16 * fm + 4 * fq;
+        const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);   // padded to cout_pad
+        const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+        const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+        uint32_t o = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = static_cast<float>(acc[fm][fn][e]) * scv[e] + shv[e];
+          if (relu) v = fmaxf(v, 0.f);
+          const float t = fminf(fmaxf(rintf(v * p.out_scale), -127.f), 127.f);
+          o |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(t)))) << (8 * e);
+        }
+        b[m] = static_cast<int>(o);
+      }
+      pacc[0][fn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw[0][g], b, pacc[0][fn], 0, 0, 0);
+      pacc[1][fn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw[1][g], b, pacc[1][fn], 0, 0, 0);
+    }
+  }
+  // the two channel halves of the tile (waves wc = 0, 1), added through LDS (the loop is done with it)
+  i32x4* xch = reinterpret_cast<i32x4*>(smem) + (wp * 64 + (fq * 16 + fr)) * 8;
+  __syncthreads();
+  if (wc == 1) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) xch[mt * 4 + fn] = pacc[mt][fn];
+  }
+  __syncthreads();
+  if (wc == 0) {
+    const int M = p.n * p.ho * p.wo;
+    int* __restrict__ part = static_cast<int*>(sf.part) + static_cast<int64_t>(co0 / (32 * FM)) * M * kSegCS;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int cls = 16 * mt + 4 * fq;
+      if (cls >= kSegCS) continue;
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn) {
+        const i32x4 o = xch[mt * 4 + fn];
+        const int64_t m = px0 + wp * 64 + fn * 16 + fr;
+        *reinterpret_cast<int4*>(part + m * kSegCS + cls) =
+            make_int4(pacc[mt][fn][0] + o[0], pacc[mt][fn][1] + o[1], pacc[mt][fn][2] + o[2], pacc[mt][fn][3] + o[3]);
+      }
+    }
+  }
+}
 
 template <typename T, bool X2, int WCO = 128, bool SEGF = false>
 __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const SegFuse& sf = SegFuse{nullptr, 0, nullptr}) {
@@ -362,7 +445,18 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the clamped re-fetches
-  if constexpr (SEGF) {
+  if constexpr (SEGF && K::ESZ == 1) {
+    static_assert(!X2 && WCO == 128, "seg fusion: the 256-channel int8 tile");
+    int accv[FM][4][4];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) accv[fm][fn][e] = acc[fm][fn][e];
+    stag_seg_i8<FM>(p, accv, px0, co0, wc, wp, fr, fq, sf, smem);
+    return;
+  } else if constexpr (SEGF) {
     // the activation as store_tile_x4 would store it (ReLU, RNE to bf16, 16-B pieces: lane
     // (fr, fq) holds channels 8 s(fq) .. +7 of 32-channel group f2 of pixel fr) is the B operand of
     // the seg GEMM, the A fragments the matching seg weight columns; then the two channel halves
@@ -373,7 +467,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int f2 = 0; f2 < FM / 2; ++f2)
-        aw[mt][f2] = *reinterpret_cast<const bf16x8*>(sf.w + static_cast<int64_t>(16 * mt + fr) * sf.k_pad + co0 + wc * WCO +
+        aw[mt][f2] = *reinterpret_cast<const bf16x8*>(static_cast<const uint16_t*>(sf.w) + static_cast<int64_t>(16 * mt + fr) * sf.k_pad + co0 + wc * WCO +
                                                       32 * f2 + chunk_of_row(fq) * 8);
     const bool relu = p.relu != 0;
     f32x4 pacc[2][4];
@@ -412,7 +506,7 @@ __device__ __forceinline__ void conv_stag_body(const drnmi_conv_args& p, const S
     __syncthreads();
     if (wc == 0) {
       const int M = p.n * p.ho * p.wo;
-      float* __restrict__ part = sf.part + static_cast<int64_t>(co0 / (2 * WCO)) * M * kSegCS;
+      float* __restrict__ part = static_cast<float*>(sf.part) + static_cast<int64_t>(co0 / (2 * WCO)) * M * kSegCS;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         const int cls = 16 * mt + 4 * fq;
@@ -472,6 +566,10 @@ __global__ void __launch_bounds__(512, 1)
 conv_stag_seg_kernel(const StagSegArgs a) {
   conv_stag_body<uint16_t, false, 128, true>(a.p, a.sf);
 }
+__global__ void __launch_bounds__(512, 1)
+conv_i8_stag_seg_kernel(const StagSegArgs a) {
+  conv_stag_body<int8_t, false, 128, true>(a.p, a.sf);
+}
 
 // + the fused 1x1 downsample (x2 != NULL; layer5.0 / layer6.0 conv2 of D-22)
 __global__ void __launch_bounds__(512, 1)
@@ -484,20 +582,22 @@ conv_stag_x2_kernel(const drnmi_conv_args p) {
 constexpr int kStagLds = 2 * 256 * 128 + 2 * kStripBytes;     // 2 A stages + 2 strips (130 KB)
 constexpr int kStag128Lds = 2 * 128 * 128 + 2 * kStripBytes;  // 128-channel tile (98 KB)
 
-hipError_t launch_stag_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_pad, float* part, hipStream_t s) {
+hipError_t launch_stag_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_pad, void* part, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_stag_seg_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kStagLds);
-    if (e != hipSuccess) return e;
+    for (const void* f : {reinterpret_cast<const void*>(&conv_stag_seg_kernel), reinterpret_cast<const void*>(&conv_i8_stag_seg_kernel)}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kStagLds);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
   StagSegArgs a;
   a.p = p;
-  a.sf = SegFuse{static_cast<const uint16_t*>(seg_w), seg_k_pad, part};
+  a.sf = SegFuse{seg_w, seg_k_pad, part};
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const dim3 grid(static_cast<unsigned>((M / kBPX) * ((p.cout + 255) / 256)));
-  hipLaunchKernelGGL(conv_stag_seg_kernel, grid, dim3(512), kStagLds, s, a);
+  if (p.dtype == DRNMI_I8) hipLaunchKernelGGL(conv_i8_stag_seg_kernel, grid, dim3(512), kStagLds, s, a);
+  else hipLaunchKernelGGL(conv_stag_seg_kernel, grid, dim3(512), kStagLds, s, a);
   return hipGetLastError();
 }
 

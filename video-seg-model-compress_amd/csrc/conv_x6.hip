@@ -473,8 +473,15 @@ hipError_t launch_x6(const drnmi_conv_args& p, int splits, hipStream_t s) {
 }
 
 // 0: 256-channel tile (8 waves), 1: 128 (4 waves), 2: 64 (4 waves)
-int x6_variant(const drnmi_conv_args& p) { return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 1 : 2; }
-constexpr int kX6Bco[3] = {256, 128, 64};
+// variants: 0 <K, 128, 2> (256 channels, 8 waves), 1 <K, 128, 1> (128, 4 waves), 2 <K, 64, 1> (64, 4
+// waves), 3 <K, 64, 2> (128 channels, 8 waves); a drnmi_conv_args.tile in 0..3 forces one (tests,
+// micro-benchmarks)
+constexpr int kX6Bco[4] = {256, 128, 64, 128};
+constexpr int kNumX6 = 4;
+// 128-channel layers take the 8-wave tile (two waves per SIMD): D-22 layer4 492 vs 511 us, its 1x1
+// stride-2 downsample 64 vs 83 us at batch 8 (scripts/x6_micro.py, profiles/r7_x6)
+int x6_auto_variant(const drnmi_conv_args& p) { return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 3 : 2; }
+int x6_variant(const drnmi_conv_args& p) { return p.tile >= 0 && p.tile < kNumX6 ? p.tile : x6_auto_variant(p); }
 
 // Split-K count for a launch whose tiles leave CUs idle (one workgroup per CU: 96 tiles of the
 // fine-tune's 2 x 128 x 96 layer5 convs used 96 of 256 CUs).  Cost model per split count S:
@@ -552,17 +559,30 @@ int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
     if (S > 1 && (reinterpret_cast<uintptr_t>(p.ws) & 15) != 0) return DRNMI_EINVAL;
   }
   hipError_t e;
-  if (p.ks == 3)
-    e = v == 0 ? launch_x6<3, 128, 2>(p, S, s) : v == 1 ? launch_x6<3, 128, 1>(p, S, s) : launch_x6<3, 64, 1>(p, S, s);
-  else
-    e = v == 0 ? launch_x6<1, 128, 2>(p, S, s) : v == 1 ? launch_x6<1, 128, 1>(p, S, s) : launch_x6<1, 64, 1>(p, S, s);
+  if (p.ks == 3) {
+    switch (v) {
+      case 0: e = launch_x6<3, 128, 2>(p, S, s); break;
+      case 1: e = launch_x6<3, 128, 1>(p, S, s); break;
+      case 2: e = launch_x6<3, 64, 1>(p, S, s); break;
+      default: e = launch_x6<3, 64, 2>(p, S, s); break;
+    }
+  } else {
+    switch (v) {
+      case 0: e = launch_x6<1, 128, 2>(p, S, s); break;
+      case 1: e = launch_x6<1, 128, 1>(p, S, s); break;
+      case 2: e = launch_x6<1, 64, 1>(p, S, s); break;
+      default: e = launch_x6<1, 64, 2>(p, S, s); break;
+    }
+  }
   return static_cast<int>(e);
 }
 
 const char* x6_conv_name(const drnmi_conv_args& p) {
   if (!x6_conv_supported(p)) return nullptr;
-  static const char* n3[3] = {"conv_x6_kernel<3, 128, 2>", "conv_x6_kernel<3, 128, 1>", "conv_x6_kernel<3, 64, 1>"};
-  static const char* n1[3] = {"conv_x6_kernel<1, 128, 2>", "conv_x6_kernel<1, 128, 1>", "conv_x6_kernel<1, 64, 1>"};
+  static const char* n3[kNumX6] = {"conv_x6_kernel<3, 128, 2>", "conv_x6_kernel<3, 128, 1>", "conv_x6_kernel<3, 64, 1>",
+                                   "conv_x6_kernel<3, 64, 2>"};
+  static const char* n1[kNumX6] = {"conv_x6_kernel<1, 128, 2>", "conv_x6_kernel<1, 128, 1>", "conv_x6_kernel<1, 64, 1>",
+                                   "conv_x6_kernel<1, 64, 2>"};
   return p.ks == 3 ? n3[x6_variant(p)] : n1[x6_variant(p)];
 }
 

@@ -262,6 +262,123 @@ up8_lsm_quad_kernel(const float* __restrict__ logits, const float* __restrict__ 
   }
 }
 
+// One output row of 4 pixels of the labels-only head: the up-sampled logits of the 4 taps (kernel
+// row ky1 = oy + 4 - 8 i1, columns kx1_0 + p), the argmax with its near-tie fallback through the
+// log-softmax (see up8_labels_oct_kernel).  Shared by the oct and the fast-path kernels, so their
+// labels are the same arithmetic.
+template <int NC>
+__device__ __forceinline__ void oct_row_labels(const float (&s00)[NC], const float (&s01)[NC], const float (&s10)[NC],
+                                               const float (&s11)[NC], const float* wk, int ky1, int kx1_0, bool vi0,
+                                               bool vi1, bool vj0, bool vj1, int (&arg)[4]) {
+  const int ky0 = ky1 + 8;
+  // two pixels per packed fp32 op (v_pk_mul_f32 / v_pk_fma_f32: the same per-element rounding
+  // as the scalar mul + fma chain), then per pixel a running top-2 with one v_med3 per class
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    f32x2_t w00, w01, w10, w11;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int kx1 = kx1_0 + 2 * pp + e, kx0 = kx1 + 8;
+      w00[e] = (vi0 && vj0) ? wk[ky0 * 16 + kx0] : 0.f;
+      w01[e] = (vi0 && vj1) ? wk[ky0 * 16 + kx1] : 0.f;
+      w10[e] = (vi1 && vj0) ? wk[ky1 * 16 + kx0] : 0.f;
+      w11[e] = (vi1 && vj1) ? wk[ky1 * 16 + kx1] : 0.f;
+    }
+    f32x2_t v[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      f32x2_t a = f32x2_t{s00[k], s00[k]} * w00;
+      a = __builtin_elementwise_fma(f32x2_t{s01[k], s01[k]}, w01, a);
+      a = __builtin_elementwise_fma(f32x2_t{s10[k], s10[k]}, w10, a);
+      a = __builtin_elementwise_fma(f32x2_t{s11[k], s11[k]}, w11, a);
+      v[k] = a;
+    }
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      // best >= second throughout, so med3(best, second, x) is the new second for every x
+      // (x > best: old best; second < x <= best: x; else second) -- the if / else-if chain
+      float best = v[0][e], second = -INFINITY;
+      int am = 0;
+#pragma unroll
+      for (int k = 1; k < NC; ++k) {
+        const float x = v[k][e];
+        am = x > best ? k : am;
+        second = __builtin_amdgcn_fmed3f(best, second, x);
+        best = fmaxf(best, x);
+      }
+      if (best - second < 0x1p-16f) {
+        float vmax = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) vmax = fmaxf(vmax, v[k][e]);
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) sum += expf(v[k][e] - vmax);
+        const float lse = logf(sum);
+        float bl = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+          const float lp = (v[k][e] - vmax) - lse;
+          if (lp > bl) { bl = lp; am = k; }
+        }
+      }
+      arg[2 * pp + e] = am;
+    }
+  }
+}
+
+template <int LABEL_DTYPE>
+__device__ __forceinline__ void store_labels4(void* labels, int64_t pix, const int (&arg)[4]) {
+  if (LABEL_DTYPE == DRNMI_U8) {
+    const uint32_t packed = static_cast<uint32_t>(arg[0]) | (static_cast<uint32_t>(arg[1]) << 8) |
+                            (static_cast<uint32_t>(arg[2]) << 16) | (static_cast<uint32_t>(arg[3]) << 24);
+    *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(labels) + pix) = packed;
+  } else {
+    int64_t* o = reinterpret_cast<int64_t*>(labels) + pix;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) o[p] = arg[p];
+  }
+}
+
+// int8 nets: the logits of the int8 seg conv from its two int32 partial planes: (float)(p0 + p1) *
+// scale + shift, fmul then fadd as store_tile_i8 (no contraction)
+template <int NC, typename B>
+__device__ __forceinline__ void load_taps_seg2_i8(const int* src, int64_t half, int w, int cs, const B& scale,
+                                                  const B& shift, int iy, int ix, float (&d)[NC]) {
+#pragma clang fp contract(off)
+  constexpr int NC4 = (NC + 3) / 4;
+  const int4* r = reinterpret_cast<const int4*>(src + (static_cast<int64_t>(iy) * w + ix) * cs);
+#pragma unroll
+  for (int k4 = 0; k4 < NC4; ++k4) {
+    const int4 a = r[k4], b = r[k4 + half / 4];
+    const int e[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * k4 + j < NC) d[4 * k4 + j] = static_cast<float>(e[j]) * scale[4 * k4 + j] + shift[4 * k4 + j];
+  }
+}
+
+// The 4 taps (19 classes each) of thread q's output block, from NHWC logit rows (cs floats per
+// pixel); SEG2: two partial planes and the bias, summed (bias + partial 0) + partial 1.
+template <int NC, bool SEG2, typename B>
+__device__ __forceinline__ void load_taps_nhwc(const float* src, int64_t half, int w, int cs, const B& bias, int iy,
+                                               int ix, float (&d)[NC]) {
+  constexpr int NC4 = (NC + 3) / 4;
+  const float4* r = reinterpret_cast<const float4*>(src + (static_cast<int64_t>(iy) * w + ix) * cs);
+#pragma unroll
+  for (int k4 = 0; k4 < NC4; ++k4) {
+    float4 v = r[k4];
+    if constexpr (SEG2) {
+      const float4 v1 = r[k4 + half / 4];
+      v = make_float4((bias[4 * k4] + v.x) + v1.x, (bias[4 * k4 + 1] + v.y) + v1.y, (bias[4 * k4 + 2] + v.z) + v1.z,
+                      (bias[4 * k4 + 3] + v.w) + v1.w);
+    }
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (4 * k4 + j < NC) d[4 * k4 + j] = e[j];
+  }
+}
+
 // Labels-only head (no log-prob planes requested: the seg_video path).  The 8 output rows
 // oy = 8*i1-4 .. 8*i1+3 all read input rows (i1-1, i1), so a thread owns 4 output columns x
 // those 8 rows: the 4 taps per class are loaded once for 32 pixels (the quad kernel re-loads
@@ -293,29 +410,12 @@ up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict_
   const int64_t plane = static_cast<int64_t>(h) * w;
   float s00[NC], s01[NC], s10[NC], s11[NC];
   if constexpr (NHWC) {
-    constexpr int NC4 = (NC + 3) / 4;
     const float* src = logits + static_cast<int64_t>(n) * plane * cs;
     const int64_t half = static_cast<int64_t>(gridDim.z) * plane * cs;   // SEG2: second partial plane
-    auto taps = [&](float (&d)[NC], int iy, int ix) {
-      const float4* r = reinterpret_cast<const float4*>(src + (static_cast<int64_t>(iy) * w + ix) * cs);
-#pragma unroll
-      for (int k4 = 0; k4 < NC4; ++k4) {
-        float4 v = r[k4];
-        if constexpr (SEG2) {
-          const float4 v1 = r[k4 + half / 4];
-          v = make_float4((bias[4 * k4] + v.x) + v1.x, (bias[4 * k4 + 1] + v.y) + v1.y, (bias[4 * k4 + 2] + v.z) + v1.z,
-                          (bias[4 * k4 + 3] + v.w) + v1.w);
-        }
-        const float e[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (4 * k4 + j < NC) d[4 * k4 + j] = e[j];
-      }
-    };
-    taps(s00, ci0, cj0);
-    taps(s01, ci0, cj1);
-    taps(s10, ci1, cj0);
-    taps(s11, ci1, cj1);
+    load_taps_nhwc<NC, SEG2>(src, half, w, cs, bias, ci0, cj0, s00);
+    load_taps_nhwc<NC, SEG2>(src, half, w, cs, bias, ci0, cj1, s01);
+    load_taps_nhwc<NC, SEG2>(src, half, w, cs, bias, ci1, cj0, s10);
+    load_taps_nhwc<NC, SEG2>(src, half, w, cs, bias, ci1, cj1, s11);
   } else {
     const float* src = logits + static_cast<int64_t>(n) * NC * plane;
 #pragma unroll
@@ -331,71 +431,188 @@ up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict_
   const int64_t HW = static_cast<int64_t>(H) * W;
   const int oy_begin = max(0, 8 * i1 - 4), oy_end = min(H, 8 * i1 + 4);
   for (int oy = oy_begin; oy < oy_end; ++oy) {
-    const int ky1 = oy + 4 - 8 * i1, ky0 = ky1 + 8;
     int arg[4];
-    // two pixels per packed fp32 op (v_pk_mul_f32 / v_pk_fma_f32: the same per-element rounding
-    // as the scalar mul + fma chain), then per pixel a running top-2 with one v_med3 per class
+    oct_row_labels<NC>(s00, s01, s10, s11, wk, oy + 4 - 8 * i1, kx1_0, vi0, vi1, vj0, vj1, arg);
+    store_labels4<LABEL_DTYPE>(labels, static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy) * W + 4 * q, arg);
+  }
+}
+
+// Labels-only head with a uniform-block fast path (the NHWC / SEG2 logits of DRNSeg.segment).
+// Thread q of row block i1 owns the 8 x 4 output pixels whose 4 taps are the low-res pixels
+// (i1 - 1 .. i1, j1 - 1 .. j1), as in up8_labels_oct_kernel.  When the 4 taps are inside the image
+// and share their argmax c with a top-2 margin of at least
+//     guard = 2^-16 / min_phase(sum w) * (1 + 2^-10) + 2^-20 * max_t |L_t[c]|
+// (up-sampling weights all >= 0), every up-sampled logit vector of the block has c on top by more
+// than 2^-16: v_c - v_k = sum_t w_t (L_t[c] - L_t[k]) >= min(margin) sum_t w_t, and the computed
+// values (one mul + 3 fma, each rounding <= 2^-24 of a partial sum bounded by sum_t w_t |L_t[k]|
+// <= sum_t w_t (|L_t[c]| + L_t[c] - L_t[k])) lose less than 2^-21 (2 max|L_t[c]| sum w + the
+// margin term) -- so the oct kernel's arithmetic would return c for all 32 pixels without its
+// near-tie fallback, and the block's labels are written without any per-pixel work.  The other
+// threads' blocks (borders, mixed argmax, small margins: ~21 % on the headline frames) are
+// compacted per wave: their taps go to LDS and all 64 lanes share their 8 x (4-pixel row) tasks,
+// each computed by oct_row_labels -- the oct kernel's arithmetic, so the labels are identical.
+// SRC: 0 = fp32 NHWC rows, 1 = two fp32 partial planes + bias (SEG2), 2 = two int32 partial planes
+// + the int8 seg conv's scale / shift (int8 nets)
+template <int NC, int LABEL_DTYPE, int SRC>
+__global__ void __launch_bounds__(256)
+up8_labels_fast_kernel(const void* __restrict__ logits, const float* __restrict__ up_w, void* __restrict__ labels,
+                       int h, int w, int cs, const float* __restrict__ bias, const float* __restrict__ scale) {
+  constexpr int TF = 4 * NC;                         // tap floats per compacted block
+  static_assert(TF % 4 == 0, "16-B tap rows");
+  __shared__ float wk[256];
+  __shared__ float wstat[2];                         // min over the 64 phases of sum w (0 if any w < 0), max sum w
+  __shared__ __attribute__((aligned(16))) float taps[4][64][TF];
+  __shared__ unsigned char slist[4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  wk[tid] = up_w[tid];
+  __syncthreads();
+  if (wave == 0) {                                   // phase (ky1, kx1) = (lane >> 3, lane & 7)
+    const int ky1 = lane >> 3, kx1 = lane & 7;
+    const float a = wk[(ky1 + 8) * 16 + kx1 + 8], b = wk[(ky1 + 8) * 16 + kx1], c = wk[ky1 * 16 + kx1 + 8],
+                d = wk[ky1 * 16 + kx1];
+    float lo = fminf(fminf(a, b), fminf(c, d)) < 0.f ? 0.f : (a + b) + (c + d), hi = (a + b) + (c + d);
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      f32x2_t w00, w01, w10, w11;
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int kx1 = kx1_0 + 2 * pp + e, kx0 = kx1 + 8;
-        w00[e] = (vi0 && vj0) ? wk[ky0 * 16 + kx0] : 0.f;
-        w01[e] = (vi0 && vj1) ? wk[ky0 * 16 + kx1] : 0.f;
-        w10[e] = (vi1 && vj0) ? wk[ky1 * 16 + kx0] : 0.f;
-        w11[e] = (vi1 && vj1) ? wk[ky1 * 16 + kx1] : 0.f;
-      }
-      f32x2_t v[NC];
-#pragma unroll
-      for (int k = 0; k < NC; ++k) {
-        f32x2_t a = f32x2_t{s00[k], s00[k]} * w00;
-        a = __builtin_elementwise_fma(f32x2_t{s01[k], s01[k]}, w01, a);
-        a = __builtin_elementwise_fma(f32x2_t{s10[k], s10[k]}, w10, a);
-        a = __builtin_elementwise_fma(f32x2_t{s11[k], s11[k]}, w11, a);
-        v[k] = a;
-      }
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        // best >= second throughout, so med3(best, second, x) is the new second for every x
-        // (x > best: old best; second < x <= best: x; else second) -- the if / else-if chain
-        float best = v[0][e], second = -INFINITY;
-        int am = 0;
-#pragma unroll
-        for (int k = 1; k < NC; ++k) {
-          const float x = v[k][e];
-          am = x > best ? k : am;
-          second = __builtin_amdgcn_fmed3f(best, second, x);
-          best = fmaxf(best, x);
-        }
-        if (best - second < 0x1p-16f) {
-          float vmax = -INFINITY;
-#pragma unroll
-          for (int k = 0; k < NC; ++k) vmax = fmaxf(vmax, v[k][e]);
-          float sum = 0.f;
-#pragma unroll
-          for (int k = 0; k < NC; ++k) sum += expf(v[k][e] - vmax);
-          const float lse = logf(sum);
-          float bl = -INFINITY;
-#pragma unroll
-          for (int k = 0; k < NC; ++k) {
-            const float lp = (v[k][e] - vmax) - lse;
-            if (lp > bl) { bl = lp; am = k; }
-          }
-        }
-        arg[2 * pp + e] = am;
-      }
+    for (int o = 32; o >= 1; o >>= 1) {
+      lo = fminf(lo, __shfl_xor(lo, o));
+      hi = fmaxf(hi, __shfl_xor(hi, o));
     }
-    const int64_t pix = static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy) * W + 4 * q;
-    if (LABEL_DTYPE == DRNMI_U8) {
-      const uint32_t packed = static_cast<uint32_t>(arg[0]) | (static_cast<uint32_t>(arg[1]) << 8) |
-                              (static_cast<uint32_t>(arg[2]) << 16) | (static_cast<uint32_t>(arg[3]) << 24);
-      *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(labels) + pix) = packed;
-    } else {
-      int64_t* o = reinterpret_cast<int64_t*>(labels) + pix;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) o[p] = arg[p];
+    if (lane == 0) {
+      wstat[0] = lo;
+      wstat[1] = hi;
     }
+  }
+  __syncthreads();
+
+  const int H = h * 8, W = w * 8;
+  const int qb = blockIdx.x * blockDim.x;
+  const int q = qb + tid;
+  const int i1 = blockIdx.y, i0 = i1 - 1;
+  const int n = blockIdx.z;
+  const bool active = 4 * q < W;                     // (no early return: the wave compacts together)
+  const int64_t plane = static_cast<int64_t>(h) * w;
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const int64_t half = static_cast<int64_t>(gridDim.z) * plane * cs;
+  auto geom = [&](int qq, int& j1, bool& vi0, bool& vi1, bool& vj0, bool& vj1) {
+    j1 = (qq + 1) >> 1;
+    vi0 = i0 >= 0;
+    vi1 = i1 < h;
+    vj0 = j1 - 1 >= 0;
+    vj1 = j1 < w;
+  };
+  int j1;
+  bool vi0, vi1, vj0, vj1;
+  geom(active ? q : qb, j1, vi0, vi1, vj0, vj1);
+  const int ci0 = vi0 ? i0 : 0, ci1 = vi1 ? i1 : 0, cj0 = vj0 ? j1 - 1 : 0, cj1 = vj1 ? j1 : 0;
+  float s[4][NC];
+  const int ty[4] = {ci0, ci0, ci1, ci1}, tx[4] = {cj0, cj1, cj0, cj1};
+  constexpr int NCP = (NC + 3) / 4 * 4;
+  float bv[NCP], sv[NCP];                            // per-class bias / shift and scale, loaded once
+#pragma unroll
+  for (int k = 0; k < NCP; ++k) {
+    bv[k] = SRC != 0 ? bias[k] : 0.f;
+    sv[k] = SRC == 2 ? scale[k] : 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if constexpr (SRC == 2)
+      load_taps_seg2_i8<NC>(static_cast<const int*>(logits) + static_cast<int64_t>(n) * plane * cs, half, w, cs, sv, bv,
+                            ty[t], tx[t], s[t]);
+    else
+      load_taps_nhwc<NC, SRC == 1>(static_cast<const float*>(logits) + static_cast<int64_t>(n) * plane * cs, half, w, cs,
+                                   bv, ty[t], tx[t], s[t]);
+  }
+
+  // ---- fast path: one argmax shared by the 4 taps with a margin above the guard
+  int cls = 0;
+  float mmin = INFINITY, amax = 0.f, vmaxabs = 0.f;   // vmaxabs: NaN / inf taps keep the block off the fast path
+  bool same = true;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    float best = s[t][0], second = -INFINITY;
+    int am = 0;
+    vmaxabs = fmaxf(vmaxabs, fabsf(s[t][0]));
+#pragma unroll
+    for (int k = 1; k < NC; ++k) {
+      const float x = s[t][k];
+      am = x > best ? k : am;
+      second = __builtin_amdgcn_fmed3f(best, second, x);
+      best = fmaxf(best, x);
+      vmaxabs = __builtin_isnan(x) ? INFINITY : fmaxf(vmaxabs, fabsf(x));
+    }
+    vmaxabs = __builtin_isnan(s[t][0]) ? INFINITY : vmaxabs;
+    if (t == 0) cls = am;
+    same = same && am == cls;
+    mmin = fminf(mmin, best - second);
+    amax = fmaxf(amax, fabsf(best));
+  }
+  const float wmin = wstat[0];
+  const bool fast = active && vi0 && vi1 && vj0 && vj1 && same && wmin > 0.f && vmaxabs < INFINITY &&
+                    mmin >= 0x1p-16f / wmin * (1.f + 0x1p-10f) + 0x1p-20f * amax;
+  if (fast) {
+    const int oy0 = 8 * i1 - 4;                      // interior block: all 8 rows exist
+    const int la[4] = {cls, cls, cls, cls};
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      store_labels4<LABEL_DTYPE>(labels, static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy0 + r) * W + 4 * q, la);
+  }
+
+  // ---- the other blocks: taps to LDS (compacted per wave), then 8 row tasks per block over all lanes
+  const bool slow = active && !fast;
+  const uint64_t sm = __ballot(slow);
+  const int nslow = __popcll(sm);
+  const int mypos = __popcll(sm & ((uint64_t(1) << lane) - 1));
+  if (slow) {
+    const int pos = mypos;
+    slist[wave][pos] = static_cast<unsigned char>(lane);
+    float4* dst = reinterpret_cast<float4*>(taps[wave][pos]);
+#pragma unroll
+    for (int i = 0; i < TF / 4; ++i) {
+      const int f = 4 * i;
+      dst[i] = make_float4(s[(f + 0) / NC][(f + 0) % NC], s[(f + 1) / NC][(f + 1) % NC], s[(f + 2) / NC][(f + 2) % NC],
+                           s[(f + 3) / NC][(f + 3) % NC]);
+    }
+  }
+  // the compacted taps are per wave (taps[wave], slist[wave]): the wave's own LDS writes land before
+  // its reads (in-order LDS per wave); no block barrier, since waves may have left above
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  // compacted: 8 nslow row tasks dealt over the 64 lanes; a wave of mostly slow blocks (no spatial
+  // coherence) gains little from that, so there each slow lane walks its own 8 rows (the oct
+  // kernel's order) from the same LDS copy
+  const bool compact = nslow <= 40;
+  const int iters = compact ? (8 * nslow + 63) / 64 : 8;
+  for (int it = 0; it < iters; ++it) {
+    const int tk = compact ? it * 64 + lane : 8 * mypos + it;
+    if (compact ? tk >= 8 * nslow : !slow) continue;
+    const int pos = tk >> 3, r = tk & 7;
+    const int sl = slist[wave][pos];
+    const int qs = qb + wave * 64 + sl;
+    int sj1;
+    bool s_vi0, s_vi1, s_vj0, s_vj1;
+    geom(qs, sj1, s_vi0, s_vi1, s_vj0, s_vj1);
+    const int oy = 8 * i1 - 4 + r;
+    if (oy < 0 || oy >= H) continue;
+    float t00[NC], t01[NC], t10[NC], t11[NC];
+    const float4* tp = reinterpret_cast<const float4*>(taps[wave][pos]);
+    float tv[TF];
+#pragma unroll
+    for (int i = 0; i < TF / 4; ++i) {
+      const float4 v = tp[i];
+      tv[4 * i] = v.x;
+      tv[4 * i + 1] = v.y;
+      tv[4 * i + 2] = v.z;
+      tv[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      t00[k] = tv[k];
+      t01[k] = tv[NC + k];
+      t10[k] = tv[2 * NC + k];
+      t11[k] = tv[3 * NC + k];
+    }
+    int arg[4];
+    oct_row_labels<NC>(t00, t01, t10, t11, wk, r, 4 * qs + 4 - 8 * sj1, s_vi0, s_vi1, s_vj0, s_vj1, arg);
+    store_labels4<LABEL_DTYPE>(labels, static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy) * W + 4 * qs, arg);
   }
 }
 
@@ -629,9 +846,11 @@ extern "C" int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const floa
   dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (label_dtype == DRNMI_I64)
-    hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_I64, true>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs);
+    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_I64, 0>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs,
+                       nullptr, nullptr);
   else
-    hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_U8, true>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs);
+    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_U8, 0>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs,
+                       nullptr, nullptr);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -648,9 +867,33 @@ extern "C" int drnmi_up8_labels_seg2(const float* partials, int32_t cs, const fl
   dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (label_dtype == DRNMI_I64)
-    hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_I64, true, true>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs, bias);
+    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_I64, 1>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
+                       bias, nullptr);
   else
-    hipLaunchKernelGGL((up8_labels_oct_kernel<19, DRNMI_U8, true, true>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs, bias);
+    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_U8, 1>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
+                       bias, nullptr);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_up8_labels_seg2_i8(const int32_t* partials, int32_t cs, const float* scale, const float* shift,
+                                        const float* up_w, void* labels, int32_t label_dtype, int32_t n, int32_t c,
+                                        int32_t h, int32_t w, void* stream) {
+  if (partials == nullptr || scale == nullptr || shift == nullptr || up_w == nullptr || labels == nullptr || n <= 0 ||
+      h <= 0 || w <= 0)
+    return DRNMI_EINVAL;
+  if (c != 19) return DRNMI_ENOTSUP;
+  if (cs < 20 || cs % 4 != 0 || (reinterpret_cast<uintptr_t>(partials) & 15) != 0) return DRNMI_EINVAL;
+  if (label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64) return DRNMI_EINVAL;
+  if (h + 1 > 65535 || n > 65535) return DRNMI_EINVAL;
+  const int W = w * 8;
+  dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (label_dtype == DRNMI_I64)
+    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_I64, 2>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
+                       shift, scale);
+  else
+    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_U8, 2>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
+                       shift, scale);
   return static_cast<int>(hipGetLastError());
 }
 

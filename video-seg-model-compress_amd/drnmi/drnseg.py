@@ -194,12 +194,17 @@ class DRNSeg(nn.Module):
                 or not labels.is_contiguous() or labels.device != frames_u8.device:
             raise ValueError(f"labels must be a contiguous uint8/int64 [{frames_u8.shape[0]}, {oh}, {ow}] tensor "
                              f"on {frames_u8.device}")
+        hook, head_idx = self.timing_hook, len(plan.packed.graph.nodes)   # (the head's launch index)
+        if hook is not None:
+            hook(head_idx, None, True)
         if path == "seg2":
             plan.head_labels_seg2(self._up_plane(plan.packed.device), stream, labels)
         elif path == "nhwc":
             plan.head_labels_nhwc(self._up_plane(plan.packed.device), stream, labels)
         else:
             self._head(plan, stream, None, labels)
+        if hook is not None:
+            hook(head_idx, None, False)
         return labels
 
     def _head(self, plan, stream, logprobs, labels):

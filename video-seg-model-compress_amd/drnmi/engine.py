@@ -50,11 +50,12 @@ INT8_MIN_COUT = 256
 # (cin_stride, cout, ks, stride, dil) served by the LDS-patch kernel (bf16 only; include/drnmi.h)
 # (32 -> 64 stride 2 runs faster on the K-32 LDS-DMA implicit GEMM: 67 vs 108 us per 4 frames)
 PATCH_SHAPES = {(8, 16, 7, 1, 1), (16, 16, 3, 1, 1), (16, 32, 3, 2, 1)}
-# fp32x: the same full-resolution layers on the split-bf16 patch kernel (fp32 in / out)
-X6_PATCH_SHAPES = PATCH_SHAPES
-# fp32: the same layers on the exact-fp32 patch kernel (csrc/patch_f32.hip, f32-input MFMA; the stem
-# reads the uint8 frame on the segment() path)
+# fp32 and fp32x inference: the same full-resolution layers on the exact-fp32 patch kernel
+# (csrc/patch_f32.hip, f32-input MFMA; the stem reads the uint8 frame on the segment() path) --
+# faster than the split-bf16 patch kernels (2.0 vs 2.4 ms per 8-frame step) and exact fp32
 F32_PATCH_SHAPES = PATCH_SHAPES
+# the fp32x fine-tune keeps these layers on the split-bf16 patch kernels (drnmi/train.py)
+X6_PATCH_SHAPES = PATCH_SHAPES
 STEM_U8_K = 224     # fused u8 stem: k = kh*32 + kw*4 + c
 
 
@@ -282,8 +283,7 @@ class PackedNet:
                 if ni in self.i8_nodes:
                     self._pack_int8(nd, full, scale, cout)
                     continue
-                if self.precision == "fp32x" and ((cs >= X6_MIN_CIN and kh in (1, 3)) or
-                                                  _uses_patch(nd, cs, "fp32x")):
+                if self.precision == "fp32x" and cs >= X6_MIN_CIN and kh in (1, 3):
                     nd.x6 = True
                     nd.wpk = split3_bf16(full)
                     nd.scale_folded = False
@@ -308,8 +308,8 @@ class PackedNet:
                 wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
                 full = torch.zeros(stem.cout_pad, STEM_U8_K, device=self.device, dtype=torch.float32)
                 full[:w.shape[0]] = wp.reshape(w.shape[0], STEM_U8_K)
-                self.stem_u8_w = split3_bf16(full) if self.base == "fp32x" else full.to(self.tdtype).contiguous()
-                # (fp32: the f32 weights in the same kh*32 + kw*4 + c layout, patch_f32.hip SRC 0)
+                # (fp32 / fp32x: the f32 weights in the same kh*32 + kw*4 + c layout, patch_f32.hip SRC 0)
+                self.stem_u8_w = full.to(self.tdtype).contiguous()
             self._front_packs = {}
             self.front_eligible = self._front_shapes_ok()
             self.block64_pairs = self._block64_pairs()
@@ -502,8 +502,7 @@ def _uses_patch(nd: ConvNode, cin_stride: int, precision: str) -> bool:
     shape = (cin_stride, c.out_channels, c.kernel_size[0], c.stride[0], c.dilation[0])
     if nd.res is not None or nd.out_fp32_nchw:
         return False
-    return (precision == "bf16" and shape in PATCH_SHAPES) or (precision == "fp32x" and shape in X6_PATCH_SHAPES) \
-        or (precision == "fp32" and shape in F32_PATCH_SHAPES)
+    return (precision == "bf16" and shape in PATCH_SHAPES) or (precision in ("fp32", "fp32x") and shape in F32_PATCH_SHAPES)
 
 
 # bf16: fold 1x1 downsamples into the block's last conv (PackedNet._fuse_downsamples)
@@ -687,14 +686,16 @@ class Plan:
 
     def _setup_seg_fused(self, i: int):
         """The seg classifier folded into its producer's epilogue (drnmi_conv_stag_seg) when that
-        producer is a 512-channel staggered-tile conv whose output nothing else reads."""
+        producer is a 512-channel staggered-tile conv whose output nothing else reads: bf16 nets
+        (fp32 partial logits, bias added by the head) and int8 nets (the int8 seg conv on the
+        producer's int8 output: int32 partials, the seg conv's dequant applied by the head)."""
         self.seg_fused = None
         if not SEG_FUSE or not self.fuse:
             return
         nodes = self.packed.graph.nodes
         seg = nodes[i]
         prod = [j for j, nd in enumerate(nodes) if nd.dst == seg.x_val and j not in self.skip]
-        if len(prod) != 1 or seg.x_val != seg.src or seg.r_val or not seg.scale_folded:
+        if len(prod) != 1 or seg.x_val != seg.src or seg.r_val:
             return
         j = prod[0]
         a = self.args[j]
@@ -702,17 +703,22 @@ class Plan:
             return
         if any(nodes[j].dst in self._reads_of[k] for k in range(len(nodes)) if k != i):
             return
-        if a.cout != 512 or a.scale or a.res or a.x2 or seg.k != a.cout or seg.cout_pad < 32:
+        i8 = seg.i8 and nodes[j].i8
+        if i8 != (seg.i8 or nodes[j].i8) or (not i8 and not seg.scale_folded):
+            return
+        if a.cout != 512 or a.res or a.x2 or seg.k != a.cout or seg.cout_pad < 32 or (a.scale and not i8):
+            return
+        if i8 and a.out_dtype != _lib.DRNMI_I8:
             return
         name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
-        if name is None or name.decode() != "conv_stag_kernel":
+        if name is None or name.decode() != ("conv_i8_stag_kernel" if i8 else "conv_stag_kernel"):
             return
         lh, lw = self.shapes[seg.dst]
         if "seg_part" not in self.bufs:
-            self.bufs["seg_part"] = torch.empty(2 * self.n * lh * lw * self.SEG_NHWC_CS, dtype=torch.float32,
-                                                device=self.packed.device)
+            self.bufs["seg_part"] = torch.empty(2 * self.n * lh * lw * self.SEG_NHWC_CS,
+                                                dtype=torch.int32 if i8 else torch.float32, device=self.packed.device)
         self.seg_fused = {"conv": j, "seg_w": seg.wpk.data_ptr(), "seg_k_pad": seg.k_pad, "seg_rows": seg.cout_pad,
-                          "bias": seg.shift.data_ptr()}
+                          "bias": seg.shift.data_ptr(), "i8": i8, "scale": seg.scale.data_ptr()}
 
     def labels_path(self, use_torch_up: bool = False) -> str:
         """How segment() produces labels on this plan: "seg2" (seg folded into the last conv),
@@ -956,8 +962,14 @@ class Plan:
         the last conv (drnmi_up8_labels_seg2)."""
         lh, lw = self.shapes["logits"]
         lab_dtype = _lib.DRNMI_I64 if labels.dtype == torch.int64 else _lib.DRNMI_U8
+        sf = self.seg_fused
+        if sf["i8"]:
+            _lib.check(_lib.load().drnmi_up8_labels_seg2_i8(
+                self.bufs["seg_part"].data_ptr(), self.SEG_NHWC_CS, sf["scale"], sf["bias"], up_w.data_ptr(),
+                labels.data_ptr(), lab_dtype, self.n, 19, lh, lw, ctypes.c_void_p(stream)), "up8_labels_seg2_i8")
+            return
         _lib.check(_lib.load().drnmi_up8_labels_seg2(
-            self.bufs["seg_part"].data_ptr(), self.SEG_NHWC_CS, self.seg_fused["bias"], up_w.data_ptr(),
+            self.bufs["seg_part"].data_ptr(), self.SEG_NHWC_CS, sf["bias"], up_w.data_ptr(),
             labels.data_ptr(), lab_dtype, self.n, 19, lh, lw, ctypes.c_void_p(stream)), "up8_labels_seg2")
 
     def head_bilinear(self, stream: int, logprobs: torch.Tensor | None, labels: torch.Tensor | None):

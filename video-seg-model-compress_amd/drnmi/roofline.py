@@ -113,7 +113,7 @@ def launch_work(plan, video: bool = True):
         # written by it and read by the head instead
         j, i = segf["conv"], plan.seg_idx
         oh, ow = plan.shapes[nodes[j].dst]
-        act = plan.n * oh * ow * nodes[j].conv.out_channels * esz
+        act = plan.n * oh * ow * nodes[j].conv.out_channels * (1 if nodes[j].i8 else esz)   # int8 nets: int8
         lh, lw = plan.shapes[nodes[i].dst]
         logits = plan.n * lh * lw * nodes[i].conv.out_channels * 4
         part = 2 * plan.n * lh * lw * plan.SEG_NHWC_CS * 4
