@@ -206,45 +206,13 @@ conv_igemm_kernel(const drnmi_conv_args p) {
     if (more) load_tiles(kt + 1);
     const T* As = smem + cur * BUF;
     const T* Bs = As + BM * LDK;
-    if constexpr (sizeof(T) == 4) {
-      // f32: the 8 k-slices of the step interleaved over the FM x FN accumulators, so consecutive
-      // MFMAs are independent (16x16x4 f32: 32-cycle issue, 40-cycle dependent latency); each
-      // accumulator still sees its k in mma_step<float>'s order, so the sums are bit-identical
-      float4 a4[FM][2], b4[FN][2];
 #pragma unroll
-      for (int fm = 0; fm < FM; ++fm) {
-        const T* ap = As + (wm * WTM + fm * 16 + frag_row) * LDK + frag_k;
-        a4[fm][0] = reinterpret_cast<const float4*>(ap)[0];
-        a4[fm][1] = reinterpret_cast<const float4*>(ap)[1];
-      }
+    for (int fm = 0; fm < FM; ++fm) {
+      const T* ap = As + (wm * WTM + fm * 16 + frag_row) * LDK + frag_k;
 #pragma unroll
       for (int fn = 0; fn < FN; ++fn) {
         const T* bp = Bs + (wn * WTN + fn * 16 + frag_row) * LDK + frag_k;
-        b4[fn][0] = reinterpret_cast<const float4*>(bp)[0];
-        b4[fn][1] = reinterpret_cast<const float4*>(bp)[1];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm)
-#pragma unroll
-          for (int fn = 0; fn < FN; ++fn) {
-            const float4& av = a4[fm][j >> 2];
-            const float4& bv = b4[fn][j >> 2];
-            const int e = j & 3;
-            const float ae = e == 0 ? av.x : e == 1 ? av.y : e == 2 ? av.z : av.w;
-            const float be = e == 0 ? bv.x : e == 1 ? bv.y : e == 2 ? bv.z : bv.w;
-            acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x4f32(ae, be, acc[fm][fn], 0, 0, 0);
-          }
-    } else {
-#pragma unroll
-      for (int fm = 0; fm < FM; ++fm) {
-        const T* ap = As + (wm * WTM + fm * 16 + frag_row) * LDK + frag_k;
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) {
-          const T* bp = Bs + (wn * WTN + fn * 16 + frag_row) * LDK + frag_k;
-          mma_step<T>(acc[fm][fn], ap, bp);
-        }
+        mma_step<T>(acc[fm][fn], ap, bp);
       }
     }
     if (more) store_tiles(cur ^ 1);
