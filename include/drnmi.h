@@ -364,6 +364,7 @@ int drnmi_pack_conv_weight(const float* w, int32_t cout, int32_t cin, int32_t ks
  *   as drnmi_pack_conv_weight, no row scale), [10] first element index of the entry (prefix sum
  *   of rows_pad*k_pad over the entries before it), [11] 0.
  * total = sum of rows_pad*k_pad.  Values are bit-identical to the per-layer calls.
+ * Limits: n <= 512, ks <= 7, kin_stride and k_pad multiples of 4, out / planes 16-B aligned.
  * drnmi_pack_table_check validates a HOST copy of the table before it is uploaded. */
 #define DRNMI_PACK_ENTRY_WORDS 12
 int drnmi_pack_table_check(const int64_t* table_host, int32_t n, int64_t* total_out);
@@ -394,6 +395,15 @@ int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float* y, const 
                          const float* invstd, const float* gamma, int32_t relu, int64_t rows,
                          int32_t C, float* dy, float* dres, int32_t dres_accumulate, float* dgamma,
                          float* dbeta, int32_t grad_accumulate, void* ws, void* stream);
+
+/* drnmi_bn_act_bwd_f32 for a residual-free BN + ReLU (relu = 1, res = NULL, dres = NULL) without z:
+ * the mask z > 0 is recomputed from y with the forward's own arithmetic (bn_act's rounding order),
+ * so it is bit-identical to reading z and each pass reads one fp32 tensor less.  gamma / beta as
+ * given to drnmi_bn_act_f32 (NULL-able); mean/invstd/gamma/beta 16-byte aligned.
+ * (semantic_seg.py:166-230 backward through lmodels/drn.py:49-65 / :86-106's bn + relu.) */
+int drnmi_bn_relu_bwd_y_f32(const float* dz, const float* y, const float* mean, const float* invstd,
+                            const float* gamma, const float* beta, int64_t rows, int32_t C, float* dy,
+                            float* dgamma, float* dbeta, int32_t grad_accumulate, void* ws, void* stream);
 
 /* out[c] (+)= sum over rows of x[row][c], c < cvalid (row stride C).  Conv-bias gradient
  * (seg 1x1 + bias, lmodels/drnseg.py:278-284). */

@@ -25,11 +25,22 @@ SHAPES = [  # name, n, h, w, cin, cout, ks, stride, pad, dil, res, split
     ("l4 128 +res b8", 8, 128, 256, 128, 128, 3, 1, 1, 1, True, False),
     ("l4.0 ds 1x1 s2 b8", 8, 256, 512, 64, 128, 1, 2, 0, 1, False, False),
     ("l5.0 ds 1x1 b8", 8, 128, 256, 128, 256, 1, 1, 0, 1, False, False),
+    ("ft 1x1 1024-256", 2, 128, 96, 1024, 256, 1, 1, 0, 1, False, True),
+    ("ft 1x1 256-1024", 2, 128, 96, 256, 1024, 1, 1, 0, 1, True, True),
+    ("ft 1x1 2048-512", 2, 128, 96, 2048, 512, 1, 1, 0, 1, False, True),
+    ("ft 1x1 512-2048", 2, 128, 96, 512, 2048, 1, 1, 0, 1, True, True),
+    ("ft 1x1 512-256", 2, 128, 96, 512, 256, 1, 1, 0, 1, False, True),
+    ("ft 3x3 256 d2", 2, 128, 96, 256, 256, 3, 1, 2, 2, False, True),
+    ("ft l3 1x1 256-64", 2, 256, 192, 256, 64, 1, 1, 0, 1, False, True),
+    ("ft l3 1x1 64-256", 2, 256, 192, 64, 256, 1, 1, 0, 1, True, True),
 ]
 SEL = os.environ.get("SHAPES")
 if SEL:
     SHAPES = [sh for sh in SHAPES if any(k in sh[0] for k in SEL.split(","))]
 VARIANTS = [(-1 if v == "auto" else int(v)) for v in os.environ.get("VARIANTS", "auto").split(",")]
+# SPLITS=1,2,4: force split-K counts on the split shapes (tile = variant + 4 * splits; the variant
+# is the auto one when VARIANTS=auto)
+SPLITS = [int(v) for v in os.environ.get("SPLITS", "0").split(",")]
 lib = _lib.load()
 for name, n, h, w, cin, cout, ks, s, pad, dil, res, split in SHAPES:
     g = torch.Generator(device=DEV).manual_seed(cin + cout + ks)
@@ -53,16 +64,17 @@ for name, n, h, w, cin, cout, ks, s, pad, dil, res, split in SHAPES:
     a.ks, a.stride, a.pad, a.dil = ks, s, pad, dil
     a.k, a.k_pad = k, wpk.shape[1]
     a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_F32X3, _lib.DRNMI_F32, -1, _lib.ALGO_IGEMM
-    ws = None
-    if split and VARIANTS != [-1]:
-        continue                      # (split-K workspaces are sized for the auto variant)
-    if split:
-        nb = lib.drnmi_conv_workspace_bytes(ctypes.byref(a))
-        ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=DEV)
-        a.ws, a.ws_bytes = ws.data_ptr(), nb
     st = ctypes.c_void_p(_lib.stream_ptr())
-    for var in VARIANTS:
+    combos = [(v, 0) for v in VARIANTS] if not split else [(v, sp) for v in VARIANTS for sp in SPLITS]
+    for var, sp in combos:
       a.tile = var
+      if sp > 0:
+          a.tile = (var if var >= 0 else 0 if cout % 256 == 0 else 3 if cout % 128 == 0 else 2) + 4 * sp
+      if split:                       # workspace for this launch's own split count
+          a.ws, a.ws_bytes = None, 0
+          nb = lib.drnmi_conv_workspace_bytes(ctypes.byref(a))
+          ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=DEV)
+          a.ws, a.ws_bytes = ws.data_ptr(), nb
       kname = lib.drnmi_conv_kernel_name(ctypes.byref(a))
       if kname is None:
         continue
@@ -80,5 +92,5 @@ for name, n, h, w, cin, cout, ks, s, pad, dil, res, split in SHAPES:
         best = us if best is None else min(best, us)
       flops = 2.0 * n * ho * wo * cout * cin * ks * ks
       sha = hashlib.sha1(y.cpu().numpy().tobytes()).hexdigest()[:12]
-      print(f"{name:22s} {kname.decode():28s} {best:9.1f} us  {flops / best / 1e6:6.1f} TF  "
+      print(f"{name:22s} {kname.decode():28s} S{sp} {best:9.1f} us  {flops / best / 1e6:6.1f} TF  "
             f"({flops / best / 1e6 / (2500 / 6):.3f} of 417)  sha {sha}", flush=True)

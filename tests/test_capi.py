@@ -67,6 +67,15 @@ def test_pack_table_check_without_gpu():
     bad = tab.copy()
     bad[0, 8] = 100                                   # k_pad < ks * ks * kin_stride
     assert lib.drnmi_pack_table_check(bad.ctypes.data_as(ctypes.c_void_p), 2, ctypes.byref(tot)) == -1
+    bad = tab.copy()
+    bad[0, 6], bad[0, 8] = 34, 308                    # kin_stride not a multiple of 4 (4-column stores)
+    assert lib.drnmi_pack_table_check(bad.ctypes.data_as(ctypes.c_void_p), 2, ctypes.byref(tot)) == -1
+    bad = tab.copy()
+    bad[0, 5], bad[0, 8] = 9, 81 * 32                 # ks > 7 (the LDS tile holds up to 7x7 taps)
+    assert lib.drnmi_pack_table_check(bad.ctypes.data_as(ctypes.c_void_p), 2, ctypes.byref(tot)) == -1
+    bad = tab.copy()
+    bad[1, 2] += 8                                    # planes not 16-B aligned
+    assert lib.drnmi_pack_table_check(bad.ctypes.data_as(ctypes.c_void_p), 2, ctypes.byref(tot)) == -1
     assert lib.drnmi_pack_conv_weights_batched(None, 2, 10, None) == -1
 
 

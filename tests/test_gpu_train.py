@@ -219,6 +219,7 @@ def _wgrad(dy_nhwc, x_nhwc, cin, cout, ks, stride, pad, dil, ho, wo, accumulate=
     (512, 512, 19, 32, 1, 1, 0, 1, 12, 10),
     (256, 256, 512, 512, 3, 1, 4, 4, 16, 16),
     (96, 128, 200, 256, 3, 1, 1, 1, 13, 17),
+    (256, 256, 256, 256, 3, 1, 2, 2, 48, 40),
 ])
 @pytest.mark.parametrize("x6", [False, True])
 def test_wgrad_kernel_matches_torch(cin, cs, cout, dys, ks, stride, pad, dil, h, w, x6):
@@ -283,6 +284,30 @@ def test_bn_and_ce_kernels_match_torch():
     assert TC.rel_err(dy.cpu(), yt.grad) <= 1e-4
     assert TC.rel_err(dg.cpu(), gt.grad) <= 1e-4 and TC.rel_err(db.cpu(), bt.grad) <= 1e-5
     assert TC.rel_err(dres.cpu(), dz * (z_ref.detach() > 0)) == 0.0
+    # residual-free BN + ReLU: the backward that recomputes the mask from y is bit-identical to the
+    # one that reads z (many y sit exactly on the mean: ties at bn_value == 0 included)
+    yq = yd.clone()
+    yq[::7] = mean
+    _lib.check(lib.drnmi_bn_stats_f32(vp(yq), rows, C, 1e-5, 0.1, vp(mean), vp(invstd), None, None, None, vp(ws), sp),
+               "stats q")
+    bz = bd.clone()
+    bz[::3] = 0.0
+    zq = torch.empty_like(yq)
+    _lib.check(lib.drnmi_bn_act_f32(vp(yq), vp(mean), vp(invstd), vp(gd), vp(bz), None, 1, rows, C, vp(zq), sp), "act q")
+    outs = []
+    for from_y in (False, True):
+        dyq, dgq, dbq = torch.empty_like(yq), torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        if from_y:
+            _lib.check(lib.drnmi_bn_relu_bwd_y_f32(vp(dzd), vp(yq), vp(mean), vp(invstd), vp(gd), vp(bz), rows, C,
+                                                   vp(dyq), vp(dgq), vp(dbq), 0, vp(ws), sp), "bwd y")
+        else:
+            _lib.check(lib.drnmi_bn_act_bwd_f32(vp(dzd), vp(zq), vp(yq), vp(mean), vp(invstd), vp(gd), 1, rows, C,
+                                                vp(dyq), None, 0, vp(dgq), vp(dbq), 0, vp(ws), sp), "bwd z")
+        outs.append((dyq, dgq, dbq))
+    torch.cuda.synchronize()
+    assert int((zq == 0).sum()) > rows * C // 4
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
     # cross entropy on log-probs with ignore_index
     lp = F.log_softmax(torch.randn(2, 19, 24, 40), 1).requires_grad_(True)
     t = torch.randint(0, 19, (2, 24, 40))

@@ -474,14 +474,15 @@ hipError_t launch_x6(const drnmi_conv_args& p, int splits, hipStream_t s) {
 
 // 0: 256-channel tile (8 waves), 1: 128 (4 waves), 2: 64 (4 waves)
 // variants: 0 <K, 128, 2> (256 channels, 8 waves), 1 <K, 128, 1> (128, 4 waves), 2 <K, 64, 1> (64, 4
-// waves), 3 <K, 64, 2> (128 channels, 8 waves); a drnmi_conv_args.tile in 0..3 forces one (tests,
-// micro-benchmarks)
+// waves), 3 <K, 64, 2> (128 channels, 8 waves); a drnmi_conv_args.tile >= 0 forces variant
+// tile % 4 and, when tile >= 4, tile / 4 split-K partitions (tests, micro-benchmarks; split-K only
+// with a caller workspace)
 constexpr int kX6Bco[4] = {256, 128, 64, 128};
 constexpr int kNumX6 = 4;
 // 128-channel layers take the 8-wave tile (two waves per SIMD): D-22 layer4 492 vs 511 us, its 1x1
 // stride-2 downsample 64 vs 83 us at batch 8 (scripts/x6_micro.py, profiles/r7_x6)
 int x6_auto_variant(const drnmi_conv_args& p) { return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 3 : 2; }
-int x6_variant(const drnmi_conv_args& p) { return p.tile >= 0 && p.tile < kNumX6 ? p.tile : x6_auto_variant(p); }
+int x6_variant(const drnmi_conv_args& p) { return p.tile >= 0 ? p.tile % kNumX6 : x6_auto_variant(p); }
 
 // Split-K count for a launch whose tiles leave CUs idle (one workgroup per CU: 96 tiles of the
 // fine-tune's 2 x 128 x 96 layer5 convs used 96 of 256 CUs).  Cost model per split count S:
@@ -502,6 +503,10 @@ int x6_num_cus() {
 int x6_splits(const drnmi_conv_args& p) {
   // the partials are [split][m][cout] rows written as float4: only cout % 4 == 0 splits
   if (p.cout % 4 != 0) return 1;
+  if (p.tile >= kNumX6) {
+    const int S = p.tile / kNumX6;
+    return S < 1 ? 1 : (S > p.k_pad / kBK ? p.k_pad / kBK : S);
+  }
   const int cus = x6_num_cus();
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const int64_t tiles = ((M + kBPX - 1) / kBPX) * ((p.cout + kX6Bco[x6_variant(p)] - 1) / kX6Bco[x6_variant(p)]);

@@ -68,52 +68,123 @@ pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int ks, int k
   }
 }
 
-// one packed element of entry e (table layout: include/drnmi.h drnmi_pack_conv_weights_batched)
-__device__ __forceinline__ float pack_value(const float* __restrict__ w, int cout, int cin, int ks, int kin_stride,
-                                            int mode, int row, int k) {
-  const int tap = k / kin_stride;
-  const int c = k - tap * kin_stride;
-  float v = 0.f;
-  if (tap < ks * ks) {
-    const int kh = tap / ks, kw = tap - (tap / ks) * ks;
-    if (mode == 0) {
-      if (row < cout && c < cin) v = w[((static_cast<int64_t>(row) * cin + c) * ks + kh) * ks + kw];
-    } else if (row < cin && c < cout) {
-      v = w[((static_cast<int64_t>(c) * cin + row) * ks + (ks - 1 - kh)) * ks + (ks - 1 - kw)];
-    }
-  }
-  return v;
-}
+// All entries of the table in one launch, as LDS-staged transposes.  An element per thread with the
+// OIHW source gathered per element ran at ~1 TB/s (0.61 ms of the fp32x fine-tune step): the dgrad
+// layout reads w[co][ci] at stride cin * ks * ks per consecutive output.  Here a tile is 32 output
+// rows x CT channel columns x all ks * ks taps.  Its source is CT (dgrad) or 32 (forward) runs of
+// contiguous floats -- w[co][ci0 .. ci0 + n)[taps] -- read coalesced into LDS.  The tile is then
+// written tap by tap, four consecutive k per thread: 16-B fp32 stores, 8-B stores per bf16 plane.
+// 37 KB of LDS per workgroup keeps four workgroups (16 waves) per CU on this memory-bound pass.
+// Pure data movement plus split3_kernel's arithmetic: bit-identical to the per-layer calls.
+constexpr int kPackRows = 32;
+constexpr int kPackMaxEntries = 512;
+constexpr int kPackLds = kPackRows * (32 * 9 + 1);        // 3x3 taps x 32 columns, run stride + 1
+// columns per tile (a multiple of 4): 32 up to 3x3, 4 up to 7x7 (4 x 49 <= 32 x 9)
+__device__ __forceinline__ int pack_cols(int taps) { return taps <= 9 ? 32 : 4; }
 
-// all entries of the table in one grid-stride pass; the entry of element i is found by a binary
-// search over the entries' first-element indices (word 10)
 __global__ void __launch_bounds__(kThreads)
-pack_batched_kernel(const int64_t* __restrict__ tab, int n, int64_t total) {
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    int lo = 0, hi = n - 1;
+pack_batched_kernel(const int64_t* __restrict__ tab, int n) {
+  __shared__ int first[kPackMaxEntries + 1];              // first tile of each entry (prefix sum)
+  __shared__ float L[kPackLds];
+  const int t = threadIdx.x;
+  for (int e = t; e < n; e += kThreads) {
+    const int64_t* q = tab + static_cast<int64_t>(e) * DRNMI_PACK_ENTRY_WORDS;
+    const int taps = static_cast<int>(q[5] * q[5]);
+    first[e + 1] = static_cast<int>(((q[7] + kPackRows - 1) / kPackRows) * ((q[6] + pack_cols(taps) - 1) / pack_cols(taps)));
+  }
+  __syncthreads();
+  if (t == 0) {
+    first[0] = 0;
+    for (int e = 0; e < n; ++e) first[e + 1] += first[e];
+  }
+  __syncthreads();
+  const int tiles = first[n];
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    int lo = 0, hi = n - 1;                                  // entry: last e with first[e] <= tile
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (tab[mid * DRNMI_PACK_ENTRY_WORDS + 10] <= i) lo = mid;
+      if (first[mid] <= tile) lo = mid;
       else hi = mid - 1;
     }
-    const int64_t* e = tab + lo * DRNMI_PACK_ENTRY_WORDS;
-    const int64_t j = i - e[10];
-    const int k_pad = static_cast<int>(e[8]);
-    const int row = static_cast<int>(j / k_pad);
-    const int k = static_cast<int>(j - static_cast<int64_t>(row) * k_pad);
-    const float v = pack_value(reinterpret_cast<const float*>(e[0]), static_cast<int>(e[3]), static_cast<int>(e[4]),
-                               static_cast<int>(e[5]), static_cast<int>(e[6]), static_cast<int>(e[9]), row, k);
-    reinterpret_cast<float*>(e[1])[j] = v;
-    if (e[2] != 0) {                                   // split3_kernel's arithmetic
-      bf16_t* pl = reinterpret_cast<bf16_t*>(e[2]);
-      const int64_t m = e[7] * e[8];
-      const bf16_t a = f32_to_bf16(v);
-      const float r = v - bf16_to_f32(a);
-      const bf16_t b = f32_to_bf16(r);
-      pl[j] = a;
-      pl[m + j] = b;
-      pl[2 * m + j] = f32_to_bf16(r - bf16_to_f32(b));
+    const int64_t* q = tab + static_cast<int64_t>(lo) * DRNMI_PACK_ENTRY_WORDS;
+    const float* __restrict__ w = reinterpret_cast<const float*>(q[0]);
+    float* __restrict__ out = reinterpret_cast<float*>(q[1]);
+    bf16_t* __restrict__ pl = reinterpret_cast<bf16_t*>(q[2]);
+    const int cout = static_cast<int>(q[3]), cin = static_cast<int>(q[4]), ks = static_cast<int>(q[5]);
+    const int kst = static_cast<int>(q[6]), rows_pad = static_cast<int>(q[7]), k_pad = static_cast<int>(q[8]);
+    const int mode = static_cast<int>(q[9]);
+    const int64_t m = static_cast<int64_t>(rows_pad) * k_pad;
+    const int T = ks * ks;
+    const int CT = pack_cols(T);
+    const int ntc = (kst + CT - 1) / CT;
+    const int local = tile - first[lo];
+    const int row0 = (local / ntc) * kPackRows;
+    const int col0 = (local % ntc) * CT;
+    // runs: forward: run r = output row co = row0 + r, its elements ci = col0 + c (c < CT);
+    //       dgrad:   run r = column co = col0 + r, its elements ci = row0 + c (c < 32)
+    const int nrun = mode == 0 ? kPackRows : CT;
+    const int nel = mode == 0 ? CT : kPackRows;
+    const int run_co0 = mode == 0 ? row0 : col0;
+    const int ci0 = mode == 0 ? col0 : row0;
+    const int rlen = nel * T;
+    const int rstr = rlen + 1;
+    const int nci = cin - ci0 < nel ? cin - ci0 : nel;       // valid elements of a run: nci * T floats
+    __syncthreads();                                         // the previous tile's reads of L
+    for (int idx = t; idx < nrun * rlen; idx += kThreads) {
+      const int r = idx / rlen;
+      const int j = idx - r * rlen;
+      const int co = run_co0 + r;
+      float v = 0.f;
+      if (co < cout && j < nci * T) v = w[(static_cast<int64_t>(co) * cin + ci0) * T + j];
+      L[r * rstr + j] = v;
+    }
+    __syncthreads();
+    // thread: 4 consecutive columns c4 .. c4 + 3 of (row r, tap); kst % 4 == 0 (table check)
+    const int cq = CT / 4;
+    for (int idx = t; idx < kPackRows * T * cq; idx += kThreads) {
+      const int c4 = (idx % cq) * 4;
+      const int rt = idx / cq;
+      const int tap = rt % T;
+      const int r = rt / T;
+      const int row = row0 + r, col = col0 + c4;
+      if (row >= rows_pad || col >= kst) continue;
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)   // forward: run r, ci c, tap; dgrad: run c, ci r, flipped tap
+        v[u] = mode == 0 ? L[r * rstr + (c4 + u) * T + tap] : L[(c4 + u) * rstr + r * T + (T - 1 - tap)];
+      const int64_t o = static_cast<int64_t>(row) * k_pad + tap * kst + col;
+      *reinterpret_cast<float4*>(out + o) = make_float4(v[0], v[1], v[2], v[3]);
+      if (pl != nullptr) {                                   // split3_kernel's arithmetic
+        uint16_t h1[4], h2[4], h3[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bf16_t a = f32_to_bf16(v[u]);
+          const float rr = v[u] - bf16_to_f32(a);
+          const bf16_t b = f32_to_bf16(rr);
+          h1[u] = a;
+          h2[u] = b;
+          h3[u] = f32_to_bf16(rr - bf16_to_f32(b));
+        }
+        *reinterpret_cast<uint2*>(pl + o) = make_uint2(h1[0] | (uint32_t(h1[1]) << 16), h1[2] | (uint32_t(h1[3]) << 16));
+        *reinterpret_cast<uint2*>(pl + m + o) = make_uint2(h2[0] | (uint32_t(h2[1]) << 16), h2[2] | (uint32_t(h2[3]) << 16));
+        *reinterpret_cast<uint2*>(pl + 2 * m + o) = make_uint2(h3[0] | (uint32_t(h3[1]) << 16), h3[2] | (uint32_t(h3[3]) << 16));
+      }
+    }
+    // the k tail past the last tap (k_pad > ks * ks * kst) is zero; column tile 0 writes it
+    const int tail = k_pad - T * kst;
+    if (col0 == 0 && tail > 0) {
+      for (int idx = t; idx < kPackRows * tail; idx += kThreads) {
+        const int r = idx / tail;
+        const int row = row0 + r;
+        if (row >= rows_pad) continue;
+        const int64_t o = static_cast<int64_t>(row) * k_pad + T * kst + (idx - r * tail);
+        out[o] = 0.f;
+        if (pl != nullptr) {
+          pl[o] = 0;
+          pl[m + o] = 0;
+          pl[2 * m + o] = 0;
+        }
+      }
     }
   }
 }
@@ -127,7 +198,7 @@ enum { RED_STATS = 0, RED_BNBWD = 1, RED_SUM = 2 };
 
 struct RedArgs {
   const float* a;       // STATS: y ; BNBWD: dz ; SUM: x
-  const float* z;       // BNBWD: z (relu mask), or NULL
+  const float* z;       // BNBWD: z (relu mask), or NULL: the mask is bn_value(y) > 0 (below)
   const float* y;       // BNBWD: y (pre-BN conv output)
   int64_t rows;
   int C;
@@ -135,7 +206,21 @@ struct RedArgs {
   int64_t rows_per_split;
   int relu;
   double* ws;
+  const float* mean;    // BNBWD with z == NULL: the forward's BN terms (gamma / beta NULL-able)
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
 };
+
+// The train-mode BN output before ReLU, one rounding order everywhere it is formed: bn_act_kernel
+// writes relu(bn_value) and the backward of a residual-free BN + ReLU recomputes the mask
+// bn_value(y) > 0 from y instead of reading z (one fp32 tensor less per pass, bit-identical mask).
+__device__ __forceinline__ float bn_value(float v, float m, float s, float g, float b) {
+  return __builtin_fmaf((v - m) * s, g, b);
+}
+__device__ __forceinline__ float4 ld4_or(const float* p, int c, float dflt) {
+  return p != nullptr ? *reinterpret_cast<const float4*>(p + c) : make_float4(dflt, dflt, dflt, dflt);
+}
 
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) colred_kernel(const RedArgs r) {
@@ -148,6 +233,17 @@ __global__ void __launch_bounds__(kThreads) colred_kernel(const RedArgs r) {
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * r.rows_per_split;
   const int64_t r1 = (r0 + r.rows_per_split) < r.rows ? (r0 + r.rows_per_split) : r.rows;
   double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
+  // BNBWD without z: the thread's four channels' forward BN terms (mask = bn_value(y) > 0)
+  float bm[4] = {0, 0, 0, 0}, bs[4] = {0, 0, 0, 0}, bg[4] = {1, 1, 1, 1}, bb[4] = {0, 0, 0, 0};
+  const bool ymask = MODE == RED_BNBWD && r.relu && r.z == nullptr;
+  if (ymask) {
+    const float4 m4 = ld4_or(r.mean, c0, 0.f), s4 = ld4_or(r.invstd, c0, 0.f);
+    const float4 g4 = ld4_or(r.gamma, c0, 1.f), b4 = ld4_or(r.beta, c0, 0.f);
+    bm[0] = m4.x; bm[1] = m4.y; bm[2] = m4.z; bm[3] = m4.w;
+    bs[0] = s4.x; bs[1] = s4.y; bs[2] = s4.z; bs[3] = s4.w;
+    bg[0] = g4.x; bg[1] = g4.y; bg[2] = g4.z; bg[3] = g4.w;
+    bb[0] = b4.x; bb[1] = b4.y; bb[2] = b4.z; bb[3] = b4.w;
+  }
   // RB rows' loads go out before their (in-order) fp64 accumulation: the same sums, with that many
   // loads in flight per thread instead of one
   constexpr int RB = 4;
@@ -159,7 +255,7 @@ __global__ void __launch_bounds__(kThreads) colred_kernel(const RedArgs r) {
       const int64_t off = (row + u * rg) * r.C + c0;
       av[u] = *reinterpret_cast<const float4*>(r.a + off);
       if constexpr (MODE == RED_BNBWD) {
-        if (r.relu) zv[u] = *reinterpret_cast<const float4*>(r.z + off);
+        if (r.relu && !ymask) zv[u] = *reinterpret_cast<const float4*>(r.z + off);
         yv[u] = *reinterpret_cast<const float4*>(r.y + off);
       }
     }
@@ -173,13 +269,16 @@ __global__ void __launch_bounds__(kThreads) colred_kernel(const RedArgs r) {
           s2[j] += static_cast<double>(a[j]) * a[j];
         }
       } else if constexpr (MODE == RED_BNBWD) {
-        if (r.relu) {
+        const float y[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
+        if (ymask) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = bn_value(y[j], bm[j], bs[j], bg[j], bb[j]) > 0.f ? a[j] : 0.f;
+        } else if (r.relu) {
           a[0] = zv[u].x > 0.f ? a[0] : 0.f;
           a[1] = zv[u].y > 0.f ? a[1] : 0.f;
           a[2] = zv[u].z > 0.f ? a[2] : 0.f;
           a[3] = zv[u].w > 0.f ? a[3] : 0.f;
         }
-        const float y[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           s1[j] += a[j];
@@ -202,15 +301,18 @@ __global__ void __launch_bounds__(kThreads) colred_kernel(const RedArgs r) {
         s2[j] += static_cast<double>(a[j]) * a[j];
       }
     } else if constexpr (MODE == RED_BNBWD) {
-      if (r.relu) {
+      const float4 yv = *reinterpret_cast<const float4*>(r.y + off);
+      const float y[4] = {yv.x, yv.y, yv.z, yv.w};
+      if (ymask) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = bn_value(y[j], bm[j], bs[j], bg[j], bb[j]) > 0.f ? a[j] : 0.f;
+      } else if (r.relu) {
         const float4 zv = *reinterpret_cast<const float4*>(r.z + off);
         a[0] = zv.x > 0.f ? a[0] : 0.f;
         a[1] = zv.y > 0.f ? a[1] : 0.f;
         a[2] = zv.z > 0.f ? a[2] : 0.f;
         a[3] = zv.w > 0.f ? a[3] : 0.f;
       }
-      const float4 yv = *reinterpret_cast<const float4*>(r.y + off);
-      const float y[4] = {yv.x, yv.y, yv.z, yv.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         s1[j] += a[j];
@@ -333,12 +435,11 @@ bn_act_kernel(const float* __restrict__ y, const float* __restrict__ mean, const
     // per-channel terms as 16-B loads (c % 4 == 0)
     const float4 m4 = *reinterpret_cast<const float4*>(mean + c);
     const float4 s4 = *reinterpret_cast<const float4*>(invstd + c);
-    const float4 g4 = gamma != nullptr ? *reinterpret_cast<const float4*>(gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
-    const float4 b4 = beta != nullptr ? *reinterpret_cast<const float4*>(beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 g4 = ld4_or(gamma, c, 1.f), b4 = ld4_or(beta, c, 0.f);
     const float cm[4] = {m4.x, m4.y, m4.z, m4.w}, cs[4] = {s4.x, s4.y, s4.z, s4.w};
     const float cg[4] = {g4.x, g4.y, g4.z, g4.w}, cb[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = ((o[j] - cm[j]) * cs[j]) * cg[j] + cb[j];
+    for (int j = 0; j < 4; ++j) o[j] = bn_value(o[j], cm[j], cs[j], cg[j], cb[j]);
     if (res != nullptr) {
       const float4 rv = reinterpret_cast<const float4*>(res)[i];
       o[0] += rv.x; o[1] += rv.y; o[2] += rv.z; o[3] += rv.w;
@@ -376,21 +477,30 @@ bn_bwd_final_kernel(const double* __restrict__ ws, int G, int C, int64_t rows, c
 __global__ void __launch_bounds__(kThreads)
 bn_bwd_apply_kernel(const float* dz, const float* __restrict__ z, const float* __restrict__ y,
                     const float* __restrict__ mean, const float* __restrict__ coef, int relu, int64_t n4, int C,
-                    float* dy, float* dres, int dres_acc) {
+                    float* dy, float* dres, int dres_acc, const float* __restrict__ invstd,
+                    const float* __restrict__ gamma, const float* __restrict__ beta) {
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int c = static_cast<int>((i * 4) & (C - 1));
     const float4 gv = reinterpret_cast<const float4*>(dz)[i];
     float dr[4] = {gv.x, gv.y, gv.z, gv.w};
-    if (relu) {
+    const float4 yv = reinterpret_cast<const float4*>(y)[i];
+    const float yy[4] = {yv.x, yv.y, yv.z, yv.w};
+    if (relu && z == nullptr) {                        // mask recomputed: bn_value(y) > 0
+      const float4 m4 = *reinterpret_cast<const float4*>(mean + c);
+      const float4 s4 = *reinterpret_cast<const float4*>(invstd + c);
+      const float4 g4 = ld4_or(gamma, c, 1.f), b4 = ld4_or(beta, c, 0.f);
+      const float cm[4] = {m4.x, m4.y, m4.z, m4.w}, cs[4] = {s4.x, s4.y, s4.z, s4.w};
+      const float cg[4] = {g4.x, g4.y, g4.z, g4.w}, cb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dr[j] = bn_value(yy[j], cm[j], cs[j], cg[j], cb[j]) > 0.f ? dr[j] : 0.f;
+    } else if (relu) {
       const float4 zv = reinterpret_cast<const float4*>(z)[i];
       dr[0] = zv.x > 0.f ? dr[0] : 0.f;
       dr[1] = zv.y > 0.f ? dr[1] : 0.f;
       dr[2] = zv.z > 0.f ? dr[2] : 0.f;
       dr[3] = zv.w > 0.f ? dr[3] : 0.f;
     }
-    const float4 yv = reinterpret_cast<const float4*>(y)[i];
-    const float yy[4] = {yv.x, yv.y, yv.z, yv.w};
     // per-channel terms as 16-B loads (c % 4 == 0; coef's three rows are C floats each)
     const float4 a4 = *reinterpret_cast<const float4*>(coef + c);
     const float4 b4 = *reinterpret_cast<const float4*>(coef + C + c);
@@ -791,6 +901,33 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
 // kernel splits only x.  Same split3 (RNE) of the same values and the same MFMA order per
 // accumulator as wgrad_x6_big_kernel, so the partial sums are bit-identical to it.
 constexpr int kPreRows = kWT2;   // dyT rows padded to a multiple of the tile (zero rows)
+__device__ float4 g_wgrad_zero[4];   // zero-initialised: the B source outside the image
+
+// LDS byte address of a __shared__ object; one ds_read_b128 at LDS address base + OFF
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)p));
+}
+template <int OFF, typename V>
+__device__ __forceinline__ void ds_rd(V& dst, uint32_t base) {
+  static_assert(sizeof(V) == 16 && OFF >= 0 && OFF < 65536, "ds_read_b128 offset");
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(OFF));
+}
+// one 16-B-per-lane LDS-DMA (global_load_lds_dwordx4) to the wave-uniform LDS address `lds`
+// (M0 holds the LDS address; its previous value is restored, as M0 is reserved to the compiler)
+__device__ __forceinline__ void dma16(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds) : "memory");
+}
+__device__ __forceinline__ int pre_swz_a(int row) { return ((row >> 3) & 1) * 3; }          // 64-B bf16 rows
+__device__ __forceinline__ int pre_swz_b(int row) { return ((row >> 1) & 1) | (row & 4); }  // 128-B fp32 rows
+// transposed B write of row RR (0..15) of a thread's 16-row group: w[k] holds the lane address for
+// swizzle value k -> (0, 1, 4, 5)
+template <int RR>
+__device__ __forceinline__ void pre_wr(const uint32_t (&w)[4], float v) {
+  constexpr int k = ((RR >> 1) & 1) | (((RR >> 2) & 1) << 1);
+  asm volatile("ds_write_b32 %0, %1 offset:%2" :: "v"(w[k]), "v"(v), "i"(RR * 128) : "memory");
+}
 
 __global__ void __launch_bounds__(kThreads)
 wgrad_dy_split_kernel(const float* __restrict__ dy, int dys, int cout, int64_t M, int64_t Mp, int Cp,
@@ -820,9 +957,6 @@ wgrad_dy_split_kernel(const float* __restrict__ dy, int dys, int cout, int64_t M
     *reinterpret_cast<bf16x8*>(o + 2 * pstride) = h3;
   }
 }
-
-__device__ __forceinline__ int pre_swz_a(int row) { return ((row >> 3) & 1) * 3; }          // 64-B bf16 rows
-__device__ __forceinline__ int pre_swz_b(int row) { return ((row >> 1) & 1) | (row & 4); }  // 128-B fp32 rows
 
 struct WgradPreP {
   WgradP p;
@@ -856,23 +990,27 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
   const int kh = kval ? tap / p.ks : 0;
   const int kw = kval ? tap - kh * p.ks : 0;
 
-  // A DMA: 24 pieces of 1 KB per chunk, 6 per wave; piece gi = plane * 8 + 16-row block
+  // A DMA: 24 pieces of 1 KB per chunk, 6 per wave; piece gi = plane * 8 + 16-row block.  Sources
+  // as element offsets from the block's first row (< 2^31: 3 x 128 rows x Mp), not 64-bit pointers
+  // (six of those spilled to scratch, and the reload waited on every load in flight)
   const int64_t plane_stride = static_cast<int64_t>(q.Cp) * q.Mp;
-  const bf16_t* a_src[6];
+  const bf16_t* a_base = q.dyt + static_cast<int64_t>(co0) * q.Mp;
+  int32_t a_off[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const int gi = wave * 6 + i;
     const int pl = gi >> 3;
     const int r = (gi & 7) * 16 + (lane >> 2);
     const int c = (lane & 3) ^ pre_swz_a(r);
-    a_src[i] = q.dyt + pl * plane_stride + static_cast<int64_t>(co0 + r) * q.Mp + 8 * c;
+    a_off[i] = static_cast<int32_t>(pl * plane_stride + static_cast<int64_t>(r) * q.Mp + 8 * c);
   }
+  // as inline asm: hipcc models the LDS-DMA builtin's address registers as pending until vmcnt(0)
+  // and drained the B loads in flight the first time it reused one
+  const uint32_t a_dst = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(lds_addr(&Ab[0][wave * 6 * 1024]))));
   auto dma_a = [&](int buf, int64_t m) {
+    const bf16_t* src = a_base + m;
 #pragma unroll
-    for (int i = 0; i < 6; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) const void*)(a_src[i] + m),
-                                       (__attribute__((address_space(3))) void*)(&Ab[buf][(wave * 6 + i) * 1024]),
-                                       16, 0, 0);
+    for (int i = 0; i < 6; ++i) dma16(src + a_off[i], a_dst + buf * static_cast<uint32_t>(sizeof(Ab[0])) + i * 1024);
   };
 
   int64_t m_cur = m_begin + lm;
@@ -884,6 +1022,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
     p_oh = qq / p.wo;
     p_ow = qq - p_oh * p.wo;
   }
+  // exactly four 16-B loads per call (the zero page outside the image / past the split), so that
+  // the chunk-end wait below can leave them in flight with a fixed vmcnt
   auto load = [&](float4 (&rb)[4]) {
     const int64_t m = m_cur;
     const int nn = p_n, oh = p_oh, ow = p_ow;
@@ -896,27 +1036,27 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
         ++p_n;
       }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) rb[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m >= m_end || !kval) return;
+    const float* xr = reinterpret_cast<const float*>(g_wgrad_zero);
     const int ih = oh * p.stride - p.pad + kh * p.dil;
     const int iw = ow * p.stride - p.pad + kw * p.dil;
-    if (static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) && static_cast<unsigned>(iw) < static_cast<unsigned>(p.w)) {
-      const float* xr = p.x + ((static_cast<int64_t>(nn) * p.h + ih) * p.w + iw) * p.cs + ci;
+    if (m < m_end && kval && static_cast<unsigned>(ih) < static_cast<unsigned>(p.h) &&
+        static_cast<unsigned>(iw) < static_cast<unsigned>(p.w))
+      xr = p.x + ((static_cast<int64_t>(nn) * p.h + ih) * p.w + iw) * p.cs + ci;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rb[j] = *reinterpret_cast<const float4*>(xr + 4 * j);
-    }
+    for (int j = 0; j < 4; ++j) rb[j] = *reinterpret_cast<const float4*>(xr + 4 * j);
   };
+  // transposed B writes as inline asm as well (a C++ LDS store made hipcc wait vmcnt(0) for the
+  // DMA in flight); row 16 lv + 4 j + e: its swizzle depends on 4 j + e only
+  const uint32_t bs_w = lds_addr(&Bs[0][0]) + static_cast<uint32_t>(16 * lv * 128 + 4 * (lm & 3));
   auto store = [&](int buf, const float4 (&rb)[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float bv[4] = {rb[j].x, rb[j].y, rb[j].z, rb[j].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = 16 * lv + 4 * j + e;
-        Bs[buf][row * 32 + 4 * ((lm >> 2) ^ pre_swz_b(row)) + (lm & 3)] = bv[e];
-      }
-    }
+    const uint32_t base = bs_w + buf * static_cast<uint32_t>(sizeof(Bs[0]));
+    // one lane address per swizzle value (0, 1, 4, 5); the row is the instruction's offset
+    const uint32_t w[4] = {base + 16u * ((lm >> 2) ^ 0), base + 16u * ((lm >> 2) ^ 1), base + 16u * ((lm >> 2) ^ 4),
+                           base + 16u * ((lm >> 2) ^ 5)};
+    pre_wr<0>(w, rb[0].x); pre_wr<1>(w, rb[0].y); pre_wr<2>(w, rb[0].z); pre_wr<3>(w, rb[0].w);
+    pre_wr<4>(w, rb[1].x); pre_wr<5>(w, rb[1].y); pre_wr<6>(w, rb[1].z); pre_wr<7>(w, rb[1].w);
+    pre_wr<8>(w, rb[2].x); pre_wr<9>(w, rb[2].y); pre_wr<10>(w, rb[2].z); pre_wr<11>(w, rb[2].w);
+    pre_wr<12>(w, rb[3].x); pre_wr<13>(w, rb[3].y); pre_wr<14>(w, rb[3].z); pre_wr<15>(w, rb[3].w);
   };
 
   f32x4 acc[4][4];
@@ -926,23 +1066,50 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15;
   const int fq = lane >> 4;
+  // Fragment reads as inline-asm ds_read_b128 with hand-counted lgkmcnt waits: hipcc cannot tell
+  // that the LDS-DMA in flight targets the other buffer, and put a vmcnt(0) before the first C++
+  // read of the chunk (draining the B loads issued for two chunks ahead).  The swizzles depend on
+  // row bits the fragment offsets (16 rows apart) do not change, so one lane address per operand.
+  const uint32_t ab_lds = lds_addr(&Ab[0][0]), bs_lds = lds_addr(&Bs[0][0]);
+  uint32_t b_lane[2], a_lane;
+  {
+    const int rb = wcn * 64 + fr;
+    b_lane[0] = bs_lds + static_cast<uint32_t>(rb * 128 + 16 * ((2 * fq) ^ pre_swz_b(rb)));
+    b_lane[1] = bs_lds + static_cast<uint32_t>(rb * 128 + 16 * ((2 * fq + 1) ^ pre_swz_b(rb)));
+    const int ra = wr * 64 + fr;
+    a_lane = ab_lds + static_cast<uint32_t>(ra * 64 + 16 * (fq ^ pre_swz_a(ra)));
+  }
+  static_assert(sizeof(Bs[0]) == kWT2 * 128 && sizeof(Ab[0]) == 3 * kWT2 * 64, "LDS buffer strides");
   auto compute = [&](int buf) {
+    const uint32_t vb0 = b_lane[0] + buf * static_cast<uint32_t>(sizeof(Bs[0]));
+    const uint32_t vb1 = b_lane[1] + buf * static_cast<uint32_t>(sizeof(Bs[0]));
+    const uint32_t va = a_lane + buf * static_cast<uint32_t>(sizeof(Ab[0]));
+    float4 blo[4], bhi[4];
+    ds_rd<0>(blo[0], vb0); ds_rd<0>(bhi[0], vb1);
+    ds_rd<2048>(blo[1], vb0); ds_rd<2048>(bhi[1], vb1);
+    ds_rd<4096>(blo[2], vb0); ds_rd<4096>(bhi[2], vb1);
+    ds_rd<6144>(blo[3], vb0); ds_rd<6144>(bhi[3], vb1);
+    bf16x8 a[3];
+    ds_rd<0>(a[0], va); ds_rd<kWT2 * 64>(a[1], va); ds_rd<2 * kWT2 * 64>(a[2], va);
+    // the reads are asm: their results are valid only after the counted wait, and a
+    // sched_barrier after each wait keeps the scheduler from hoisting their uses above it
+    asm volatile("s_waitcnt lgkmcnt(3)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
     bf16x8 b[4][3];
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const int r = wcn * 64 + f * 16 + fr;
-      const float* br = &Bs[buf][r * 32];
-      split3(*reinterpret_cast<const float4*>(br + 4 * ((2 * fq) ^ pre_swz_b(r))),
-             *reinterpret_cast<const float4*>(br + 4 * ((2 * fq + 1) ^ pre_swz_b(r))), b[f][0], b[f][1], b[f][2]);
-    }
+    for (int f = 0; f < 4; ++f) split3(blo[f], bhi[f], b[f][0], b[f][1], b[f][2]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int fi = 0; fi < 4; ++fi) {
-      const int r = wr * 64 + fi * 16 + fr;
-      const char* ar = &Ab[buf][r * 64 + ((fq ^ pre_swz_a(r)) * 16)];
-      bf16x8 a[3];
-      a[0] = *reinterpret_cast<const bf16x8*>(ar);
-      a[1] = *reinterpret_cast<const bf16x8*>(ar + kWT2 * 64);
-      a[2] = *reinterpret_cast<const bf16x8*>(ar + 2 * kWT2 * 64);
+      bf16x8 an[3];
+      // the next fragment's three planes (rows 16 apart: +1 KB), read under this one's MFMAs
+      switch (fi) {
+        case 0: ds_rd<1024>(an[0], va); ds_rd<1024 + kWT2 * 64>(an[1], va); ds_rd<1024 + 2 * kWT2 * 64>(an[2], va); break;
+        case 1: ds_rd<2048>(an[0], va); ds_rd<2048 + kWT2 * 64>(an[1], va); ds_rd<2048 + 2 * kWT2 * 64>(an[2], va); break;
+        case 2: ds_rd<3072>(an[0], va); ds_rd<3072 + kWT2 * 64>(an[1], va); ds_rd<3072 + 2 * kWT2 * 64>(an[2], va); break;
+        default: break;
+      }
 #pragma unroll
       for (int fj = 0; fj < 4; ++fj) {
         f32x4& c = acc[fi][fj];
@@ -953,32 +1120,43 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][1], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[fj][0], c, 0, 0, 0);
       }
+      if (fi < 3) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        a[0] = an[0];
+        a[1] = an[1];
+        a[2] = an[2];
+      }
     }
   };
 
-  // chunk c: A by DMA into buffer c & 1 (issued one chunk ahead), B through registers as in
-  // wgrad_x6_big_kernel (two register sets); every chunk ends with vmcnt(0) + barrier
-  float4 r0[4], r1[4];
+  // Chunk c computes from buffers c & 1.  At the start of its phase the B registers of chunk c + 1
+  // (loaded during the previous phase) are written to the other buffer, chunk c + 1's A DMA goes to
+  // it as well, then chunk c + 2's B loads are issued into the same registers -- so hipcc's wait for
+  // those registers (it cannot count LDS-DMA and waits vmcnt(0)) drains nothing else.  The phase
+  // ends with vmcnt(4) (the DMA landed, the four B loads stay in flight across the barrier) +
+  // lgkmcnt(0) + s_barrier.  Compiler barriers keep the DMA ahead of the B loads in issue order.
+  float4 rb[4];
   dma_a(0, m_begin);
-  load(r0);
-  store(0, r0);
-  load(r0);                                        // chunk 1
+  load(rb);                                        // chunk 0
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int64_t mc = m_begin; mc < m_end; mc += 2 * kWM) {
-    if (mc + kWM < m_end) dma_a(1, mc + kWM);
-    load(r1);                                      // chunk c + 2
-    compute(0);
-    if (mc + kWM < m_end) store(1, r0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (mc + kWM >= m_end) break;
-    if (mc + 2 * kWM < m_end) dma_a(0, mc + 2 * kWM);
-    load(r0);                                      // chunk c + 3
-    compute(1);
-    if (mc + 2 * kWM < m_end) store(0, r1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  store(0, rb);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  load(rb);                                        // chunk 1
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  int cur = 0;
+  for (int64_t mc = m_begin; mc < m_end; mc += kWM, cur ^= 1) {
+    store(cur ^ 1, rb);                            // chunk c + 1 (zeros past the split, never read)
+    if (mc + kWM < m_end) dma_a(cur ^ 1, mc + kWM);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    load(rb);                                      // chunk c + 2 (the zero page past the split)
+    __builtin_amdgcn_sched_barrier(0);
+    compute(cur);
+    asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
   float* out = p.ws + static_cast<int64_t>(blockIdx.z) * p.cout * p.K;
 #pragma unroll
@@ -1014,6 +1192,44 @@ wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin,
     const int64_t o = (static_cast<int64_t>(co) * cin + ci) * ks * ks + tap;   // tap = kh * ks + kw
     dw[o] = acc ? dw[o] + s : s;
   }
+}
+
+// Few outputs over many splits (the stem's 16 x 392 partials over 432 splits): one thread per
+// output walked its splits as a chain of dependent loads on 18 workgroups (125 us).  Here 8
+// threads share an output, each sums a contiguous eighth of the splits (8 loads in flight), and
+// the eighths are added in order: a fixed order, so dw stays bit-reproducible.
+constexpr int kRedOut = 32;
+constexpr int kRedGrp = kThreads / kRedOut;
+
+__global__ void __launch_bounds__(kThreads)
+wgrad_reduce_grouped_kernel(const float* __restrict__ ws, int splits, int cout, int cin, int cs, int ks, int K,
+                            float* __restrict__ dw, int acc) {
+  __shared__ float part[kRedGrp][kRedOut];
+  const int t = threadIdx.x;
+  const int oi = t % kRedOut, g = t / kRedOut;
+  const int64_t total = static_cast<int64_t>(cout) * K;
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kRedOut + oi;
+  const int z0 = static_cast<int>(static_cast<int64_t>(splits) * g / kRedGrp);
+  const int z1 = static_cast<int>(static_cast<int64_t>(splits) * (g + 1) / kRedGrp);
+  float s = 0.f;
+  if (i < total) {
+    const float* p = ws + i;
+#pragma unroll 8
+    for (int z = z0; z < z1; ++z) s += p[static_cast<int64_t>(z) * total];
+  }
+  part[g][oi] = s;
+  __syncthreads();
+  if (g != 0 || i >= total) return;
+  const int co = static_cast<int>(i / K);
+  const int k = static_cast<int>(i - static_cast<int64_t>(co) * K);
+  const int tap = k / cs;
+  const int ci = k - tap * cs;
+  if (ci >= cin) return;
+  float v = part[0][oi];
+#pragma unroll
+  for (int j = 1; j < kRedGrp; ++j) v += part[j][oi];
+  const int64_t o = (static_cast<int64_t>(co) * cin + ci) * ks * ks + tap;
+  dw[o] = acc ? dw[o] + v : v;
 }
 
 // The pixel range is split so that the launch fills the chip: at least two rounds of the resident
@@ -1347,13 +1563,15 @@ extern "C" int drnmi_pack_conv_weight(const float* w, int32_t cout, int32_t cin,
 }
 
 extern "C" int drnmi_pack_table_check(const int64_t* t, int32_t n, int64_t* total_out) {
-  if (t == nullptr || n <= 0) return DRNMI_EINVAL;
+  if (t == nullptr || n <= 0 || n > kPackMaxEntries) return DRNMI_EINVAL;
   int64_t total = 0;
   for (int e = 0; e < n; ++e) {
     const int64_t* q = t + static_cast<int64_t>(e) * DRNMI_PACK_ENTRY_WORDS;
     const int64_t cout = q[3], cin = q[4], ks = q[5], kst = q[6], rows = q[7], kp = q[8], mode = q[9];
-    if (q[0] == 0 || q[1] == 0 || cout <= 0 || cin <= 0 || ks <= 0 || kst <= 0 || rows <= 0 || kp <= 0) return DRNMI_EINVAL;
+    if (q[0] == 0 || q[1] == 0 || cout <= 0 || cin <= 0 || ks <= 0 || ks > 7 || kst <= 0 || rows <= 0 || kp <= 0)
+      return DRNMI_EINVAL;
     if ((mode != 0 && mode != 1) || kp < ks * ks * kst || kp >= (int64_t(1) << 31) || rows >= (int64_t(1) << 31)) return DRNMI_EINVAL;
+    if (kst % 4 != 0 || kp % 4 != 0 || ((q[1] | q[2]) & 15) != 0) return DRNMI_EINVAL;   // 4-column stores
     if (mode == 0 && (rows < cout || kst < cin)) return DRNMI_EINVAL;
     if (mode == 1 && (rows < cin || kst < cout)) return DRNMI_EINVAL;
     if (q[10] != total || q[11] != 0) return DRNMI_EINVAL;
@@ -1364,9 +1582,9 @@ extern "C" int drnmi_pack_table_check(const int64_t* t, int32_t n, int64_t* tota
 }
 
 extern "C" int drnmi_pack_conv_weights_batched(const int64_t* table, int32_t n, int64_t total, void* stream) {
-  if (table == nullptr || n <= 0 || total <= 0) return DRNMI_EINVAL;
-  hipLaunchKernelGGL(pack_batched_kernel, dim3(grid_of(total)), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
-                     table, n, total);
+  if (table == nullptr || n <= 0 || n > kPackMaxEntries || total <= 0) return DRNMI_EINVAL;
+  // grid-stride over the tiles (their count is known on the device only): 8 workgroups per CU
+  hipLaunchKernelGGL(pack_batched_kernel, dim3(2048), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream), table, n);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -1412,14 +1630,10 @@ extern "C" int drnmi_bn_act_f32(const float* y, const float* mean, const float* 
   return static_cast<int>(hipGetLastError());
 }
 
-extern "C" int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float* y, const float* mean,
-                                    const float* invstd, const float* gamma, int32_t relu, int64_t rows, int32_t C,
-                                    float* dy, float* dres, int32_t dres_accumulate, float* dgamma, float* dbeta,
-                                    int32_t grad_accumulate, void* ws, void* stream) {
-  if (dz == nullptr || y == nullptr || mean == nullptr || invstd == nullptr || dy == nullptr || ws == nullptr ||
-      rows <= 0 || !pow2_ge4(C) || (relu && z == nullptr))
-    return DRNMI_EINVAL;
-  if (reinterpret_cast<uintptr_t>(mean) & 15) return DRNMI_EINVAL;   // read as 16-B pieces
+static int bn_bwd_launch(const float* dz, const float* z, const float* y, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, int32_t relu, int64_t rows, int32_t C, float* dy,
+                         float* dres, int32_t dres_accumulate, float* dgamma, float* dbeta, int32_t grad_accumulate,
+                         void* ws, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   RedArgs r{};
   r.a = dz;
@@ -1429,6 +1643,10 @@ extern "C" int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float
   r.C = C;
   r.relu = relu;
   r.ws = reinterpret_cast<double*>(ws);
+  r.mean = mean;
+  r.invstd = invstd;
+  r.gamma = gamma;
+  r.beta = beta;
   hipError_t e = launch_colred<RED_BNBWD>(r, s);
   if (e != hipSuccess) return static_cast<int>(e);
   float* coef = reinterpret_cast<float*>(r.ws + static_cast<int64_t>(2) * r.G * C);
@@ -1438,8 +1656,33 @@ extern "C" int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float
   if (e != hipSuccess) return static_cast<int>(e);
   const int64_t n4 = rows * C / 4;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_of(n4)), dim3(kThreads), 0, s, dz, z, y, mean, coef, relu, n4,
-                     C, dy, dres, dres_accumulate);
+                     C, dy, dres, dres_accumulate, invstd, gamma, beta);
   return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_bn_act_bwd_f32(const float* dz, const float* z, const float* y, const float* mean,
+                                    const float* invstd, const float* gamma, int32_t relu, int64_t rows, int32_t C,
+                                    float* dy, float* dres, int32_t dres_accumulate, float* dgamma, float* dbeta,
+                                    int32_t grad_accumulate, void* ws, void* stream) {
+  if (dz == nullptr || y == nullptr || mean == nullptr || invstd == nullptr || dy == nullptr || ws == nullptr ||
+      rows <= 0 || !pow2_ge4(C) || (relu && z == nullptr))
+    return DRNMI_EINVAL;
+  if (reinterpret_cast<uintptr_t>(mean) & 15) return DRNMI_EINVAL;   // read as 16-B pieces
+  return bn_bwd_launch(dz, z, y, mean, invstd, gamma, nullptr, relu, rows, C, dy, dres, dres_accumulate, dgamma, dbeta,
+                       grad_accumulate, ws, stream);
+}
+
+extern "C" int drnmi_bn_relu_bwd_y_f32(const float* dz, const float* y, const float* mean, const float* invstd,
+                                       const float* gamma, const float* beta, int64_t rows, int32_t C, float* dy,
+                                       float* dgamma, float* dbeta, int32_t grad_accumulate, void* ws, void* stream) {
+  if (dz == nullptr || y == nullptr || mean == nullptr || invstd == nullptr || dy == nullptr || ws == nullptr ||
+      rows <= 0 || !pow2_ge4(C))
+    return DRNMI_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(mean) | reinterpret_cast<uintptr_t>(invstd) | reinterpret_cast<uintptr_t>(gamma) |
+       reinterpret_cast<uintptr_t>(beta)) & 15)
+    return DRNMI_EINVAL;
+  return bn_bwd_launch(dz, nullptr, y, mean, invstd, gamma, beta, 1, rows, C, dy, nullptr, 0, dgamma, dbeta,
+                       grad_accumulate, ws, stream);
 }
 
 extern "C" int drnmi_channel_sum_f32(const float* x, int64_t rows, int32_t C, int32_t cvalid, float* out,
@@ -1569,8 +1812,14 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
   const int64_t total = static_cast<int64_t>(a->cout) * p.K;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_of(total)), dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin,
-                     a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
+  // the grouped form where one thread per output would leave the chip mostly idle on a long chain
+  if (splits >= 4 * kRedGrp && total <= 2048 * kThreads)
+    hipLaunchKernelGGL(wgrad_reduce_grouped_kernel, dim3(static_cast<unsigned>((total + kRedOut - 1) / kRedOut)),
+                       dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin, a->cin_stride, a->ks, p.K, a->dw,
+                       a->accumulate);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_of(total)), dim3(kThreads), 0, s, p.ws, splits, a->cout, a->cin,
+                       a->cin_stride, a->ks, p.K, a->dw, a->accumulate);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -98,6 +98,8 @@ SIGNATURES = {
     "drnmi_bn_act_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _I32, _I64, _I32, _VP, _VP]),
     "drnmi_bn_act_bwd_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _I32, _I64, _I32, _VP, _VP, _I32,
                                             _VP, _VP, _I32, _VP, _VP]),
+    "drnmi_bn_relu_bwd_y_f32": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, _I64, _I32, _VP, _VP, _VP, _I32,
+                                               _VP, _VP]),
     "drnmi_channel_sum_f32": (ctypes.c_int, [_VP, _I64, _I32, _I32, _VP, _I32, _VP, _VP]),
     "drnmi_conv_wgrad_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
     "drnmi_conv_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(ConvArgs)]),

@@ -406,11 +406,19 @@ class TrainRunner:
                         dres_acc = 1
                 gw, gb = bn.weight, bn.bias
                 ws = self._ws("_red_ws", lib.drnmi_reduce_workspace_bytes(rows, dys), dev)
-                _lib.check(lib.drnmi_bn_act_bwd_f32(
-                    _vp(dz), _vp(z), _vp(y), _vp(mean), _vp(invstd), _vp(gw.detach()), 1 if nd.relu else 0, rows,
-                    dys, _vp(dz), _vp(dres), dres_acc,
-                    _vp(gw.grad) if gw.requires_grad else None, _vp(gb.grad) if gb.requires_grad else None,
-                    1 if (gw.requires_grad and acc[id(gw)]) else 0, _vp(ws), sp), f"bn_bwd {nd.name}")
+                gacc = 1 if (gw.requires_grad and acc[id(gw)]) else 0
+                if nd.relu and not nd.res:
+                    # residual-free BN + ReLU: the mask is recomputed from y (z is not read)
+                    _lib.check(lib.drnmi_bn_relu_bwd_y_f32(
+                        _vp(dz), _vp(y), _vp(mean), _vp(invstd), _vp(gw.detach()), _vp(gb.detach()), rows, dys,
+                        _vp(dz), _vp(gw.grad) if gw.requires_grad else None,
+                        _vp(gb.grad) if gb.requires_grad else None, gacc, _vp(ws), sp), f"bn_bwd {nd.name}")
+                else:
+                    _lib.check(lib.drnmi_bn_act_bwd_f32(
+                        _vp(dz), _vp(z), _vp(y), _vp(mean), _vp(invstd), _vp(gw.detach()), 1 if nd.relu else 0,
+                        rows, dys, _vp(dz), _vp(dres), dres_acc,
+                        _vp(gw.grad) if gw.requires_grad else None, _vp(gb.grad) if gb.requires_grad else None,
+                        gacc, _vp(ws), sp), f"bn_bwd {nd.name}")
                 if gw.requires_grad and gb.requires_grad and acc[id(gw)] != acc[id(gb)]:
                     raise RuntimeError("BN weight/bias grads must be both set or both None")
                 done += [q for q in (gw, gb) if q.requires_grad]
