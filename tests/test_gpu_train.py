@@ -220,11 +220,16 @@ def _wgrad(dy_nhwc, x_nhwc, cin, cout, ks, stride, pad, dil, ho, wo, accumulate=
     (256, 256, 512, 512, 3, 1, 4, 4, 16, 16),
     (96, 128, 200, 256, 3, 1, 1, 1, 13, 17),
     (256, 256, 256, 256, 3, 1, 2, 2, 48, 40),
+    (3, 8, 16, 16, 7, 2, 3, 1, 30, 64),      # wo % 32 == 0: the direct small-cout fp32x kernel
+    (16, 16, 16, 16, 3, 1, 1, 1, 9, 64),
+    (16, 16, 32, 32, 3, 2, 1, 1, 21, 64),
+    (32, 32, 19, 32, 1, 1, 0, 1, 5, 96),
 ])
 @pytest.mark.parametrize("x6", [False, True])
 def test_wgrad_kernel_matches_torch(cin, cs, cout, dys, ks, stride, pad, dil, h, w, x6):
-    """fp32 wgrad and the fp32x split-bf16 one (drnmi_conv_wgrad_f32x3: the 64 x 64 tile, and the
-    128 x 128 tile where cout and K >= 128, ragged cout / pixel counts included) vs torch autograd."""
+    """fp32 wgrad and the fp32x split-bf16 one (drnmi_conv_wgrad_f32x3: the 64 x 64 tile, the
+    128 x 128 tile where cout and K >= 128, the direct small-cout kernel where cout <= 32 and
+    wo % 32 == 0; ragged cout / pixel counts included) vs torch autograd."""
     torch.manual_seed(cin + cout)
     n = 2
     x = torch.randn(n, cin, h, w)

@@ -1173,6 +1173,126 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
     }
 }
 
+// ---- fp32x weight gradient of the small-cout convs (cout <= 32: stem, layer1, layer2) ----------
+// The 64 x 64 tile left 3/4 of its rows idle at cout 16, and the stem's 8-channel input stride left
+// 5/8 of its k columns zero (cin 3): 474 us for 20 GFLOP of the fine-tune step.  Here the MFMA
+// operands come straight from global memory into registers -- no LDS, no barriers: lane (fr, fq)
+// loads dy[m][16 fm + fr] and x[pix(m, tap)][ci] of its 8 pixels m = m0 + 8 fq + j, as the
+// 16x16x32 bf16 A / B layouts ask -- and the k columns are the dense (tap, ci < cin) pairs only
+// (147 at the stem instead of 392).  Each wave owns FN 16-column fragments and a contiguous range of
+// 32-pixel chunks (one output row segment each: wo % 32 == 0) and writes its own partial sums,
+// reduced in split order by wgrad_reduce*_kernel; same split3 and six-product order per
+// accumulator as wgrad_kernel<true>.
+constexpr int kDirFN = 4;
+static bool wgrad_direct_ok(const drnmi_wgrad_args& a) {
+  return a.cout <= 32 && a.wo % 32 == 0 && a.ks * a.ks * a.cin <= 4096;
+}
+static int wgrad_direct_tiles(const drnmi_wgrad_args& a) {
+  return (a.ks * a.ks * a.cin + 16 * kDirFN - 1) / (16 * kDirFN);
+}
+// wave splits: ~2048 waves in all (8 per CU), whole workgroups of 4, <= one chunk per wave
+static int wgrad_direct_splits(const drnmi_wgrad_args& a) {
+  const int64_t chunks = static_cast<int64_t>(a.n) * a.ho * a.wo / 32;
+  int64_t s = 2048 / wgrad_direct_tiles(a);
+  if (s > chunks) s = chunks;
+  s = (s + 3) / 4 * 4;
+  return static_cast<int>(s < 4 ? 4 : s);
+}
+
+template <int FM>
+__global__ void __launch_bounds__(kThreads) wgrad_x6_direct_kernel(const WgradP p, int cin) {
+  const int lane = threadIdx.x & 63;
+  const int z = blockIdx.y * 4 + (threadIdx.x >> 6);        // this wave's split
+  const int nz = gridDim.y * 4;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int hw = p.ho * p.wo;
+  const int chunks = static_cast<int>(p.M / 32);
+  const int c_begin = static_cast<int>(static_cast<int64_t>(chunks) * z / nz);
+  const int c_end = static_cast<int>(static_cast<int64_t>(chunks) * (z + 1) / nz);
+  const int kdense = p.ks * p.ks * cin;
+  // the lane's B column of each fragment: dense column kv -> (tap, ci) -> tap offsets
+  int b_dh[kDirFN], b_dw[kDirFN], b_ci[kDirFN];
+  bool b_ok[kDirFN];
+#pragma unroll
+  for (int f = 0; f < kDirFN; ++f) {
+    const int kv = (blockIdx.x * kDirFN + f) * 16 + fr;
+    b_ok[f] = kv < kdense;
+    const int tap = b_ok[f] ? kv / cin : 0;
+    b_ci[f] = b_ok[f] ? kv - tap * cin : 0;
+    const int kh = tap / p.ks;
+    b_dh[f] = kh * p.dil - p.pad;
+    b_dw[f] = (tap - kh * p.ks) * p.dil - p.pad;
+  }
+  f32x4 acc[FM][kDirFN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < kDirFN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = c_begin; c < c_end; ++c) {
+    const int m0 = c * 32;
+    const int n = m0 / hw;
+    const int q = m0 - n * hw;
+    const int oh = q / p.wo;
+    const int ow = q - oh * p.wo + 8 * fq;                 // the lane's first pixel (same row)
+    const int64_t mrow = static_cast<int64_t>(m0 + 8 * fq) * p.dys;
+    float av[FM][8], bv[kDirFN][8];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      const int co = 16 * fm + fr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) av[fm][j] = co < p.cout ? p.dy[mrow + static_cast<int64_t>(j) * p.dys + co] : 0.f;
+    }
+#pragma unroll
+    for (int f = 0; f < kDirFN; ++f) {
+      const int ih = oh * p.stride + b_dh[f];
+      const bool row_ok = b_ok[f] && static_cast<unsigned>(ih) < static_cast<unsigned>(p.h);
+      const float* xr = p.x + (static_cast<int64_t>(n) * p.h + (row_ok ? ih : 0)) * p.w * p.cs + b_ci[f];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int iw = (ow + j) * p.stride + b_dw[f];
+        bv[f][j] = row_ok && static_cast<unsigned>(iw) < static_cast<unsigned>(p.w) ? xr[static_cast<int64_t>(iw) * p.cs] : 0.f;
+      }
+    }
+    bf16x8 b[kDirFN][3];
+#pragma unroll
+    for (int f = 0; f < kDirFN; ++f)
+      split3(make_float4(bv[f][0], bv[f][1], bv[f][2], bv[f][3]), make_float4(bv[f][4], bv[f][5], bv[f][6], bv[f][7]),
+             b[f][0], b[f][1], b[f][2]);
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+      bf16x8 a[3];
+      split3(make_float4(av[fm][0], av[fm][1], av[fm][2], av[fm][3]),
+             make_float4(av[fm][4], av[fm][5], av[fm][6], av[fm][7]), a[0], a[1], a[2]);
+#pragma unroll
+      for (int f = 0; f < kDirFN; ++f) {
+        f32x4& cc = acc[fm][f];
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[f][0], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[f][1], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[f][2], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[f][0], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[f][1], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[f][0], cc, 0, 0, 0);
+      }
+    }
+  }
+  // C[row = 16 fm + 4 fq + r][col = 16 f + fr] -> ws[z][co][tap * cs + ci] (the reduce skips ci >= cin)
+  float* out = p.ws + static_cast<int64_t>(z) * p.cout * p.K;
+#pragma unroll
+  for (int f = 0; f < kDirFN; ++f) {
+    if (!b_ok[f]) continue;
+    const int kv = (blockIdx.x * kDirFN + f) * 16 + fr;
+    const int tap = kv / cin;
+    const int k = tap * p.cs + (kv - tap * cin);
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 16 * fm + 4 * fq + r;
+        if (co < p.cout) out[static_cast<int64_t>(co) * p.K + k] = acc[fm][f][r];
+      }
+  }
+}
+
 // dw[co][ci][kh][kw] (+)= sum_z ws[z][co][(kh*ks + kw)*cs + ci]
 __global__ void __launch_bounds__(kThreads)
 wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin, int cs, int ks, int K,
@@ -1755,6 +1875,7 @@ extern "C" int64_t drnmi_conv_wgrad_workspace_bytes(const drnmi_wgrad_args* a) {
     if (s2 > splits) splits = s2;
     pre = wgrad_pre_bytes(*a);
   }
+  if (wgrad_direct_ok(*a) && wgrad_direct_splits(*a) > splits) splits = wgrad_direct_splits(*a);
   return wgrad_partials_bytes(*a, splits) + pre;
 }
 
@@ -1783,7 +1904,12 @@ static int wgrad_launch(const drnmi_wgrad_args* a, bool x6, void* stream) {
   int splits;
   wgrad_plan(*a, big, &splits, &p.pix_per_split);
   const dim3 grid((p.K + kWT - 1) / kWT, (a->cout + kWT - 1) / kWT, splits);
-  if (big && wgrad_pre_ok(*a)) {
+  if (x6 && !big && wgrad_direct_ok(*a)) {
+    splits = wgrad_direct_splits(*a);
+    const dim3 gd(static_cast<unsigned>(wgrad_direct_tiles(*a)), static_cast<unsigned>(splits / 4));
+    if (a->cout <= 16) hipLaunchKernelGGL(wgrad_x6_direct_kernel<1>, gd, dim3(kThreads), 0, s, p, a->cin);
+    else hipLaunchKernelGGL(wgrad_x6_direct_kernel<2>, gd, dim3(kThreads), 0, s, p, a->cin);
+  } else if (big && wgrad_pre_ok(*a)) {
     WgradPreP q{};
     q.p = p;
     q.Mp = (p.M + kWM - 1) / kWM * kWM;
