@@ -105,11 +105,12 @@ typedef struct drnmi_conv_args {
    *     DRNMI_ENOTSUP.                                                                       */
   const void* x2;
   int32_t cin2, h2, w2, stride2;
-  /* Optional fp32 scratch (16-B aligned) for a split-K launch of the F32X3 kernel (conv_x6) on
-   * grids that leave CUs idle: the K range is split over gridDim.y workgroups per tile, their
-   * partial sums land here and a second kernel adds them in split order and applies the
-   * epilogue.  Size: drnmi_conv_workspace_bytes (0 = this launch would not split).  ws = NULL
-   * never splits (the inference engine's launches); other dtypes ignore it. */
+  /* Optional fp32 scratch (16-B aligned) of the F32X3 kernel (conv_x6): a launch given one takes
+   * the training plan -- a tile variant and split-K count chosen for grids that leave CUs idle
+   * (the K range split over gridDim.y workgroups per tile, their partial sums land here and a
+   * second kernel adds them in split order and applies the epilogue).  Size:
+   * drnmi_conv_workspace_bytes (0 = the plan is the inference one: pass NULL).  ws = NULL keeps
+   * the inference plan (the inference engine's launches); other dtypes ignore it. */
   void* ws;
   int64_t ws_bytes;
 } drnmi_conv_args;
@@ -134,10 +135,11 @@ enum drnmi_algo { DRNMI_ALGO_IGEMM = 0, DRNMI_ALGO_PATCH = 1 };
 
 int drnmi_conv2d_bn_act(const drnmi_conv_args* args, void* stream);
 
-/* Bytes of args->ws a split-K launch of these arguments needs (0: it would not split; -1: NULL).
- * Only DRNMI_F32X3 implicit-GEMM launches split (drnmi/train.py passes it for the fp32x
- * fine-tune); the split count depends on the geometry alone, so a size queried once per layer
- * holds for every step. */
+/* Bytes of args->ws the training plan of these arguments needs (0: the inference plan; 256: a
+ * different tile variant, no split; else S x M x cout x 4 for S split-K partitions; -1: NULL).
+ * Only DRNMI_F32X3 implicit-GEMM launches use it (drnmi/train.py passes it for the fp32x
+ * fine-tune); the plan depends on the geometry alone, so a size queried once per layer holds for
+ * every step. */
 int64_t drnmi_conv_workspace_bytes(const drnmi_conv_args* args);
 
 /* Fused stem + layer1 (bf16, csrc/patch_conv.hip stem_l1_kernel): replaces the two launches

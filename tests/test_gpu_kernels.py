@@ -583,7 +583,28 @@ def test_conv_x6_split_k(case):
     _x6_case(case, split=True)
 
 
-def _x6_case(case, split):
+@pytest.mark.parametrize("case", [X6_CASES[0], X6_CASES[2], X6_CASES[4]])
+def test_conv_x6_variants_bit_identical(case):
+    """Every conv_x6 tile variant (forced through drnmi_conv_args.tile: 256 / 128 / 64 channels,
+    8- and 4-wave, and the 128 x 128 two-per-CU tile) keeps each accumulator's MFMA order: the
+    outputs are bit-identical to the auto variant's."""
+    outs = {}
+    for v in (-1, 0, 1, 2, 3, 4):
+        y = _x6_case(case, split=False, tile=v, check=v == -1)
+        if y is not None:
+            outs[v] = y
+    assert len(outs) >= 3
+    for v, y in outs.items():
+        assert torch.equal(y, outs[-1]), v
+
+
+def test_conv_x6_two_per_cu_split_k():
+    """The two-workgroups-per-CU tile under a forced split-K (tile = 4 + 5 * 2): as accurate as the
+    unsplit kernel."""
+    _x6_case(X6_CASES[0], split=True, tile=4 + 5 * 2)
+
+
+def _x6_case(case, split, tile=-1, check=True):
     import torch.nn.functional as F
     from drnmi import ops
     from drnmi.engine import split3_bf16
@@ -621,9 +642,12 @@ def _x6_case(case, split):
     a.ho, a.wo, a.cout, a.cout_pad = ho, wo, cout, wpk.shape[0]
     a.ks, a.stride, a.pad, a.dil = ks, s, pad, dil
     a.k, a.k_pad = k, wpk.shape[1]
-    a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_F32X3, _lib.DRNMI_F32, -1, _lib.ALGO_IGEMM
+    a.relu, a.dtype, a.out_dtype, a.tile, a.algo = 1, _lib.DRNMI_F32X3, _lib.DRNMI_F32, tile, _lib.ALGO_IGEMM
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
     assert name.startswith("conv_x6_kernel")
+    bco = int(name.split("<")[1].split(",")[1]) * int(name.split(",")[2])
+    if (cout + bco - 1) // bco * bco > wpk.shape[0]:
+        return None                                   # a forced tile wider than the packed rows
     if split:
         nb = _lib.load().drnmi_conv_workspace_bytes(ctypes.byref(a))
         assert nb > 0, "these geometries leave most CUs idle: the launch must split"
@@ -637,7 +661,9 @@ def _x6_case(case, split):
     e_f32 = np.abs(f32.cpu().double().numpy() - ref).max()
     scale = np.abs(ref).max()
     print(f"{name} {case}: max-abs vs fp64 {e_x6:.2e} (exact-f32 kernel {e_f32:.2e}, |y| {scale:.1f})")
-    assert e_x6 <= max(4 * e_f32, 1e-6 * scale)
+    if check:
+        assert e_x6 <= max(4 * e_f32, 1e-6 * scale)
+    return y
 
 
 @pytest.mark.parametrize("case", [

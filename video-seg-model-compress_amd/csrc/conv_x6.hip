@@ -38,7 +38,6 @@ typedef __attribute__((address_space(1))) const void g_void_t;
 __device__ uint4 g_x6_zero[64];   // zero-initialised: the source of padded taps / rows
 
 
-constexpr int kBPX = 256;   // pixels per tile
 constexpr int kBK = 32;     // input channels per K step
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
@@ -63,45 +62,51 @@ __device__ __forceinline__ void ds_rd(V& dst, uint32_t base) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(OFF));
 }
 
-template <int WCO, int WC>
+// Tile = BCO = WCO x WC output channels x BPX = 64 x PS pixels; one wave per (channel column,
+// 64-pixel slice).  PS = 4: one workgroup per CU (2- or 3-stage ring in up to 160 KB of LDS);
+// PS = 2: a 128 x 128 tile of four waves in <= 80 KB, two workgroups per CU (their barriers
+// interleave, and the short-K 1/8-resolution launches get twice the tiles).
+template <int WCO, int WC, int PS>
 struct X6Cfg {
   static constexpr int BCO = WCO * WC;
+  static constexpr int BPX = 64 * PS;
   static constexpr int FM = WCO / 16;
   static constexpr int FN = 4;
-  static constexpr int NW = 4 * WC;
+  static constexpr int NW = PS * WC;
   static constexpr int THREADS = 64 * NW;
+  static constexpr int OCC = PS == 2 ? 2 : 1;       // workgroups per CU the LDS ring is sized for
   static constexpr int A_PLANE = BCO * 64;          // one bf16 plane: BCO rows x 32 K x 2 B
   static constexpr int A_BYTES = 3 * A_PLANE;
-  static constexpr int B_BYTES = kBPX * 128;        // 256 pixel rows x 32 ch x 4 B
+  static constexpr int B_BYTES = BPX * 128;         // BPX pixel rows x 32 ch x 4 B
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int A_PW = A_BYTES / 1024 / NW;  // 1-KB DMA pieces per wave per step
   static constexpr int B_PW = B_BYTES / 1024 / NW;
   static constexpr int GLDS = A_PW + B_PW;
-  static constexpr int NST = (2 * STAGE <= 160 * 1024 && 3 * STAGE > 160 * 1024) ? 2 : 3;
+  static constexpr int NST = 3 * STAGE * OCC <= 160 * 1024 ? 3 : 2;
   static constexpr int LDS = NST * STAGE;
   static_assert(A_PW * NW * 1024 == A_BYTES && B_PW * NW * 1024 == B_BYTES, "DMA split");
-  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(LDS * OCC <= 160 * 1024, "LDS");
 };
 
-template <int KS, int WCO, int WC>
-__global__ void __launch_bounds__(256 * WC, 1)
+template <int KS, int WCO, int WC, int PS>
+__global__ void __launch_bounds__(64 * PS * WC, PS == 2 ? 2 : 1)   // X6Cfg::OCC
 conv_x6_kernel(const drnmi_conv_args p) {
-  using C = X6Cfg<WCO, WC>;
+  using C = X6Cfg<WCO, WC, PS>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wc = wave >> 2;          // channel column of the tile
-  const int wp = wave & 3;           // 64-pixel slice of the tile
+  const int wc = wave / PS;          // channel column of the tile
+  const int wp = wave % PS;          // 64-pixel slice of the tile
   const int fr = lane & 15;
   const int fq = lane >> 4;
   const int M = p.n * p.ho * p.wo;
   const int hw_o = p.ho * p.wo;
   const int nco = (p.cout + C::BCO - 1) / C::BCO;
-  const int npx = (M + kBPX - 1) / kBPX;
+  const int npx = (M + C::BPX - 1) / C::BPX;
   const int tile = xcd_remap(blockIdx.x, npx * nco);
-  const int px0 = (tile / nco) * kBPX;
+  const int px0 = (tile / nco) * C::BPX;
   const int co0 = (tile % nco) * C::BCO;
 
   const int cin = p.cin;
@@ -449,19 +454,19 @@ __global__ void __launch_bounds__(256) x6_splitk_epilogue_kernel(const drnmi_con
   }
 }
 
-template <int KS, int WCO, int WC>
+template <int KS, int WCO, int WC, int PS>
 hipError_t launch_x6(const drnmi_conv_args& p, int splits, hipStream_t s) {
-  using C = X6Cfg<WCO, WC>;
+  using C = X6Cfg<WCO, WC, PS>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x6_kernel<KS, WCO, WC>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x6_kernel<KS, WCO, WC, PS>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
-  const int64_t blocks = ((M + kBPX - 1) / kBPX) * ((p.cout + C::BCO - 1) / C::BCO);
-  hipLaunchKernelGGL((conv_x6_kernel<KS, WCO, WC>), dim3(static_cast<unsigned>(blocks), splits), dim3(C::THREADS),
+  const int64_t blocks = ((M + C::BPX - 1) / C::BPX) * ((p.cout + C::BCO - 1) / C::BCO);
+  hipLaunchKernelGGL((conv_x6_kernel<KS, WCO, WC, PS>), dim3(static_cast<unsigned>(blocks), splits), dim3(C::THREADS),
                      C::LDS, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || splits == 1) return e;
@@ -472,25 +477,24 @@ hipError_t launch_x6(const drnmi_conv_args& p, int splits, hipStream_t s) {
   return hipGetLastError();
 }
 
-// 0: 256-channel tile (8 waves), 1: 128 (4 waves), 2: 64 (4 waves)
-// variants: 0 <K, 128, 2> (256 channels, 8 waves), 1 <K, 128, 1> (128, 4 waves), 2 <K, 64, 1> (64, 4
-// waves), 3 <K, 64, 2> (128 channels, 8 waves); a drnmi_conv_args.tile >= 0 forces variant
-// tile % 4 and, when tile >= 4, tile / 4 split-K partitions (tests, micro-benchmarks; split-K only
-// with a caller workspace)
-constexpr int kX6Bco[4] = {256, 128, 64, 128};
-constexpr int kNumX6 = 4;
+// variants: 0 <K, 128, 2, 4> (256 channels x 256 pixels, 8 waves), 1 <K, 128, 1, 4> (128 x 256, 4
+// waves), 2 <K, 64, 1, 4> (64 x 256, 4 waves), 3 <K, 64, 2, 4> (128 x 256, 8 waves), 4 <K, 64, 2, 2>
+// (128 x 128, 4 waves, two workgroups per CU).  A drnmi_conv_args.tile >= 0 forces variant
+// tile % 5 and, when tile >= 5, tile / 5 split-K partitions (tests, micro-benchmarks; split-K only
+// with a caller workspace).  Every variant keeps each accumulator's MFMA order: bit-identical.
+constexpr int kNumX6 = 5;
+constexpr int kX6Bco[kNumX6] = {256, 128, 64, 128, 128};
+constexpr int kX6Bpx[kNumX6] = {256, 256, 256, 256, 128};
+constexpr int kX6Occ[kNumX6] = {1, 1, 1, 1, 2};
+// seconds per 32-channel K step of one workgroup tile, fitted to scripts/x6_micro.py's sweep on
+// the fine-tune shapes (profiles/r8_finetune/x6_micro_variants.txt): the 256 x 256 tile ~4.3 us,
+// the 8-wave 128 x 256 ~3.0 us, the two-per-CU 128 x 128 ~2.7 us (its 2.1-3.0 us spread tracks
+// how the two resident workgroups overlap; past two rounds the model under-charges it)
+constexpr double kX6Step[kNumX6] = {4.3e-6, 3.6e-6, 2.2e-6, 3.0e-6, 2.7e-6};
 // 128-channel layers take the 8-wave tile (two waves per SIMD): D-22 layer4 492 vs 511 us, its 1x1
 // stride-2 downsample 64 vs 83 us at batch 8 (scripts/x6_micro.py, profiles/r7_x6)
 int x6_auto_variant(const drnmi_conv_args& p) { return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 3 : 2; }
-int x6_variant(const drnmi_conv_args& p) { return p.tile >= 0 ? p.tile % kNumX6 : x6_auto_variant(p); }
 
-// Split-K count for a launch whose tiles leave CUs idle (one workgroup per CU: 96 tiles of the
-// fine-tune's 2 x 128 x 96 layer5 convs used 96 of 256 CUs).  Cost model per split count S:
-// MFMA time at the fraction of CUs busy in each round plus the partials' HBM round trip
-// (S x M x cout fp32 written and read); S = 1 unless that is >= 5 % faster (the model is within a
-// few % of scripts/x6_micro.py's SPLITS sweep on the fine-tune shapes: 512 -> 512 d4 at 2 x 128 x 96
-// 619 / 568 us modelled for S = 1 / 4, 627 / 580 measured, profiles/r8_finetune).  Only with a
-// caller workspace (the fp32x training path): inference launches never split.
 int x6_num_cus() {
   static int cus = 0;
   if (cus == 0) {
@@ -502,42 +506,68 @@ int x6_num_cus() {
   return cus;
 }
 
-int x6_splits(const drnmi_conv_args& p) {
+// Launch plan (variant, split-K count); split_ok: the launch has (drnmi_conv_args.ws) or is sizing
+// (drnmi_conv_workspace_bytes) a caller workspace.  Inference launches (none) take the auto variant
+// unsplit.  The fp32x training path (a workspace) picks among the 256- / 128-channel tiles
+// and S = 1..4 by a cost model: rounds of resident workgroups x K steps per workgroup x the
+// variant's step time, plus the split partials' HBM round trip (S x M x cout fp32 written and
+// read) and the output (+ residual) stream.  The default (auto variant, S = 1) is kept unless the
+// best plan is >= 5 % faster.  The model is within a few % of the SPLITS sweep (512 -> 512 d4 at
+// 2 x 128 x 96: 631 / 580 us modelled for S = 1 / 4, 627 / 580 measured).
+struct X6Plan { int v, S; };
+X6Plan x6_plan(const drnmi_conv_args& p, bool split_ok) {
   // the partials are [split][m][cout] rows written as float4: only cout % 4 == 0 splits
-  if (p.cout % 4 != 0) return 1;
-  if (p.tile >= kNumX6) {
-    const int S = p.tile / kNumX6;
-    return S < 1 ? 1 : (S > p.k_pad / kBK ? p.k_pad / kBK : S);
+  if (p.cout % 4 != 0) split_ok = false;
+  if (p.tile >= 0) {
+    const int v = p.tile % kNumX6;
+    int S = p.tile / kNumX6;
+    if (!split_ok || S < 1) S = 1;
+    if (S > p.k_pad / kBK) S = p.k_pad / kBK;
+    return {v, S};
   }
+  const int v0 = x6_auto_variant(p);
+  if (!split_ok) return {v0, 1};
   const int cus = x6_num_cus();
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
-  const int64_t tiles = ((M + kBPX - 1) / kBPX) * ((p.cout + kX6Bco[x6_variant(p)] - 1) / kX6Bco[x6_variant(p)]);
   const int nk = p.k_pad / kBK;
-  const double flops = 2.0 * static_cast<double>(M) * p.cout * p.k;
-  auto cost = [&](int S) {
-    const int64_t wgs = tiles * S;
-    const int64_t rounds = (wgs + cus - 1) / cus;
-    const double busy = static_cast<double>(wgs) / static_cast<double>(rounds * cus);
-    double t = flops / (250e12 * busy);
+  const double out_s = static_cast<double>(M) * p.cout * 4.0 * (p.res != nullptr ? 2 : 1) / 4.5e12;
+  auto cost = [&](int v, int S) {
+    const int64_t tiles = ((M + kX6Bpx[v] - 1) / kX6Bpx[v]) * ((p.cout + kX6Bco[v] - 1) / kX6Bco[v]);
+    const int64_t slots = static_cast<int64_t>(cus) * kX6Occ[v];
+    const int64_t rounds = (tiles * S + slots - 1) / slots;
+    double t = static_cast<double>(rounds) * ((nk + S - 1) / S) * kX6Step[v] + out_s;
     if (S > 1) t += 2.0 * S * static_cast<double>(M) * p.cout * 4.0 / 4e12 + 4e-6;
     return t;
   };
-  const double c1 = cost(1);
-  int best = 1;
-  double bc = c1;
-  for (int S = 2; S <= 4 && nk / S >= 8; ++S) {
-    const double c = cost(S);
-    if (c < 0.95 * c1 && c < bc) {
-      best = S;
-      bc = c;
+  const double c0 = cost(v0, 1);
+  X6Plan best{v0, 1};
+  double bc = c0;
+  // Only the auto variant's split counts: with the two-per-CU 128 x 128 tile as a candidate (<= two
+  // rounds of it) the plan moved 1/3 of the step's conv_x6 launches onto it and the step's conv_x6
+  // time did not move (19.52 -> 19.57 ms, profiles/r8_finetune/x6_plan_v4.txt); variant 4 stays a
+  // forced tile for A/B runs.
+  const int cands[1] = {v0};
+  for (int v : cands) {
+    if ((p.cout + kX6Bco[v] - 1) / kX6Bco[v] * kX6Bco[v] > p.cout_pad) continue;
+    for (int S = 1; S <= 4 && (S == 1 || nk / S >= 8); ++S) {
+      const int64_t tiles = ((M + kX6Bpx[v] - 1) / kX6Bpx[v]) * ((p.cout + kX6Bco[v] - 1) / kX6Bco[v]);
+      if (kX6Occ[v] == 2 && tiles * S > 2 * 2 * static_cast<int64_t>(cus)) continue;
+      const double c = cost(v, S);
+      if (c < 0.95 * c0 && c < bc) {
+        best = {v, S};
+        bc = c;
+      }
     }
   }
   return best;
 }
-
+// the workspace a training launch of this geometry needs (its plan with splits allowed); a plan
+// that differs from the inference default without splitting asks for a token 256 B, since a
+// launch takes the training plan exactly when it is given a workspace
 int64_t x6_workspace_bytes(const drnmi_conv_args& p) {
-  const int S = x6_splits(p);
-  return S > 1 ? static_cast<int64_t>(S) * p.n * p.ho * p.wo * p.cout * 4 : 0;
+  const X6Plan pl = x6_plan(p, true);
+  if (pl.S > 1) return static_cast<int64_t>(pl.S) * p.n * p.ho * p.wo * p.cout * 4;
+  return pl.v != x6_plan(p, false).v ? 256 : 0;
 }
 
 }  // namespace
@@ -555,30 +585,30 @@ int64_t x6_conv_workspace_bytes(const drnmi_conv_args& p) {
 
 int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!x6_conv_supported(p)) return DRNMI_ENOTSUP;
-  const int v = x6_variant(p);
+  const X6Plan pl = x6_plan(p, p.ws != nullptr);
+  const int v = pl.v;
   // every weight row a tile's DMA reads must exist in each plane
   if ((p.cout + kX6Bco[v] - 1) / kX6Bco[v] * kX6Bco[v] > p.cout_pad) return DRNMI_EINVAL;
   if (3 * static_cast<int64_t>(p.cout_pad) * p.k_pad >= (int64_t(1) << 31)) return DRNMI_EINVAL;
-  int S = 1;
-  if (p.ws != nullptr) {
-    S = x6_splits(p);
-    if (S > 1 && p.ws_bytes < x6_workspace_bytes(p)) return DRNMI_EINVAL;
-    if (S > 1 && (reinterpret_cast<uintptr_t>(p.ws) & 15) != 0) return DRNMI_EINVAL;
-  }
+  const int S = pl.S;
+  if (S > 1 && p.ws_bytes < x6_workspace_bytes(p)) return DRNMI_EINVAL;
+  if (S > 1 && (reinterpret_cast<uintptr_t>(p.ws) & 15) != 0) return DRNMI_EINVAL;
   hipError_t e;
   if (p.ks == 3) {
     switch (v) {
-      case 0: e = launch_x6<3, 128, 2>(p, S, s); break;
-      case 1: e = launch_x6<3, 128, 1>(p, S, s); break;
-      case 2: e = launch_x6<3, 64, 1>(p, S, s); break;
-      default: e = launch_x6<3, 64, 2>(p, S, s); break;
+      case 0: e = launch_x6<3, 128, 2, 4>(p, S, s); break;
+      case 1: e = launch_x6<3, 128, 1, 4>(p, S, s); break;
+      case 2: e = launch_x6<3, 64, 1, 4>(p, S, s); break;
+      case 3: e = launch_x6<3, 64, 2, 4>(p, S, s); break;
+      default: e = launch_x6<3, 64, 2, 2>(p, S, s); break;
     }
   } else {
     switch (v) {
-      case 0: e = launch_x6<1, 128, 2>(p, S, s); break;
-      case 1: e = launch_x6<1, 128, 1>(p, S, s); break;
-      case 2: e = launch_x6<1, 64, 1>(p, S, s); break;
-      default: e = launch_x6<1, 64, 2>(p, S, s); break;
+      case 0: e = launch_x6<1, 128, 2, 4>(p, S, s); break;
+      case 1: e = launch_x6<1, 128, 1, 4>(p, S, s); break;
+      case 2: e = launch_x6<1, 64, 1, 4>(p, S, s); break;
+      case 3: e = launch_x6<1, 64, 2, 4>(p, S, s); break;
+      default: e = launch_x6<1, 64, 2, 2>(p, S, s); break;
     }
   }
   return static_cast<int>(e);
@@ -586,11 +616,14 @@ int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
 
 const char* x6_conv_name(const drnmi_conv_args& p) {
   if (!x6_conv_supported(p)) return nullptr;
-  static const char* n3[kNumX6] = {"conv_x6_kernel<3, 128, 2>", "conv_x6_kernel<3, 128, 1>", "conv_x6_kernel<3, 64, 1>",
-                                   "conv_x6_kernel<3, 64, 2>"};
-  static const char* n1[kNumX6] = {"conv_x6_kernel<1, 128, 2>", "conv_x6_kernel<1, 128, 1>", "conv_x6_kernel<1, 64, 1>",
-                                   "conv_x6_kernel<1, 64, 2>"};
-  return p.ks == 3 ? n3[x6_variant(p)] : n1[x6_variant(p)];
+  static const char* n3[kNumX6] = {"conv_x6_kernel<3, 128, 2, 4>", "conv_x6_kernel<3, 128, 1, 4>",
+                                   "conv_x6_kernel<3, 64, 1, 4>", "conv_x6_kernel<3, 64, 2, 4>",
+                                   "conv_x6_kernel<3, 64, 2, 2>"};
+  static const char* n1[kNumX6] = {"conv_x6_kernel<1, 128, 2, 4>", "conv_x6_kernel<1, 128, 1, 4>",
+                                   "conv_x6_kernel<1, 64, 1, 4>", "conv_x6_kernel<1, 64, 2, 4>",
+                                   "conv_x6_kernel<1, 64, 2, 2>"};
+  const int v = x6_plan(p, p.ws != nullptr).v;
+  return p.ks == 3 ? n3[v] : n1[v];
 }
 
 }  // namespace drnmi
