@@ -30,7 +30,7 @@ extern "C" {
  * against another header must not pass them: check drnmi_abi_version() == DRNMI_ABI_VERSION and
  * drnmi_conv_args_size() == sizeof(drnmi_conv_args) once after loading the library (drnmi/_lib.py
  * does, and refuses a mismatched library). */
-#define DRNMI_ABI_VERSION 4
+#define DRNMI_ABI_VERSION 5
 int32_t drnmi_abi_version(void);
 int64_t drnmi_conv_args_size(void);
 
@@ -113,6 +113,13 @@ typedef struct drnmi_conv_args {
    * the inference plan (the inference engine's launches); other dtypes ignore it. */
   void* ws;
   int64_t ws_bytes;
+  /* Optional train-mode BN statistics of the stored output (F32X3 conv_x6 launches that do not
+   * split K: drnmi_conv_stats_rows(args) > 0): the epilogue writes per-channel fp64 partial sums
+   * of y and y^2, one row per 64-pixel wave slice, as [2][rows][cout] (sums, then sums of
+   * squares), in a fixed order.  drnmi_bn_stats_partials_f32 turns them into the batch mean /
+   * invstd exactly as drnmi_bn_stats_f32 would from y (semantic_seg.py:166-230's train-mode
+   * BatchNorm2d after the conv), without reading y again.  NULL: off. */
+  double* stats;
 } drnmi_conv_args;
 
 /* Algorithms behind drnmi_conv2d_bn_act:
@@ -134,6 +141,10 @@ typedef struct drnmi_conv_args {
 enum drnmi_algo { DRNMI_ALGO_IGEMM = 0, DRNMI_ALGO_PATCH = 1 };
 
 int drnmi_conv2d_bn_act(const drnmi_conv_args* args, void* stream);
+
+/* Rows of the args->stats partials this launch writes (4 per 256-pixel tile), or 0 when it
+ * cannot produce them (not conv_x6, or a split-K plan: compute the statistics from y). */
+int64_t drnmi_conv_stats_rows(const drnmi_conv_args* args);
 
 /* Bytes of args->ws the training plan of these arguments needs (0: the inference plan; 256: a
  * different tile variant, no split; else S x M x cout x 4 for S split-K partitions; -1: NULL).
@@ -381,6 +392,13 @@ int64_t drnmi_reduce_workspace_bytes(int64_t rows, int32_t channels);
 int drnmi_bn_stats_f32(const float* y, int64_t rows, int32_t C, float eps, float momentum,
                        float* mean, float* invstd, float* running_mean, float* running_var,
                        int64_t* num_batches_tracked, void* ws, void* stream);
+
+/* drnmi_bn_stats_f32 from the partial sums a conv epilogue wrote (drnmi_conv_args.stats:
+ * [2][G][C] fp64, G = drnmi_conv_stats_rows): the same finalize (mean, biased variance, invstd,
+ * running-stat update) over `rows` pixels. */
+int drnmi_bn_stats_partials_f32(const double* partials, int64_t G, int64_t rows, int32_t C, float eps,
+                                float momentum, float* mean, float* invstd, float* running_mean,
+                                float* running_var, int64_t* num_batches_tracked, void* stream);
 
 /* z = relu?(((y - mean) * invstd) * gamma + beta [+ res]) over [rows][C]; gamma/beta/res NULL-able.
  * (BasicBlock / Bottleneck tail: lmodels/drn.py:49-65, :86-106.)  mean/invstd/gamma/beta must be

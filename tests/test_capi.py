@@ -50,6 +50,18 @@ def test_argument_validation_without_gpu():
     assert lib.drnmi_up8_logsoftmax_argmax(None, None, None, None, 2, 1, 19, 8, 8, None) == -1
     assert lib.drnmi_mask_apply_f32(-1, None, None, None, None) == -1
     assert lib.drnmi_mask_apply_f32(0, None, None, None, None) == 0
+    # BN-statistics partials: only from an fp32x conv_x6 launch; the finalize validates its inputs
+    assert lib.drnmi_conv_stats_rows(None) == -1
+    b = _lib.ConvArgs()
+    b.n, b.h, b.w, b.cin, b.ho, b.wo, b.cout, b.cout_pad = 1, 8, 8, 64, 8, 8, 64, 128
+    b.ks, b.stride, b.pad, b.dil, b.k, b.k_pad = 1, 1, 0, 1, 64, 64
+    b.dtype = b.out_dtype = _lib.DRNMI_F32
+    assert lib.drnmi_conv_stats_rows(ctypes.byref(b)) == 0          # not fp32x: no partials
+    b.stats = 0x1000
+    assert lib.drnmi_conv2d_bn_act(ctypes.byref(b), None) == -1    # refused before any launch
+    b.dtype = _lib.DRNMI_F32X3
+    assert lib.drnmi_conv_stats_rows(ctypes.byref(b)) == 4         # one 256-pixel tile: 4 wave rows
+    assert lib.drnmi_bn_stats_partials_f32(None, 4, 64, 64, 1e-5, 0.1, None, None, None, None, None, None) == -1
 
 
 def test_pack_table_check_without_gpu():

@@ -604,7 +604,48 @@ def test_conv_x6_two_per_cu_split_k():
     _x6_case(X6_CASES[0], split=True, tile=4 + 5 * 2)
 
 
-def _x6_case(case, split, tile=-1, check=True):
+@pytest.mark.parametrize("case", [X6_CASES[1], X6_CASES[2], (2, 24, 20, 64, 256, 1, 1, 0, 1, False)])
+def test_conv_x6_bn_stats_partials(case):
+    """drnmi_conv_args.stats: the conv_x6 epilogue's per-channel fp64 sums of y and y^2 (one row
+    per 64-pixel wave slice) match fp64 sums over the stored y, and drnmi_bn_stats_partials_f32
+    gives the batch mean / invstd / running stats of drnmi_bn_stats_f32 over y."""
+    n, h, w, cin, cout, ks, s, pad, dil, _ = case
+    y, args, keep = _x6_case(case, split=False, check=False, stats=True)
+    rows = y.numel() // cout
+    G = _lib.load().drnmi_conv_stats_rows(ctypes.byref(args))
+    part = keep["stats"].view(2, G, cout).cpu().numpy()
+    yd = y.reshape(rows, cout).double().cpu().numpy()
+    np.testing.assert_allclose(part[0].sum(0), yd.sum(0), rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(part[1].sum(0), (yd * yd).sum(0), rtol=1e-12, atol=1e-9)
+    lib = _lib.load()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    sp = ctypes.c_void_p(_lib.stream_ptr())
+    outs = []
+    for fused in (True, False):
+        mean, invstd = torch.empty(cout, device=DEV), torch.empty(cout, device=DEV)
+        rm, rv = torch.zeros(cout, device=DEV), torch.ones(cout, device=DEV)
+        if fused:
+            _lib.check(lib.drnmi_bn_stats_partials_f32(vp(keep["stats"]), G, rows, cout, 1e-5, 0.1, vp(mean),
+                                                       vp(invstd), vp(rm), vp(rv), None, sp), "partials")
+        else:
+            ws = torch.empty(lib.drnmi_reduce_workspace_bytes(rows, cout), dtype=torch.uint8, device=DEV)
+            _lib.check(lib.drnmi_bn_stats_f32(vp(y), rows, cout, 1e-5, 0.1, vp(mean), vp(invstd), vp(rm), vp(rv),
+                                              None, vp(ws), sp), "stats")
+        outs.append([t.cpu() for t in (mean, invstd, rm, rv)])
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=2e-7, atol=1e-9)
+
+
+def test_conv_x6_bn_stats_refused_with_split_k():
+    """A split-K plan cannot write the statistics: the launch is refused, nothing runs."""
+    y, args, keep = _x6_case(X6_CASES[0], split=True, check=False, stats="query")
+    assert _lib.load().drnmi_conv_stats_rows(ctypes.byref(args)) == 0
+    args.stats = keep["y"].data_ptr()
+    assert _lib.load().drnmi_conv2d_bn_act(ctypes.byref(args), ctypes.c_void_p(_lib.stream_ptr())) == -1
+
+
+def _x6_case(case, split, tile=-1, check=True, stats=False):
     import torch.nn.functional as F
     from drnmi import ops
     from drnmi.engine import split3_bf16
@@ -648,12 +689,21 @@ def _x6_case(case, split, tile=-1, check=True):
     bco = int(name.split("<")[1].split(",")[1]) * int(name.split(",")[2])
     if (cout + bco - 1) // bco * bco > wpk.shape[0]:
         return None                                   # a forced tile wider than the packed rows
+    keep = {"y": y}
     if split:
         nb = _lib.load().drnmi_conv_workspace_bytes(ctypes.byref(a))
         assert nb > 0, "these geometries leave most CUs idle: the launch must split"
         ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
         a.ws, a.ws_bytes = ws.data_ptr(), nb
+        keep["ws"] = ws
         name += f" split-K {nb // (4 * n * ho * wo * cout)}"
+    if stats == "query":
+        return y, a, keep
+    if stats:
+        rows = _lib.load().drnmi_conv_stats_rows(ctypes.byref(a))
+        assert rows > 0
+        keep["stats"] = torch.full((2 * rows * cout,), float("nan"), dtype=torch.float64, device=DEV)
+        a.stats = keep["stats"].data_ptr()
     _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "x6")
     torch.cuda.synchronize()
     ref = y64.permute(0, 2, 3, 1).numpy()
@@ -663,7 +713,7 @@ def _x6_case(case, split, tile=-1, check=True):
     print(f"{name} {case}: max-abs vs fp64 {e_x6:.2e} (exact-f32 kernel {e_f32:.2e}, |y| {scale:.1f})")
     if check:
         assert e_x6 <= max(4 * e_f32, 1e-6 * scale)
-    return y
+    return (y, a, keep) if stats else y
 
 
 @pytest.mark.parametrize("case", [

@@ -175,6 +175,26 @@ def test_batched_weight_pack_matches_per_layer(precision, monkeypatch):
     assert all(torch.equal(a, b) for a, b in zip(outs[0][1], outs[1][1]))
 
 
+def test_fused_bn_stats_match_separate_pass(monkeypatch):
+    """fp32x: the BN batch statistics from the conv_x6 epilogue partials (FUSED_BN_STATS) vs the
+    separate fp64 pass over y -- the same sums in another fixed order: three steps' losses and
+    parameters agree to fp32 rounding."""
+    import drnmi.train as T
+    g = TC.load()
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setattr(T, "FUSED_BN_STATS", fused)
+        m, pr = TC.model_and_masks(g)
+        m.set_precision("fp32x")
+        xs, ts = TC.inputs(g)
+        m, losses = _run_hip_steps(m, pr, xs * 3, ts * 3)
+        outs.append((losses, {k: v.detach().double().cpu() for k, v in m.state_dict().items()
+                              if v.is_floating_point()}))
+    np.testing.assert_allclose(outs[1][0], outs[0][0], rtol=1e-6)
+    for k, v in outs[0][1].items():
+        assert TC.rel_err(outs[1][1][k].numpy(), v.numpy()) <= 1e-5, k
+
+
 def test_eval_after_train_uses_new_weights():
     """Training bumps parameter/buffer versions, so the eval plan repacks (drnseg._state_key)."""
     from drnmi.drnseg import DRNSeg

@@ -321,6 +321,8 @@ extern "C" const char* drnmi_conv_tile_name(int tile) {
 extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (a == nullptr) return DRNMI_EINVAL;
   const drnmi_conv_args& p = *a;
+  // BN-statistics partials come from conv_x6's epilogue only (drnmi_conv_stats_rows)
+  if (p.stats != nullptr && (p.algo != DRNMI_ALGO_IGEMM || x6_conv_stats_rows(p) <= 0)) return DRNMI_EINVAL;
   if (p.algo == DRNMI_ALGO_PATCH) {
     if (p.x2 != nullptr) return DRNMI_ENOTSUP;     // fused second input: LDS-DMA kernels only
     if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.shift == nullptr ||
@@ -369,6 +371,11 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
 extern "C" int64_t drnmi_conv_workspace_bytes(const drnmi_conv_args* a) {
   if (a == nullptr) return -1;
   return a->dtype == DRNMI_F32X3 && a->algo == DRNMI_ALGO_IGEMM ? x6_conv_workspace_bytes(*a) : 0;
+}
+
+extern "C" int64_t drnmi_conv_stats_rows(const drnmi_conv_args* a) {
+  if (a == nullptr) return -1;
+  return a->dtype == DRNMI_F32X3 && a->algo == DRNMI_ALGO_IGEMM ? x6_conv_stats_rows(*a) : 0;
 }
 
 extern "C" int drnmi_stem_layer1(const drnmi_conv_args* stem, const drnmi_conv_args* next, void* stream) {

@@ -55,6 +55,25 @@ __device__ __forceinline__ int swz64(int row, int chunk) { return chunk ^ (((row
 __device__ __forceinline__ int swz128(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }   // fp32 B rows
 
 
+// x from the lane DPP control CTRL selects, as two 32-bit DPP moves
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(u & 0xffffffffu), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
+}
+// sum over the 16 lanes of a DPP row, the same in every lane: quad_perm xor 1, xor 2, then
+// row_half_mirror (quads 0 <-> 1) and row_mirror (halves) -- a fixed order, ALU only (the
+// ds_bpermute form of __shfl_xor cost the short-K launches ~10 % in their epilogue)
+__device__ __forceinline__ double row16_sum(double x) {
+  x += dpp_f64<0xB1>(x);    // quad_perm [1, 0, 3, 2]
+  x += dpp_f64<0x4E>(x);    // quad_perm [2, 3, 0, 1]
+  x += dpp_f64<0x141>(x);   // row_half_mirror
+  x += dpp_f64<0x140>(x);   // row_mirror
+  return x;
+}
+
 // one ds_read_b128 at LDS byte address base + OFF (smem is the kernel's only LDS object: byte 0)
 template <int OFF, typename V>
 __device__ __forceinline__ void ds_rd(V& dst, uint32_t base) {
@@ -337,58 +356,110 @@ conv_x6_kernel(const drnmi_conv_args p) {
   // --- epilogue: lane owns channels co..co+3 of pixel m, fp32
   const float* __restrict__ res = reinterpret_cast<const float*>(p.res);
   const bool nhwc = p.y_sc == 1;
+  // the lane's output row offsets, one per pixel fragment (-1: past the last pixel)
+  int64_t ybase_fn[C::FN];
 #pragma unroll
   for (int fn = 0; fn < C::FN; ++fn) {
     const int m = px0 + wp * 64 + fn * 16 + fr;
-    if (m >= M) continue;
     const int n = m / hw_o;
     const int q = m - n * hw_o;
-    const int64_t ybase = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp;
-#pragma unroll
-    for (int fm = 0; fm < C::FM; ++fm) {
-      const int co = co0 + wc * WCO + fm * 16 + fq * 4;
-      if (co >= p.cout) continue;
-      const bool full = co + 3 < p.cout;
-      const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);   // padded to cout_pad
-      float v[4] = {acc[fm][fn][0], acc[fm][fn][1], acc[fm][fn][2], acc[fm][fn][3]};
-      if (p.scale != nullptr) {
-        const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);
-        v[0] = v[0] * sc.x + sh.x;
-        v[1] = v[1] * sc.y + sh.y;
-        v[2] = v[2] * sc.z + sh.z;
-        v[3] = v[3] * sc.w + sh.w;
-      } else {
-        v[0] += sh.x;
-        v[1] += sh.y;
-        v[2] += sh.z;
-        v[3] += sh.w;
-      }
-      if (res != nullptr) {
-        const float* rp = res + static_cast<int64_t>(m) * p.cout + co;
-        if (full) {
-          const float4 rv = *reinterpret_cast<const float4*>(rp);
-          v[0] += rv.x;
-          v[1] += rv.y;
-          v[2] += rv.z;
-          v[3] += rv.w;
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (co + j < p.cout) v[j] += rp[j];
-        }
-      }
-      if (p.relu) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
-      }
-      float* y = reinterpret_cast<float*>(p.y);
-      if (nhwc && full) {
-        *reinterpret_cast<float4*>(y + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
+    ybase_fn[fn] = m < M ? static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp : -1;
+  }
+  // one (fragment fm, pixel fragment fn) of the lane: v = acc * scale + shift (+ res), ReLU,
+  // stored; false when the pixel or the channel group lies outside the output
+  auto epi = [&](int fm, int fn, float (&v)[4]) -> bool {
+    const int m = px0 + wp * 64 + fn * 16 + fr;
+    const int co = co0 + wc * WCO + fm * 16 + fq * 4;
+    const int64_t ybase = ybase_fn[fn];
+    if (ybase < 0 || co >= p.cout) return false;
+    const bool full = co + 3 < p.cout;
+    const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);   // padded to cout_pad
+    v[0] = acc[fm][fn][0];
+    v[1] = acc[fm][fn][1];
+    v[2] = acc[fm][fn][2];
+    v[3] = acc[fm][fn][3];
+    if (p.scale != nullptr) {
+      const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);
+      v[0] = v[0] * sc.x + sh.x;
+      v[1] = v[1] * sc.y + sh.y;
+      v[2] = v[2] * sc.z + sh.z;
+      v[3] = v[3] * sc.w + sh.w;
+    } else {
+      v[0] += sh.x;
+      v[1] += sh.y;
+      v[2] += sh.z;
+      v[3] += sh.w;
+    }
+    if (res != nullptr) {
+      const float* rp = res + static_cast<int64_t>(m) * p.cout + co;
+      if (full) {
+        const float4 rv = *reinterpret_cast<const float4*>(rp);
+        v[0] += rv.x;
+        v[1] += rv.y;
+        v[2] += rv.z;
+        v[3] += rv.w;
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (co + j < p.cout) y[ybase + static_cast<int64_t>(co + j) * p.y_sc] = v[j];
+          if (co + j < p.cout) v[j] += rp[j];
       }
+    }
+    if (p.relu) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    float* y = reinterpret_cast<float*>(p.y);
+    if (nhwc && full) {
+      *reinterpret_cast<float4*>(y + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (co + j < p.cout) y[ybase + static_cast<int64_t>(co + j) * p.y_sc] = v[j];
+    }
+    return true;
+  };
+  if (p.stats == nullptr) {
+#pragma unroll
+    for (int fn = 0; fn < C::FN; ++fn)
+#pragma unroll
+      for (int fm = 0; fm < C::FM; ++fm) {
+        float v[4];
+        epi(fm, fn, v);
+      }
+    return;
+  }
+  // BN statistics of the stored values (drnmi_conv_args.stats): per channel fragment, the lane's
+  // four pixels in fp64, then a fixed xor tree over the 16 lanes of its pixel column; row g = this
+  // wave's 64-pixel slice, [2][G][cout] (sums, then sums of squares)
+  const int G = npx * PS;
+  const int g = (tile / nco) * PS + wp;
+#pragma unroll
+  for (int fm = 0; fm < C::FM; ++fm) {
+    double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int fn = 0; fn < C::FN; ++fn) {
+      float v[4];
+      if (epi(fm, fn, v)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a1[j] += static_cast<double>(v[j]);
+          a2[j] += static_cast<double>(v[j]) * v[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a1[j] = row16_sum(a1[j]);
+      a2[j] = row16_sum(a2[j]);
+    }
+    const int co = co0 + wc * WCO + fm * 16 + fq * 4;
+    if (fr == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (co + j < p.cout) {
+          p.stats[static_cast<int64_t>(g) * p.cout + co + j] = a1[j];
+          p.stats[static_cast<int64_t>(G + g) * p.cout + co + j] = a2[j];
+        }
     }
   }
 }
@@ -583,6 +654,15 @@ int64_t x6_conv_workspace_bytes(const drnmi_conv_args& p) {
   return x6_conv_supported(p) ? x6_workspace_bytes(p) : 0;
 }
 
+// rows of BN-statistics partials a launch with these arguments writes (0: it cannot -- split K)
+int64_t x6_conv_stats_rows(const drnmi_conv_args& p) {
+  if (!x6_conv_supported(p)) return 0;
+  const X6Plan pl = x6_plan(p, p.ws != nullptr);
+  if (pl.S > 1) return 0;
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  return (M + kX6Bpx[pl.v] - 1) / kX6Bpx[pl.v] * (kX6Bpx[pl.v] / 64);
+}
+
 int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!x6_conv_supported(p)) return DRNMI_ENOTSUP;
   const X6Plan pl = x6_plan(p, p.ws != nullptr);
@@ -591,6 +671,8 @@ int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if ((p.cout + kX6Bco[v] - 1) / kX6Bco[v] * kX6Bco[v] > p.cout_pad) return DRNMI_EINVAL;
   if (3 * static_cast<int64_t>(p.cout_pad) * p.k_pad >= (int64_t(1) << 31)) return DRNMI_EINVAL;
   const int S = pl.S;
+  if (S > 1 && p.stats != nullptr) return DRNMI_EINVAL;   // statistics only from an unsplit launch
+  if (p.stats != nullptr && (reinterpret_cast<uintptr_t>(p.stats) & 7) != 0) return DRNMI_EINVAL;
   if (S > 1 && p.ws_bytes < x6_workspace_bytes(p)) return DRNMI_EINVAL;
   if (S > 1 && (reinterpret_cast<uintptr_t>(p.ws) & 15) != 0) return DRNMI_EINVAL;
   hipError_t e;

@@ -29,6 +29,7 @@ const char* halo_conv_name(const drnmi_conv_args& p);
 bool x6_conv_supported(const drnmi_conv_args& p);
 int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s);
 int64_t x6_conv_workspace_bytes(const drnmi_conv_args& p);
+int64_t x6_conv_stats_rows(const drnmi_conv_args& p);
 const char* x6_conv_name(const drnmi_conv_args& p);
 // The strip tile with staggered SIMD partners (conv_stag.hip): 3x3 stride-1 bf16, wo % 256 == 0,
 // cin % 128 == 0 (conv_big.hip's dispatch checks the shape).

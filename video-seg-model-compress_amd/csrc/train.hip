@@ -1735,6 +1735,19 @@ extern "C" int drnmi_bn_stats_f32(const float* y, int64_t rows, int32_t C, float
   return static_cast<int>(hipGetLastError());
 }
 
+extern "C" int drnmi_bn_stats_partials_f32(const double* partials, int64_t G, int64_t rows, int32_t C, float eps,
+                                           float momentum, float* mean, float* invstd, float* running_mean,
+                                           float* running_var, int64_t* num_batches_tracked, void* stream) {
+  if (partials == nullptr || mean == nullptr || invstd == nullptr || G <= 0 || G >= (int64_t(1) << 31) || rows <= 0 ||
+      C <= 0)
+    return DRNMI_EINVAL;
+  if ((running_mean == nullptr) != (running_var == nullptr)) return DRNMI_EINVAL;
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(fin_grid(C)), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                     partials, static_cast<int>(G), C, rows, eps, momentum, mean, invstd, running_mean, running_var,
+                     num_batches_tracked);
+  return static_cast<int>(hipGetLastError());
+}
+
 extern "C" int drnmi_bn_act_f32(const float* y, const float* mean, const float* invstd, const float* gamma,
                                 const float* beta, const float* res, int32_t relu, int64_t rows, int32_t C,
                                 float* z, void* stream) {

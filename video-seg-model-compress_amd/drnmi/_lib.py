@@ -44,6 +44,7 @@ class ConvArgs(ctypes.Structure):
         ("x2", ctypes.c_void_p),
         ("cin2", ctypes.c_int32), ("h2", ctypes.c_int32), ("w2", ctypes.c_int32), ("stride2", ctypes.c_int32),
         ("ws", ctypes.c_void_p), ("ws_bytes", ctypes.c_int64),
+        ("stats", ctypes.c_void_p),
     ]
 
 
@@ -103,6 +104,8 @@ SIGNATURES = {
     "drnmi_channel_sum_f32": (ctypes.c_int, [_VP, _I64, _I32, _I32, _VP, _I32, _VP, _VP]),
     "drnmi_conv_wgrad_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
     "drnmi_conv_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(ConvArgs)]),
+    "drnmi_conv_stats_rows": (ctypes.c_int64, [ctypes.POINTER(ConvArgs)]),
+    "drnmi_bn_stats_partials_f32": (ctypes.c_int, [_VP, _I64, _I64, _I32, _F32, _F32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "drnmi_conv_wgrad_f32": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
     "drnmi_conv_wgrad_f32x3": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
     "drnmi_split3_bf16": (ctypes.c_int, [_VP, ctypes.c_int64, _VP, _VP]),
@@ -127,7 +130,7 @@ SIGNATURES = {
     "drnmi_pack_table_check": (ctypes.c_int, [_VP, _I32, ctypes.POINTER(ctypes.c_int64)]),
     "drnmi_pack_conv_weights_batched": (ctypes.c_int, [_VP, _I32, _I64, _VP]),
 }
-ABI_VERSION = 4          # include/drnmi.h DRNMI_ABI_VERSION
+ABI_VERSION = 5          # include/drnmi.h DRNMI_ABI_VERSION
 
 _lib = None
 

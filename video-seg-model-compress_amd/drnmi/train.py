@@ -40,6 +40,9 @@ from .engine import COUT_ALIGN, K_ALIGN, X6_PATCH_SHAPES, _conv_out, _pow2_at_le
 F32 = _lib.DRNMI_F32
 # TrainRunner default (tests switch it off to compare against the per-layer packs)
 BATCHED_PACK = True
+# BN batch statistics from the conv_x6 epilogue where the launch can write them (tests switch it
+# off to compare against the separate statistics pass over y)
+FUSED_BN_STATS = True
 
 
 def _vp(t):
@@ -73,6 +76,7 @@ class TrainRunner:
         self._red_ws = None
         self._wg_ws = None
         self._cv_ws = None
+        self._st_ws = None
         self._zeros = None
         self.grad_ready = None          # callback(list[Parameter]) after each node's grads land
         self.grad_scale = 1.0           # multiplies dL/dlogprobs (DDP averaging: 1 / world_size)
@@ -241,7 +245,9 @@ class TrainRunner:
         return out
 
     def _conv(self, x, cin_stride, h, w, wpk, k, k_pad, cout_pad, cout, ks, stride, pad, dil, y, y_strides,
-              shift, res, n, ho, wo, stream, what, wx=None, algo=_lib.ALGO_IGEMM):
+              shift, res, n, ho, wo, stream, what, wx=None, algo=_lib.ALGO_IGEMM, want_stats=False):
+        """One drnmi_conv2d_bn_act launch.  want_stats: let a conv_x6 launch write the BN statistics
+        partials of its output (self._st_ws); returns their row count, 0 when it cannot."""
         a = _lib.ConvArgs()
         a.x, a.wgt, a.scale, a.shift = x.data_ptr(), (wx if wx is not None else wpk).data_ptr(), None, shift.data_ptr()
         a.res = res.data_ptr() if res is not None else None
@@ -263,7 +269,13 @@ class TrainRunner:
             if nb > 0:
                 ws = self._ws("_cv_ws", nb, y.device)
                 a.ws, a.ws_bytes = ws.data_ptr(), ws.numel()
+        rows = 0
+        if want_stats and wx is not None and algo == _lib.ALGO_IGEMM:
+            rows = lib.drnmi_conv_stats_rows(ctypes.byref(a))
+            if rows > 0:
+                a.stats = self._ws("_st_ws", 2 * rows * cout * 8, y.device).data_ptr()
         _lib.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(stream)), what)
+        return max(rows, 0)
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, save: bool):
@@ -303,19 +315,26 @@ class TrainRunner:
                 raise NotImplementedError("train path: channel count must be a power of two")
             rows = n * oh * ow
             y = torch.empty(rows, cs, dtype=torch.float32, device=dev)
-            self._conv(vals[nd.src], cs_in, ih, iw, st.wf, st.k, st.k_pad, st.cout_pad, cout, ks, s, p, d,
-                       y, (oh * ow * cs, cs, 1), st.shift, None, n, oh, ow, stream, nd.name, st.wfx,
-                       _lib.ALGO_PATCH if st.patch else _lib.ALGO_IGEMM)
             bn = nd.bn
             if bn.momentum is None or not bn.track_running_stats:
                 raise NotImplementedError("BatchNorm2d with momentum=None / no running stats")
+            # conv_x6 launches write the BN statistics partials in their epilogue (no pass over y)
+            g_rows = self._conv(vals[nd.src], cs_in, ih, iw, st.wf, st.k, st.k_pad, st.cout_pad, cout, ks, s, p,
+                                d, y, (oh * ow * cs, cs, 1), st.shift, None, n, oh, ow, stream, nd.name, st.wfx,
+                                _lib.ALGO_PATCH if st.patch else _lib.ALGO_IGEMM, want_stats=FUSED_BN_STATS)
             mean = torch.empty(cs, dtype=torch.float32, device=dev)
             invstd = torch.empty(cs, dtype=torch.float32, device=dev)
-            ws = self._ws("_red_ws", lib.drnmi_reduce_workspace_bytes(rows, cs), dev)
-            _lib.check(lib.drnmi_bn_stats_f32(_vp(y), rows, cs, float(bn.eps), float(bn.momentum), _vp(mean),
-                                              _vp(invstd), _vp(bn.running_mean), _vp(bn.running_var),
-                                              _vp(bn.num_batches_tracked), _vp(ws), ctypes.c_void_p(stream)),
-                       f"bn_stats {nd.name}")
+            if g_rows > 0:
+                _lib.check(lib.drnmi_bn_stats_partials_f32(
+                    _vp(self._st_ws), g_rows, rows, cs, float(bn.eps), float(bn.momentum), _vp(mean), _vp(invstd),
+                    _vp(bn.running_mean), _vp(bn.running_var), _vp(bn.num_batches_tracked), ctypes.c_void_p(stream)),
+                    f"bn_stats {nd.name}")
+            else:
+                ws = self._ws("_red_ws", lib.drnmi_reduce_workspace_bytes(rows, cs), dev)
+                _lib.check(lib.drnmi_bn_stats_f32(_vp(y), rows, cs, float(bn.eps), float(bn.momentum), _vp(mean),
+                                                  _vp(invstd), _vp(bn.running_mean), _vp(bn.running_var),
+                                                  _vp(bn.num_batches_tracked), _vp(ws), ctypes.c_void_p(stream)),
+                           f"bn_stats {nd.name}")
             for b in (bn.running_mean, bn.running_var, bn.num_batches_tracked):
                 torch.autograd.graph.increment_version(b)
             z = torch.empty(rows, cs, dtype=torch.float32, device=dev)
