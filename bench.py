@@ -656,8 +656,11 @@ def pmc_traffic(args, kernel, precision=None):
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("config") == want and kernel in d.get("kernels", {}):
-            return round(d["kernels"][kernel]["traffic_bytes"]), os.path.relpath(f, here)
+        ks = d.get("kernels", {})
+        # drnmi_conv_kernel_name spells the fp32 igemm's element type "f32"; rocprof demangles "float"
+        for k in (kernel, kernel.replace("<f32,", "<float,")):
+            if d.get("config") == want and k in ks:
+                return round(ks[k]["traffic_bytes"]), os.path.relpath(f, here)
     return None, None
 
 
