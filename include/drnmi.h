@@ -120,6 +120,13 @@ typedef struct drnmi_conv_args {
    * invstd exactly as drnmi_bn_stats_f32 would from y (semantic_seg.py:166-230's train-mode
    * BatchNorm2d after the conv), without reading y again.  NULL: off. */
   double* stats;
+  /* Optional output row stride in elements (F32X3 conv_x6 launches only): y(n, oh, ow, c) =
+   * y[n*y_sn + oh*y_sr + ow*y_sp + c*y_sc]; a residual then has y's layout.  0 = rows packed
+   * (oh*wo*y_sp).  A stride-2 conv's data gradient runs as four of these launches, one per output
+   * parity class, writing every other pixel of every other row (drnmi_dgrad_s2_class_planes).  With
+   * y_sr != 0 the output size is free (ho x wo need not follow the conv formula): taps past the
+   * input's edges read zeros. */
+  int64_t y_sr;
 } drnmi_conv_args;
 
 /* Algorithms behind drnmi_conv2d_bn_act:
@@ -392,6 +399,18 @@ int64_t drnmi_reduce_workspace_bytes(int64_t rows, int32_t channels);
 int drnmi_bn_stats_f32(const float* y, int64_t rows, int32_t C, float eps, float momentum,
                        float* mean, float* invstd, float* running_mean, float* running_var,
                        int64_t* num_batches_tracked, void* ws, void* stream);
+
+/* Weight planes of parity class (a, b) of a stride-2 conv's data gradient (the transpose of
+ * lmodels/drn.py's strided conv3x3 / downsample 1x1 in the fine-tune backward): gathered from the
+ * dgrad's packed bf16 planes `planes` ([3][rows][k_pad], drnmi_pack_conv_weight mode 1 + split3,
+ * k = tap' * kst + co, taps flipped, pad_d = dil*(ks-1) - pad) into `out` [3][rows][k_pad_c] for a
+ * ksc x ksc stride-1 conv of dy: tap (khc, kwc) = flipped tap ((pad_d - a) mod 2 + 2 khc, likewise
+ * for b), zero where the class has fewer taps.  Launch the class conv with F32X3, x = dy, pad 0,
+ * y = dx + (a * W + b) * cs, y_sp = 2 cs, y_sr = 2 W cs, y_sn = H W cs: the four classes together
+ * are bit-identical to the conv of the zero-inserted dy (drnmi_zero_insert_f32).  kst % 8 == 0. */
+int drnmi_dgrad_s2_class_planes(const void* planes, int32_t rows, int32_t k_pad, int32_t kst, int32_t ks,
+                                int32_t pad_d, int32_t a, int32_t b, int32_t ksc, void* out, int32_t k_pad_c,
+                                void* stream);
 
 /* drnmi_bn_stats_f32 from the partial sums a conv epilogue wrote (drnmi_conv_args.stats:
  * [2][G][C] fp64, G = drnmi_conv_stats_rows): the same finalize (mean, biased variance, invstd,

@@ -195,6 +195,33 @@ def test_fused_bn_stats_match_separate_pass(monkeypatch):
         assert TC.rel_err(outs[1][1][k].numpy(), v.numpy()) <= 1e-5, k
 
 
+@pytest.mark.parametrize("arch,shape", [("drn_d_54", (2, 3, 96, 64)), ("drn_d_22", (1, 3, 72, 40))])
+def test_s2_class_dgrad_bit_identical(arch, shape, monkeypatch):
+    """fp32x: the data gradient of every stride-2 conv as four parity-class convs of dy (y_sr
+    strided stores, 2x2 / 1x1 class kernels) is bit-identical to the conv of the zero-inserted dy
+    (3x3 classes with 1x1 .. 2x2 taps, and 1x1 downsamples whose odd classes no tap reaches).
+    Split-K is off in both runs (it re-associates the sums)."""
+    import drnmi.train as T
+    from drnmi.drnseg import DRNSeg
+    from drnmi.weights import synth_state_dict
+    monkeypatch.setattr(T, "X6_SPLIT_K", False)
+    torch.manual_seed(5)
+    x = torch.randn(*shape)
+    t = torch.randint(0, 19, (shape[0], shape[2], shape[3]))
+    outs = []
+    for cls in (False, True):
+        monkeypatch.setattr(T, "S2_CLASS_DGRAD", cls)
+        m = DRNSeg(arch, 19, pretrained=False)
+        m.load_state_dict(synth_state_dict(m, 5))
+        m.set_precision("fp32x")
+        steps = []
+        _run_hip_steps(m, None, [x, x], [t, t], grads_per_step=steps)
+        outs.append(steps)
+    for s0, s1 in zip(*outs):
+        for k in s0:
+            assert torch.equal(s0[k], s1[k]), k
+
+
 def test_eval_after_train_uses_new_weights():
     """Training bumps parameter/buffer versions, so the eval plan repacks (drnseg._state_key)."""
     from drnmi.drnseg import DRNSeg

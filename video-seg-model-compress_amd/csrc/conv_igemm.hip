@@ -321,8 +321,11 @@ extern "C" const char* drnmi_conv_tile_name(int tile) {
 extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
   if (a == nullptr) return DRNMI_EINVAL;
   const drnmi_conv_args& p = *a;
-  // BN-statistics partials come from conv_x6's epilogue only (drnmi_conv_stats_rows)
+  // BN-statistics partials and output row strides: conv_x6 only
   if (p.stats != nullptr && (p.algo != DRNMI_ALGO_IGEMM || x6_conv_stats_rows(p) <= 0)) return DRNMI_EINVAL;
+  if (p.y_sr != 0 && (p.algo != DRNMI_ALGO_IGEMM || p.dtype != DRNMI_F32X3 || p.y_sc != 1 || p.y_sr < 0 ||
+                      !x6_conv_supported(p)))
+    return DRNMI_EINVAL;
   if (p.algo == DRNMI_ALGO_PATCH) {
     if (p.x2 != nullptr) return DRNMI_ENOTSUP;     // fused second input: LDS-DMA kernels only
     if (p.x == nullptr || p.wgt == nullptr || p.y == nullptr || p.shift == nullptr ||
@@ -349,9 +352,11 @@ extern "C" int drnmi_conv2d_bn_act(const drnmi_conv_args* a, void* stream) {
              (p.out_dtype != DRNMI_BF16 && p.out_dtype != DRNMI_F32)) {
     return DRNMI_EINVAL;
   }
-  // Output geometry must be the conv's: ho = (h + 2 pad - dil (ks-1) - 1) / stride + 1.
-  if (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
-      p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1)
+  // Output geometry must be the conv's: ho = (h + 2 pad - dil (ks-1) - 1) / stride + 1 -- except for
+  // the row-strided (y_sr) class launches of a stride-2 data gradient, whose taps past the input's
+  // bottom / right edge read zeros (an asymmetric pad; conv_x6 bounds-checks every tap)
+  if (p.y_sr == 0 && (p.ho != (p.h + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1 ||
+                      p.wo != (p.w + 2 * p.pad - p.dil * (p.ks - 1) - 1) / p.stride + 1))
     return DRNMI_EINVAL;
   if (p.dtype == DRNMI_I8) return i8_conv_dispatch(p, reinterpret_cast<hipStream_t>(stream));   // int8: one kernel family
   if (p.dtype == DRNMI_F32X3) return x6_conv_dispatch(p, reinterpret_cast<hipStream_t>(stream));

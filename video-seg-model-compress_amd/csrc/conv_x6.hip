@@ -363,7 +363,9 @@ conv_x6_kernel(const drnmi_conv_args p) {
     const int m = px0 + wp * 64 + fn * 16 + fr;
     const int n = m / hw_o;
     const int q = m - n * hw_o;
-    ybase_fn[fn] = m < M ? static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp : -1;
+    const int64_t qo = p.y_sr != 0 ? static_cast<int64_t>(q / p.wo) * p.y_sr + static_cast<int64_t>(q % p.wo) * p.y_sp
+                                   : static_cast<int64_t>(q) * p.y_sp;
+    ybase_fn[fn] = m < M ? static_cast<int64_t>(n) * p.y_sn + qo : -1;
   }
   // one (fragment fm, pixel fragment fn) of the lane: v = acc * scale + shift (+ res), ReLU,
   // stored; false when the pixel or the channel group lies outside the output
@@ -391,7 +393,7 @@ conv_x6_kernel(const drnmi_conv_args p) {
       v[3] += sh.w;
     }
     if (res != nullptr) {
-      const float* rp = res + static_cast<int64_t>(m) * p.cout + co;
+      const float* rp = res + (p.y_sr != 0 ? ybase : static_cast<int64_t>(m) * p.cout) + co;   // y_sr: y's layout
       if (full) {
         const float4 rv = *reinterpret_cast<const float4*>(rp);
         v[0] += rv.x;
@@ -504,18 +506,21 @@ __global__ void __launch_bounds__(256) x6_splitk_epilogue_kernel(const drnmi_con
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] += shv[j];
     }
+    const int n = static_cast<int>(m / hw_o);
+    const int q = static_cast<int>(m - static_cast<int64_t>(n) * hw_o);
+    const int64_t ybase = static_cast<int64_t>(n) * p.y_sn +
+                          (p.y_sr != 0 ? static_cast<int64_t>(q / p.wo) * p.y_sr + static_cast<int64_t>(q % p.wo) * p.y_sp
+                                       : static_cast<int64_t>(q) * p.y_sp);
     if (res != nullptr) {
+      const int64_t ro = p.y_sr != 0 ? ybase + co : o;   // y_sr: the residual has y's layout
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (co + j < p.cout) v[j] += res[o + j];
+        if (co + j < p.cout) v[j] += res[ro + j];
     }
     if (p.relu) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
     }
-    const int n = static_cast<int>(m / hw_o);
-    const int q = static_cast<int>(m - static_cast<int64_t>(n) * hw_o);
-    const int64_t ybase = static_cast<int64_t>(n) * p.y_sn + static_cast<int64_t>(q) * p.y_sp;
     if (p.y_sc == 1 && full) {
       *reinterpret_cast<float4*>(y + ybase + co) = make_float4(v[0], v[1], v[2], v[3]);
     } else {
@@ -645,9 +650,10 @@ int64_t x6_workspace_bytes(const drnmi_conv_args& p) {
 
 bool x6_conv_supported(const drnmi_conv_args& p) {
   return p.dtype == DRNMI_F32X3 && p.out_dtype == DRNMI_F32 && p.cin >= kBK && (p.cin & (p.cin - 1)) == 0 &&
-         (p.ks == 1 || p.ks == 3) && p.k == p.ks * p.ks * p.cin && p.k_pad == p.k &&
+         (p.ks == 1 || p.ks == 2 || p.ks == 3) && p.k == p.ks * p.ks * p.cin && p.k_pad == p.k &&
          static_cast<int64_t>(p.n) * p.h * p.w * p.cin < (int64_t(1) << 31) && p.h < 16384 && p.w < 16384 &&
-         (p.y_sc != 1 || p.y_sp == p.cout);
+         (p.y_sc != 1 || p.y_sp == p.cout ||
+          (p.y_sr != 0 && p.y_sp % 4 == 0 && p.y_sr % 4 == 0 && p.y_sn % 4 == 0));
 }
 
 int64_t x6_conv_workspace_bytes(const drnmi_conv_args& p) {
@@ -676,7 +682,15 @@ int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (S > 1 && p.ws_bytes < x6_workspace_bytes(p)) return DRNMI_EINVAL;
   if (S > 1 && (reinterpret_cast<uintptr_t>(p.ws) & 15) != 0) return DRNMI_EINVAL;
   hipError_t e;
-  if (p.ks == 3) {
+  if (p.ks == 2) {        // the 2x2 parity-class kernels of a stride-2 conv's data gradient
+    switch (v) {
+      case 0: e = launch_x6<2, 128, 2, 4>(p, S, s); break;
+      case 1: e = launch_x6<2, 128, 1, 4>(p, S, s); break;
+      case 2: e = launch_x6<2, 64, 1, 4>(p, S, s); break;
+      case 3: e = launch_x6<2, 64, 2, 4>(p, S, s); break;
+      default: e = launch_x6<2, 64, 2, 2>(p, S, s); break;
+    }
+  } else if (p.ks == 3) {
     switch (v) {
       case 0: e = launch_x6<3, 128, 2, 4>(p, S, s); break;
       case 1: e = launch_x6<3, 128, 1, 4>(p, S, s); break;
@@ -704,8 +718,11 @@ const char* x6_conv_name(const drnmi_conv_args& p) {
   static const char* n1[kNumX6] = {"conv_x6_kernel<1, 128, 2, 4>", "conv_x6_kernel<1, 128, 1, 4>",
                                    "conv_x6_kernel<1, 64, 1, 4>", "conv_x6_kernel<1, 64, 2, 4>",
                                    "conv_x6_kernel<1, 64, 2, 2>"};
+  static const char* n2[kNumX6] = {"conv_x6_kernel<2, 128, 2, 4>", "conv_x6_kernel<2, 128, 1, 4>",
+                                   "conv_x6_kernel<2, 64, 1, 4>", "conv_x6_kernel<2, 64, 2, 4>",
+                                   "conv_x6_kernel<2, 64, 2, 2>"};
   const int v = x6_plan(p, p.ws != nullptr).v;
-  return p.ks == 3 ? n3[v] : n1[v];
+  return p.ks == 3 ? n3[v] : p.ks == 2 ? n2[v] : n1[v];
 }
 
 }  // namespace drnmi

@@ -1399,6 +1399,39 @@ static void wgrad_plan(const drnmi_wgrad_args& a, bool big, int* splits, int64_t
   *per = best_pp;
 }
 
+// ------------------------------------------------------------------ stride-2 dgrad parity classes
+// The data gradient of a stride-2 conv is a stride-1 conv of dy zero-inserted to the input grid
+// (zero_insert_kernel below) with the flipped weights: 3/4 of its B rows are zeros.  Split by the
+// parity (a, b) of the output pixel, each class is a dense stride-1 conv of dy itself with the
+// flipped taps kh' = (pad_d - a) mod 2, + 2, ... (kw' likewise), embedded in a KSC x KSC kernel
+// (zero weights where a class has fewer taps in one dimension), written to every other pixel of
+// every other row (drnmi_conv_args.y_sr).  Products with the zero rows were exact zeros: the four
+// class launches are bit-identical to the zero-inserted conv.  This gathers one class's weight
+// planes from the packed dgrad planes ([3][rows][k_pad], k = tap' * kst + co).
+__global__ void __launch_bounds__(kThreads)
+dgrad_class_planes_kernel(const uint4* __restrict__ in, int rows, int k_pad, int kst, int ks, int kh0, int nh, int kw0,
+                          int nw, int ksc, uint4* __restrict__ out, int k_pad_c) {
+  const int c8 = kst / 8;
+  const int64_t per_plane = static_cast<int64_t>(rows) * ksc * ksc * c8;
+  const int64_t total = 3 * per_plane;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int pl = static_cast<int>(i / per_plane);
+    int64_t j = i - pl * per_plane;
+    const int c = static_cast<int>(j % c8);
+    j /= c8;
+    const int tc = static_cast<int>(j % (ksc * ksc));
+    const int r = static_cast<int>(j / (ksc * ksc));
+    const int khc = tc / ksc, kwc = tc - (tc / ksc) * ksc;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (khc < nh && kwc < nw) {
+      const int tap = (kh0 + 2 * khc) * ks + (kw0 + 2 * kwc);
+      v = in[((static_cast<int64_t>(pl) * rows + r) * k_pad + tap * kst) / 8 + c];
+    }
+    out[((static_cast<int64_t>(pl) * rows + r) * k_pad_c + tc * kst) / 8 + c] = v;
+  }
+}
+
 // ------------------------------------------------------------------ zero insert (stride-s dgrad)
 __global__ void __launch_bounds__(kThreads)
 zero_insert_kernel(const float* __restrict__ dy, int n, int ho, int wo, int c4, int s, int hu, int wu,
@@ -1732,6 +1765,23 @@ extern "C" int drnmi_bn_stats_f32(const float* y, int64_t rows, int32_t C, float
   if (e != hipSuccess) return static_cast<int>(e);
   hipLaunchKernelGGL(bn_stats_final_kernel, dim3(fin_grid(C)), dim3(kThreads), 0, s, r.ws, r.G, C, rows, eps,
                      momentum, mean, invstd, running_mean, running_var, num_batches_tracked);
+  return static_cast<int>(hipGetLastError());
+}
+
+extern "C" int drnmi_dgrad_s2_class_planes(const void* planes, int32_t rows, int32_t k_pad, int32_t kst, int32_t ks,
+                                           int32_t pad_d, int32_t a, int32_t b, int32_t ksc, void* out, int32_t k_pad_c,
+                                           void* stream) {
+  if (planes == nullptr || out == nullptr || rows <= 0 || ks <= 0 || ksc <= 0 || kst <= 0 || kst % 8 != 0 ||
+      k_pad % 8 != 0 || k_pad < ks * ks * kst || k_pad_c != ksc * ksc * kst || (a != 0 && a != 1) || (b != 0 && b != 1) ||
+      ((reinterpret_cast<uintptr_t>(planes) | reinterpret_cast<uintptr_t>(out)) & 15))
+    return DRNMI_EINVAL;
+  const int kh0 = ((pad_d - a) % 2 + 2) % 2, kw0 = ((pad_d - b) % 2 + 2) % 2;
+  const int nh = kh0 < ks ? (ks - kh0 + 1) / 2 : 0, nw = kw0 < ks ? (ks - kw0 + 1) / 2 : 0;
+  if (nh > ksc || nw > ksc) return DRNMI_EINVAL;
+  const int64_t total = 3LL * rows * ksc * ksc * (kst / 8);
+  hipLaunchKernelGGL(dgrad_class_planes_kernel, dim3(grid_of(total)), dim3(kThreads), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const uint4*>(planes), rows, k_pad, kst,
+                     ks, kh0, nh, kw0, nw, ksc, reinterpret_cast<uint4*>(out), k_pad_c);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -45,6 +45,7 @@ class ConvArgs(ctypes.Structure):
         ("cin2", ctypes.c_int32), ("h2", ctypes.c_int32), ("w2", ctypes.c_int32), ("stride2", ctypes.c_int32),
         ("ws", ctypes.c_void_p), ("ws_bytes", ctypes.c_int64),
         ("stats", ctypes.c_void_p),
+        ("y_sr", ctypes.c_int64),
     ]
 
 
@@ -105,6 +106,8 @@ SIGNATURES = {
     "drnmi_conv_wgrad_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(WgradArgs)]),
     "drnmi_conv_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(ConvArgs)]),
     "drnmi_conv_stats_rows": (ctypes.c_int64, [ctypes.POINTER(ConvArgs)]),
+    "drnmi_dgrad_s2_class_planes": (ctypes.c_int, [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _VP, _I32,
+                                                   _VP]),
     "drnmi_bn_stats_partials_f32": (ctypes.c_int, [_VP, _I64, _I64, _I32, _F32, _F32, _VP, _VP, _VP, _VP, _VP, _VP]),
     "drnmi_conv_wgrad_f32": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),
     "drnmi_conv_wgrad_f32x3": (ctypes.c_int, [ctypes.POINTER(WgradArgs), _VP]),

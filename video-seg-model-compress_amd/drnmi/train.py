@@ -43,6 +43,12 @@ BATCHED_PACK = True
 # BN batch statistics from the conv_x6 epilogue where the launch can write them (tests switch it
 # off to compare against the separate statistics pass over y)
 FUSED_BN_STATS = True
+# fp32x data gradient of a stride-2 conv as four parity-class convs of dy (tests switch it off to
+# compare against the zero-inserted conv, which it reproduces bit for bit when neither splits K)
+S2_CLASS_DGRAD = True
+# conv_x6 training launches may split K where their tiles leave CUs idle (tests switch it off for
+# bit-for-bit comparisons of launch forms: a split sums the same products in another association)
+X6_SPLIT_K = True
 
 
 def _vp(t):
@@ -53,12 +59,13 @@ class _NodeState:
     """Per-node packed weights (forward / dgrad layouts) cached across steps."""
 
     __slots__ = ("wf", "wd", "wfx", "wdx", "k", "k_pad", "cout_pad", "kd", "kd_pad", "rows_d", "shift", "patch",
-                 "dpatch", "dys")
+                 "dpatch", "dys", "s2_step", "s2_cls", "s2_planes")
 
     def __init__(self):
         self.wf = self.wd = self.wfx = self.wdx = self.shift = None
         self.patch = self.dpatch = False
         self.dys = None
+        self.s2_step = self.s2_cls = self.s2_planes = None   # stride-2 dgrad parity classes (per step)
 
 
 class TrainRunner:
@@ -77,6 +84,7 @@ class TrainRunner:
         self._wg_ws = None
         self._cv_ws = None
         self._st_ws = None
+        self._step_id = 0               # backward passes run (keys the per-step stride-2 class planes)
         self._zeros = None
         self.grad_ready = None          # callback(list[Parameter]) after each node's grads land
         self.grad_scale = 1.0           # multiplies dL/dlogprobs (DDP averaging: 1 / world_size)
@@ -186,6 +194,48 @@ class TrainRunner:
         st.wdx = self._split(st.wd, dys, st.kd, st.kd_pad, patch=st.dpatch, out=st.wdx)
         return dys
 
+    def _s2_classes(self, nd, st, device, stream):
+        """The parity classes of a stride-2 conv's data gradient in fp32x (drnmi_dgrad_s2_class_planes):
+        [(a, b, ksc, planes)] for the classes some tap reaches, their weight planes gathered from this
+        step's packed dgrad planes; None when the layer keeps the zero-insert path (not conv_x6, a
+        dilated conv, or a class whose taps would start above its pixel).  Cached per step."""
+        if st.s2_step == self._step_id:
+            return st.s2_cls
+        st.s2_step, st.s2_cls = self._step_id, None
+        cout, cin, ks, _ = nd.conv.weight.shape
+        p, d = nd.conv.padding[0], nd.conv.dilation[0]
+        dys = self._pack_dgrad(nd, st, device, stream)
+        if st.wdx is None or st.dpatch or d != 1 or dys % 8 != 0 or st.kd != st.kd_pad:
+            return None
+        pad_d = d * (ks - 1) - p
+        parts = []
+        for a_ in (0, 1):
+            k0 = (pad_d - a_) % 2
+            nh = (ks - k0 + 1) // 2 if k0 < ks else 0
+            if nh and (a_ - pad_d + k0) // 2 != 0:       # the class conv would need a nonzero pad
+                return None
+            parts.append((k0, nh))
+        lib = _lib.load()
+        cls = []
+        cache = st.s2_planes or {}
+        for a_ in (0, 1):
+            for b_ in (0, 1):
+                nh, nw = parts[a_][1], parts[b_][1]
+                if nh == 0 or nw == 0:
+                    continue
+                ksc = max(nh, nw)
+                kpc = ksc * ksc * dys
+                buf = cache.get((a_, b_))
+                if buf is None or buf.shape != (3, st.rows_d, kpc):
+                    buf = torch.empty(3, st.rows_d, kpc, dtype=torch.bfloat16, device=device)
+                    cache[(a_, b_)] = buf
+                _lib.check(lib.drnmi_dgrad_s2_class_planes(_vp(st.wdx), st.rows_d, st.kd_pad, dys, ks, pad_d, a_, b_,
+                                                           ksc, _vp(buf), kpc, stream), f"dgrad classes {nd.name}")
+                cls.append((a_, b_, ksc, buf))
+        st.s2_planes = cache
+        st.s2_cls = cls
+        return cls
+
     def _batched_pack(self, device, stream) -> bool:
         """Re-pack every forward and dgrad weight (and fp32x planes) of the network in one launch
         (drnmi_pack_conv_weights_batched), bit-identical to the per-layer calls.  Needs the buffers
@@ -245,7 +295,8 @@ class TrainRunner:
         return out
 
     def _conv(self, x, cin_stride, h, w, wpk, k, k_pad, cout_pad, cout, ks, stride, pad, dil, y, y_strides,
-              shift, res, n, ho, wo, stream, what, wx=None, algo=_lib.ALGO_IGEMM, want_stats=False):
+              shift, res, n, ho, wo, stream, what, wx=None, algo=_lib.ALGO_IGEMM, want_stats=False, y_sr=0,
+              split=True):
         """One drnmi_conv2d_bn_act launch.  want_stats: let a conv_x6 launch write the BN statistics
         partials of its output (self._st_ws); returns their row count, 0 when it cannot."""
         a = _lib.ConvArgs()
@@ -253,6 +304,7 @@ class TrainRunner:
         a.res = res.data_ptr() if res is not None else None
         a.y = y.data_ptr()
         a.y_sn, a.y_sp, a.y_sc = y_strides
+        a.y_sr = y_sr
         a.n, a.h, a.w, a.cin = n, h, w, cin_stride
         a.ho, a.wo, a.cout, a.cout_pad = ho, wo, cout, cout_pad
         a.ks, a.stride, a.pad, a.dil = ks, stride, pad, dil
@@ -263,7 +315,7 @@ class TrainRunner:
             a.dtype = _lib.DRNMI_F32X3           # fp32x: conv_x6 (fp32 in/out, bf16 weight planes)
         a.tile, a.algo = -1, algo
         lib = _lib.load()
-        if wx is not None and algo == _lib.ALGO_IGEMM:
+        if wx is not None and algo == _lib.ALGO_IGEMM and split and X6_SPLIT_K:
             # split-K scratch for the launches whose tiles would leave CUs idle (the 1/8-res layers)
             nb = lib.drnmi_conv_workspace_bytes(ctypes.byref(a))
             if nb > 0:
@@ -364,6 +416,7 @@ class TrainRunner:
     # ------------------------------------------------------------------ backward
     def backward(self, saved, logprobs, logits, g_lp, g_logits):
         lib = _lib.load()
+        self._step_id += 1
         dev = logprobs.device
         stream = _lib.stream_ptr(dev)
         sp = ctypes.c_void_p(stream)
@@ -465,7 +518,30 @@ class TrainRunner:
             if self.grad_ready is not None and done:
                 self.grad_ready(done)
             # data gradient (not needed for the network input)
-            if nd.src != "input":
+            if nd.src != "input" and s == 2 and S2_CLASS_DGRAD and self._s2_classes(nd, st, dev, sp) is not None:
+                # stride 2: four parity-class convs of dy itself, no zero-inserted copy
+                cs_src = self.cstride[nd.src]
+                prev = grads.get(nd.src)
+                classes = self._s2_classes(nd, st, dev, sp)
+                if prev is not None:
+                    out = prev
+                elif len(classes) < 4:          # pixels no tap reaches keep a zero gradient
+                    out = torch.zeros(n * ih * iw, cs_src, dtype=torch.float32, device=dev)
+                else:
+                    out = torch.empty(n * ih * iw, cs_src, dtype=torch.float32, device=dev)
+                flat = out.view(-1)
+                for (a_, b_, ksc, planes) in classes:
+                    ho_c, wo_c = (ih - a_ + 1) // 2, (iw - b_ + 1) // 2
+                    if ho_c <= 0 or wo_c <= 0:
+                        continue
+                    base = (a_ * iw + b_) * cs_src
+                    view = flat[base:]
+                    self._conv(dy, dys, oh, ow, None, ksc * ksc * dys, ksc * ksc * dys, st.rows_d, cin, ksc, 1, 0,
+                               1, view, (ih * iw * cs_src, 2 * cs_src, 1), self._zeros_f32(st.rows_d, dev),
+                               view if prev is not None else None, n, ho_c, wo_c, stream,
+                               f"dgrad {nd.name} class {a_}{b_}", planes, y_sr=2 * iw * cs_src, split=False)
+                grads[nd.src] = out
+            elif nd.src != "input":
                 dys_d = self._pack_dgrad(nd, st, dev, sp)
                 assert dys_d == dys
                 cs_src = self.cstride[nd.src]
