@@ -13,6 +13,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 TILES = [int(t) for t in os.environ.get("TILES", "4,5,6,16,17").split(",")]
 SHAPES = [  # name, cin, cout, ks, stride, dil, H(in), W(in), residual
     ("l8 512x512 d1", 512, 512, 3, 1, 1, 128, 256, False),
+    ("l7 512x512 d2", 512, 512, 3, 1, 2, 128, 256, False),
     ("l6 512x512 d4 +res", 512, 512, 3, 1, 4, 128, 256, True),
     ("l6 512x512 d4 nores", 512, 512, 3, 1, 4, 128, 256, False),
     ("l6.0c1 256->512 d4", 256, 512, 3, 1, 4, 128, 256, False),
