@@ -356,11 +356,11 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
         names[plan.seg_fused["conv"]] = "conv_i8_stag_seg_kernel" if plan.seg_fused["i8"] else "conv_stag_seg_kernel"
         names[plan.seg_idx] = ""
     # the head launch (index len(nodes), DRNSeg._segment_impl): up x8 + argmax -> uint8 labels
-    # (ops.hip drnmi_up8_labels_seg2 / _seg2_i8 / _nhwc launch the uniform-block fast kernel; NCHW
+    # (ops.hip drnmi_up8_labels_seg2 / _seg2_i8 / _nhwc launch the tiled uniform-window kernel; NCHW
     # logits the oct kernel)
     i8_head = path == "seg2" and plan.seg_fused["i8"]
-    names.append({"seg2": "up8_labels_fast_kernel<19, U8, SEG2%s>" % ("_I8" if i8_head else ""),
-                  "nhwc": "up8_labels_fast_kernel<19, U8, NHWC>"}.get(path, "up8_labels_oct_kernel<19, U8>"))
+    names.append({"seg2": "up8_labels_tile_kernel<19, U8, SEG2%s>" % ("_I8" if i8_head else ""),
+                  "nhwc": "up8_labels_tile_kernel<19, U8, NHWC>"}.get(path, "up8_labels_oct_kernel<19, U8>"))
     nodes = plan.packed.graph.nodes
     # per-launch work (roofline.launch_work): a folded downsample's FLOPs and input run inside its
     # block's last conv, the fused stem launch carries layer1; useful work of a pruned layer

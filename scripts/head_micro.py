@@ -1,5 +1,5 @@
 """Labels-only head on the D-22 batch-8 logits shape (8 x 128 x 256 x 20 fp32 NHWC rows -> 8 x 1024 x
-2048 uint8 labels): per-launch time of the NHWC head (up8_labels_fast_kernel) and of the NCHW oct
+2048 uint8 labels): per-launch time of the NHWC head (up8_labels_tile_kernel) and of the NCHW oct
 head on the same logits, the share of 2 x 2 tap windows the fast path takes, and a label checksum.
 LOGITS=random (i.i.d. normal logits: no uniform windows) or network (the bf16 D-22 seg logits of 8
 random frames, as bench.py's).  python scripts/head_micro.py"""

@@ -54,7 +54,7 @@ def test_labels_nhwc_match_nchw_head(shape, ldt):
 
 def _smooth_logits(n, h, w, seed):
     """Spatially smooth logits (bilinearly enlarged coarse noise): large same-argmax regions, the
-    fast path of up8_labels_fast_kernel, with engineered top-2 margins around its guard."""
+    fast path of up8_labels_tile_kernel, with engineered top-2 margins around its guard."""
     import torch.nn.functional as F
     g = torch.Generator().manual_seed(seed)
     coarse = torch.randn(n, 19, h // 6 + 2, w // 6 + 2, generator=g) * 4
@@ -75,7 +75,7 @@ def _smooth_logits(n, h, w, seed):
 @pytest.mark.parametrize("up", ["bilinear", "random", "negative"])
 @pytest.mark.parametrize("seg2", [False, True])
 def test_labels_fast_path_identical(shape, up, seg2):
-    """up8_labels_fast_kernel (NHWC / SEG2 entry points): blocks whose 4 taps share an argmax with a
+    """up8_labels_tile_kernel (NHWC / SEG2 entry points): windows whose 4 taps share an argmax with a
     margin above the guard are written without per-pixel work; labels must equal the oct head's
     (NCHW) bit for bit, with margins engineered around the guard, non-bilinear up weights and a
     negative weight (which disables the fast path)."""
@@ -113,6 +113,43 @@ def test_labels_fast_path_identical(shape, up, seg2):
         nhwc[..., :19] = lg.permute(0, 2, 3, 1)
         _lib.check(lib.drnmi_up8_logsoftmax_argmax(lg.data_ptr(), upw.data_ptr(), None, a.data_ptr(), _lib.DRNMI_U8,
                                                    n, 19, h, w, st), "nchw head")
+        _lib.check(lib.drnmi_up8_labels_nhwc(nhwc.data_ptr(), cs, upw.data_ptr(), b.data_ptr(), _lib.DRNMI_U8,
+                                             n, 19, h, w, st), "nhwc head")
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), f"{int((a != b).sum())} labels differ"
+
+
+@pytest.mark.parametrize("amp", [3e-5, 1e-3, 0.05])
+@pytest.mark.parametrize("seg2", [False, True])
+def test_labels_candidate_pruning_identical(amp, seg2):
+    """The slow blocks' candidate-class pruning (a class is skipped when its largest tap logit sits a
+    guard below the best smallest one, up8_labels_tile_kernel): labels equal the oct head's bit for
+    bit when the logits are compressed so that margins between classes are near the 2^-16 tie rule
+    and the pruning guard (amp 3e-5: most blocks tie or nearly tie; 1e-3 / 0.05: a few candidates per
+    block, some classes close to the threshold)."""
+    import torch.nn.functional as F
+    n, h, w = 2, 24, 40
+    g = torch.Generator().manual_seed(int(amp * 1e6) + (7 if seg2 else 0))
+    coarse = torch.randn(n, 19, h // 4 + 2, w // 4 + 2, generator=g)
+    logits = (F.interpolate(coarse, size=(h, w), mode="bilinear", align_corners=True) * amp).contiguous()
+    upw = _up_plane()
+    cs = 20
+    lib = _lib.load()
+    st = ctypes.c_void_p(_lib.stream_ptr())
+    a = torch.empty(n, 8 * h, 8 * w, dtype=torch.uint8, device=DEV)
+    b = torch.empty_like(a)
+    lg = logits.to(DEV)
+    _lib.check(lib.drnmi_up8_logsoftmax_argmax(lg.data_ptr(), upw.data_ptr(), None, a.data_ptr(), _lib.DRNMI_U8,
+                                               n, 19, h, w, st), "nchw head")
+    if seg2:   # partial 0 = 0, bias = 0: the SEG2 sum (0 + 0) + p1 is p1 exactly
+        parts = torch.zeros(2, n, h, w, cs, device=DEV)
+        parts[1, ..., :19] = lg.permute(0, 2, 3, 1)
+        bias = torch.zeros(cs, device=DEV)
+        _lib.check(lib.drnmi_up8_labels_seg2(parts.data_ptr(), cs, bias.data_ptr(), upw.data_ptr(), b.data_ptr(),
+                                             _lib.DRNMI_U8, n, 19, h, w, st), "seg2 head")
+    else:
+        nhwc = torch.zeros(n, h, w, cs, device=DEV)
+        nhwc[..., :19] = lg.permute(0, 2, 3, 1)
         _lib.check(lib.drnmi_up8_labels_nhwc(nhwc.data_ptr(), cs, upw.data_ptr(), b.data_ptr(), _lib.DRNMI_U8,
                                              n, 19, h, w, st), "nhwc head")
     torch.cuda.synchronize()

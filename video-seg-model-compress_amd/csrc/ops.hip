@@ -326,6 +326,68 @@ __device__ __forceinline__ void oct_row_labels(const float (&s00)[NC], const flo
   }
 }
 
+// oct_row_labels over a candidate subset of the classes (bit k of cm), the four taps' class-k
+// logits read from LDS rows tp00[k] .. tp11[k].  The caller guarantees (up8_labels_tile_kernel,
+// candidate pruning) that every class outside cm sits more than 2^-16 below the best class at every pixel of
+// the block, so the argmax over cm, in class order, is oct_row_labels' argmax whenever the top two
+// candidates are >= 2^-16 apart; returns false (no labels) when a pixel's top two are closer, and
+// the caller runs the full row.  Same per-class arithmetic as oct_row_labels.
+template <int NC>
+__device__ __forceinline__ bool oct_row_labels_cand(const float* tp00, const float* tp01, const float* tp10,
+                                                    const float* tp11, uint32_t cm, const float* wk, int ky1, int kx1_0,
+                                                    int (&arg)[4]) {
+  const int ky0 = ky1 + 8;
+  f32x2_t w00[2], w01[2], w10[2], w11[2];
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int kx1 = kx1_0 + 2 * pp + e, kx0 = kx1 + 8;
+      w00[pp][e] = wk[ky0 * 16 + kx0];
+      w01[pp][e] = wk[ky0 * 16 + kx1];
+      w10[pp][e] = wk[ky1 * 16 + kx0];
+      w11[pp][e] = wk[ky1 * 16 + kx1];
+    }
+  float best[4], second[4];
+  int am[4];
+  const int k0 = __builtin_ctz(cm);
+  bool first = true;
+  while (cm != 0) {
+    const int k = __builtin_ctz(cm);
+    cm &= cm - 1;
+    const float a00 = tp00[k], a01 = tp01[k], a10 = tp10[k], a11 = tp11[k];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      f32x2_t v = f32x2_t{a00, a00} * w00[pp];
+      v = __builtin_elementwise_fma(f32x2_t{a01, a01}, w01[pp], v);
+      v = __builtin_elementwise_fma(f32x2_t{a10, a10}, w10[pp], v);
+      v = __builtin_elementwise_fma(f32x2_t{a11, a11}, w11[pp], v);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int px = 2 * pp + e;
+        const float x = v[e];
+        if (first) {
+          best[px] = x;
+          second[px] = -INFINITY;
+          am[px] = k0;
+        } else {
+          am[px] = x > best[px] ? k : am[px];
+          second[px] = __builtin_amdgcn_fmed3f(best[px], second[px], x);
+          best[px] = fmaxf(best[px], x);
+        }
+      }
+    }
+    first = false;
+  }
+  bool ok = true;
+#pragma unroll
+  for (int px = 0; px < 4; ++px) {
+    ok = ok && !(best[px] - second[px] < 0x1p-16f);
+    arg[px] = am[px];
+  }
+  return ok;
+}
+
 template <int LABEL_DTYPE>
 __device__ __forceinline__ void store_labels4(void* labels, int64_t pix, const int (&arg)[4]) {
   if (LABEL_DTYPE == DRNMI_U8) {
@@ -437,182 +499,213 @@ up8_labels_oct_kernel(const float* __restrict__ logits, const float* __restrict_
   }
 }
 
-// Labels-only head with a uniform-block fast path (the NHWC / SEG2 logits of DRNSeg.segment).
-// Thread q of row block i1 owns the 8 x 4 output pixels whose 4 taps are the low-res pixels
-// (i1 - 1 .. i1, j1 - 1 .. j1), as in up8_labels_oct_kernel.  When the 4 taps are inside the image
-// and share their argmax c with a top-2 margin of at least
+// Labels-only head with a uniform-window fast path (the NHWC / SEG2 / int8-SEG2 logits of
+// DRNSeg.segment).  A workgroup owns TI x TJ tap windows (i1, j1) -- window = the 8 x 8 output
+// pixels whose taps are the 1/8-res pixels (i1 - 1 .. i1, j1 - 1 .. j1), as in the oct kernel --
+// and reads and summarises each of its 1/8-res pixels once.
+// Fast path: when the 4 taps are inside the image and share their argmax c with a top-2 margin of
+// at least
 //     guard = 2^-16 / min_phase(sum w) * (1 + 2^-10) + 2^-20 * max_t |L_t[c]|
-// (up-sampling weights all >= 0), every up-sampled logit vector of the block has c on top by more
+// (up-sampling weights all >= 0), every up-sampled logit vector of the window has c on top by more
 // than 2^-16: v_c - v_k = sum_t w_t (L_t[c] - L_t[k]) >= min(margin) sum_t w_t, and the computed
 // values (one mul + 3 fma, each rounding <= 2^-24 of a partial sum bounded by sum_t w_t |L_t[k]|
 // <= sum_t w_t (|L_t[c]| + L_t[c] - L_t[k])) lose less than 2^-21 (2 max|L_t[c]| sum w + the
-// margin term) -- so the oct kernel's arithmetic would return c for all 32 pixels without its
-// near-tie fallback, and the block's labels are written without any per-pixel work.  The other
-// threads' blocks (borders, mixed argmax, small margins: ~21 % on the headline frames) are
-// compacted per wave: their taps go to LDS and all 64 lanes share their 8 x (4-pixel row) tasks,
-// each computed by oct_row_labels -- the oct kernel's arithmetic, so the labels are identical.
-// SRC: 0 = fp32 NHWC rows, 1 = two fp32 partial planes + bias (SEG2), 2 = two int32 partial planes
-// + the int8 seg conv's scale / shift (int8 nets)
+// margin term) -- so the oct kernel's arithmetic would return c for all 64 pixels without its
+// near-tie fallback, and the window's labels are written without any per-pixel work (~79 % of the
+// windows on the headline frames).
+//   1. its (TI + 1) x (TJ + 1) 1/8-res pixels: logit vector (the entry point's sum, as
+//      load_taps_nhwc / load_taps_seg2_i8) to LDS, plus the per-tap summary (argmax, top-2 margin
+//      from a med3 chain, |best|, all classes finite);
+//   2. one window per thread: the fast path's test (interior, one argmax, margin above the guard)
+//      on the four summaries, in the same float operations; a passing window's 64 labels are
+//      written at once; the others go to a slow list, with their candidate classes (a class whose
+//      largest tap logit sits a guard below the best smallest one can neither win nor come within
+//      2^-16 of the winner anywhere in the window: oct_row_labels_cand);
+//   3. the slow windows' 16 tasks (8 rows x 2 four-pixel halves) over all threads:
+//      oct_row_labels_cand where it decides, else oct_row_labels -- the oct kernel's arithmetic.
+//      Border windows (a tap outside the image, zero weight) read their clamped taps from global
+//      memory exactly as the oct kernel does.
+// Labels are identical to the oct kernel's (test_gpu_head_nhwc.py).  Measured on the bench's network
+// logits (scripts/head_micro.py, profiles/r9_head): SEG2 68.5 -> 40.4 us, NHWC 63.5 -> 35.8 us
+// against the per-block form this replaced (each 8 x 4 block re-read and re-summarised its taps).
+constexpr int kHeadTI = 8, kHeadTJ = 32;             // TI x TJ = 256 windows = one per thread
 template <int NC, int LABEL_DTYPE, int SRC>
 __global__ void __launch_bounds__(256)
-up8_labels_fast_kernel(const void* __restrict__ logits, const float* __restrict__ up_w, void* __restrict__ labels,
+up8_labels_tile_kernel(const void* __restrict__ logits, const float* __restrict__ up_w, void* __restrict__ labels,
                        int h, int w, int cs, const float* __restrict__ bias, const float* __restrict__ scale) {
-  constexpr int TF = 4 * NC;                         // tap floats per compacted block
-  static_assert(TF % 4 == 0, "16-B tap rows");
+  constexpr int TI = kHeadTI, TJ = kHeadTJ, PJ = TJ + 1, NPX = (TI + 1) * PJ;
+  constexpr int VS = (NC + 3) / 4 * 4;               // LDS floats per pixel vector (16-B rows)
+  static_assert(TI * TJ == 256, "one window per thread");
   __shared__ float wk[256];
-  __shared__ float wstat[2];                         // min over the 64 phases of sum w (0 if any w < 0), max sum w
-  __shared__ __attribute__((aligned(16))) float taps[4][64][TF];
-  __shared__ unsigned char slist[4][64];
+  __shared__ float wstat[1];
+  __shared__ __attribute__((aligned(16))) float vec[NPX][VS];
+  __shared__ float smarg[NPX], sabsb[NPX];
+  __shared__ int sam[NPX];                           // argmax | 0x100 when every class is finite
+  __shared__ int nslow;
+  __shared__ unsigned short slist[256];
+  __shared__ uint32_t scm[256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   wk[tid] = up_w[tid];
+  if (tid == 0) nslow = 0;
   __syncthreads();
-  if (wave == 0) {                                   // phase (ky1, kx1) = (lane >> 3, lane & 7)
+  if (wave == 0) {                                   // min over the 64 phases of sum w (0 if any w < 0)
     const int ky1 = lane >> 3, kx1 = lane & 7;
     const float a = wk[(ky1 + 8) * 16 + kx1 + 8], b = wk[(ky1 + 8) * 16 + kx1], c = wk[ky1 * 16 + kx1 + 8],
                 d = wk[ky1 * 16 + kx1];
-    float lo = fminf(fminf(a, b), fminf(c, d)) < 0.f ? 0.f : (a + b) + (c + d), hi = (a + b) + (c + d);
+    float lo = fminf(fminf(a, b), fminf(c, d)) < 0.f ? 0.f : (a + b) + (c + d);
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      lo = fminf(lo, __shfl_xor(lo, o));
-      hi = fmaxf(hi, __shfl_xor(hi, o));
-    }
-    if (lane == 0) {
-      wstat[0] = lo;
-      wstat[1] = hi;
-    }
+    for (int o = 32; o >= 1; o >>= 1) lo = fminf(lo, __shfl_xor(lo, o));
+    if (lane == 0) wstat[0] = lo;
   }
-  __syncthreads();
-
   const int H = h * 8, W = w * 8;
-  const int qb = blockIdx.x * blockDim.x;
-  const int q = qb + tid;
-  const int i1 = blockIdx.y, i0 = i1 - 1;
+  const int I0 = blockIdx.y * TI, J0 = blockIdx.x * TJ;
   const int n = blockIdx.z;
-  const bool active = 4 * q < W;                     // (no early return: the wave compacts together)
   const int64_t plane = static_cast<int64_t>(h) * w;
   const int64_t HW = static_cast<int64_t>(H) * W;
   const int64_t half = static_cast<int64_t>(gridDim.z) * plane * cs;
-  auto geom = [&](int qq, int& j1, bool& vi0, bool& vi1, bool& vj0, bool& vj1) {
-    j1 = (qq + 1) >> 1;
-    vi0 = i0 >= 0;
-    vi1 = i1 < h;
-    vj0 = j1 - 1 >= 0;
-    vj1 = j1 < w;
-  };
-  int j1;
-  bool vi0, vi1, vj0, vj1;
-  geom(active ? q : qb, j1, vi0, vi1, vj0, vj1);
-  const int ci0 = vi0 ? i0 : 0, ci1 = vi1 ? i1 : 0, cj0 = vj0 ? j1 - 1 : 0, cj1 = vj1 ? j1 : 0;
-  float s[4][NC];
-  const int ty[4] = {ci0, ci0, ci1, ci1}, tx[4] = {cj0, cj1, cj0, cj1};
   constexpr int NCP = (NC + 3) / 4 * 4;
-  float bv[NCP], sv[NCP];                            // per-class bias / shift and scale, loaded once
+  auto load_px = [&](int iy, int ix, float (&d)[NC]) {
+    float bv[NCP], sv[NCP];
 #pragma unroll
-  for (int k = 0; k < NCP; ++k) {
-    bv[k] = SRC != 0 ? bias[k] : 0.f;
-    sv[k] = SRC == 2 ? scale[k] : 0.f;
-  }
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
+    for (int k = 0; k < NCP; ++k) {
+      bv[k] = SRC != 0 ? bias[k] : 0.f;
+      sv[k] = SRC == 2 ? scale[k] : 0.f;
+    }
     if constexpr (SRC == 2)
       load_taps_seg2_i8<NC>(static_cast<const int*>(logits) + static_cast<int64_t>(n) * plane * cs, half, w, cs, sv, bv,
-                            ty[t], tx[t], s[t]);
+                            iy, ix, d);
     else
-      load_taps_nhwc<NC, SRC == 1>(static_cast<const float*>(logits) + static_cast<int64_t>(n) * plane * cs, half, w, cs,
-                                   bv, ty[t], tx[t], s[t]);
-  }
+      load_taps_nhwc<NC, SRC == 1>(static_cast<const float*>(logits) + static_cast<int64_t>(n) * plane * cs, half, w,
+                                   cs, bv, iy, ix, d);
+  };
 
-  // ---- fast path: one argmax shared by the 4 taps with a margin above the guard
-  int cls = 0;
-  float mmin = INFINITY, amax = 0.f, vmaxabs = 0.f;   // vmaxabs: NaN / inf taps keep the block off the fast path
-  bool same = true;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    float best = s[t][0], second = -INFINITY;
+  // ---- 1. the tile's 1/8-res pixels (tap rows I0 - 1 .. I0 + TI - 1, columns J0 - 1 .. J0 + TJ - 1)
+  for (int px = tid; px < NPX; px += 256) {
+    const int iy = I0 - 1 + px / PJ, ix = J0 - 1 + px % PJ;
+    if (iy < 0 || iy >= h || ix < 0 || ix >= w) continue;   // only border windows use them (from global)
+    float v[NC];
+    load_px(iy, ix, v);
+    // the per-tap summary: argmax, top-2 margin (running top-2, one v_med3 per class), |best|, finite
+    float best = v[0], second = -INFINITY, vmaxabs = fabsf(v[0]);
     int am = 0;
-    vmaxabs = fmaxf(vmaxabs, fabsf(s[t][0]));
 #pragma unroll
     for (int k = 1; k < NC; ++k) {
-      const float x = s[t][k];
+      const float x = v[k];
       am = x > best ? k : am;
       second = __builtin_amdgcn_fmed3f(best, second, x);
       best = fmaxf(best, x);
       vmaxabs = __builtin_isnan(x) ? INFINITY : fmaxf(vmaxabs, fabsf(x));
     }
-    vmaxabs = __builtin_isnan(s[t][0]) ? INFINITY : vmaxabs;
-    if (t == 0) cls = am;
-    same = same && am == cls;
-    mmin = fminf(mmin, best - second);
-    amax = fmaxf(amax, fabsf(best));
-  }
-  const float wmin = wstat[0];
-  const bool fast = active && vi0 && vi1 && vj0 && vj1 && same && wmin > 0.f && vmaxabs < INFINITY &&
-                    mmin >= 0x1p-16f / wmin * (1.f + 0x1p-10f) + 0x1p-20f * amax;
-  if (fast) {
-    const int oy0 = 8 * i1 - 4;                      // interior block: all 8 rows exist
-    const int la[4] = {cls, cls, cls, cls};
+    vmaxabs = __builtin_isnan(v[0]) ? INFINITY : vmaxabs;
+    smarg[px] = best - second;
+    sabsb[px] = fabsf(best);
+    sam[px] = am | (vmaxabs < INFINITY ? 0x100 : 0);
+    float4* dst = reinterpret_cast<float4*>(vec[px]);
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
-      store_labels4<LABEL_DTYPE>(labels, static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy0 + r) * W + 4 * q, la);
+    for (int i = 0; i < VS / 4; ++i)
+      dst[i] = make_float4(4 * i < NC ? v[4 * i] : 0.f, 4 * i + 1 < NC ? v[4 * i + 1] : 0.f,
+                           4 * i + 2 < NC ? v[4 * i + 2] : 0.f, 4 * i + 3 < NC ? v[4 * i + 3] : 0.f);
   }
+  __syncthreads();
 
-  // ---- the other blocks: taps to LDS (compacted per wave), then 8 row tasks per block over all lanes
-  const bool slow = active && !fast;
-  const uint64_t sm = __ballot(slow);
-  const int nslow = __popcll(sm);
-  const int mypos = __popcll(sm & ((uint64_t(1) << lane) - 1));
-  if (slow) {
-    const int pos = mypos;
-    slist[wave][pos] = static_cast<unsigned char>(lane);
-    float4* dst = reinterpret_cast<float4*>(taps[wave][pos]);
+  // ---- 2. one window per thread
+  const float wmin = wstat[0];
+  {
+    const int ti = tid / TJ, tj = tid % TJ;
+    const int i1 = I0 + ti, j1 = J0 + tj;
+    if (i1 <= h && j1 <= w) {
+      const bool interior = i1 >= 1 && i1 < h && j1 >= 1 && j1 < w;
+      bool fast = false;
+      int cls = 0;
+      uint32_t cm = 0;
+      if (interior) {
+        const int p[4] = {ti * PJ + tj, ti * PJ + tj + 1, (ti + 1) * PJ + tj, (ti + 1) * PJ + tj + 1};
+        cls = sam[p[0]] & 0xff;
+        bool same = true, finite = true;
+        float mmin = INFINITY, amax = 0.f;
 #pragma unroll
-    for (int i = 0; i < TF / 4; ++i) {
-      const int f = 4 * i;
-      dst[i] = make_float4(s[(f + 0) / NC][(f + 0) % NC], s[(f + 1) / NC][(f + 1) % NC], s[(f + 2) / NC][(f + 2) % NC],
-                           s[(f + 3) / NC][(f + 3) % NC]);
+        for (int t = 0; t < 4; ++t) {
+          const int a = sam[p[t]];
+          same = same && (a & 0xff) == cls;
+          finite = finite && (a & 0x100) != 0;
+          mmin = fminf(mmin, smarg[p[t]]);
+          amax = fmaxf(amax, sabsb[p[t]]);
+        }
+        fast = same && wmin > 0.f && finite && mmin >= 0x1p-16f / wmin * (1.f + 0x1p-10f) + 0x1p-20f * amax;
+        if (!fast && finite && wmin > 0.f) {
+          // candidate classes (see oct_row_labels_cand): kept when max_t L_t[k] >= max_j min_t L_t[j] - guard
+          float vmaxabs = 0.f, lmax = -INFINITY;
+#pragma unroll
+          for (int k = 0; k < NC; ++k) {
+            const float a0 = vec[p[0]][k], a1 = vec[p[1]][k], a2 = vec[p[2]][k], a3 = vec[p[3]][k];
+            vmaxabs = fmaxf(vmaxabs, fmaxf(fmaxf(fabsf(a0), fabsf(a1)), fmaxf(fabsf(a2), fabsf(a3))));
+            lmax = fmaxf(lmax, fminf(fminf(a0, a1), fminf(a2, a3)));
+          }
+          const float thr = lmax - (0x1p-16f / wmin * (1.f + 0x1p-10f) + 0x1p-20f * vmaxabs);
+#pragma unroll
+          for (int k = 0; k < NC; ++k) {
+            const float u = fmaxf(fmaxf(vec[p[0]][k], vec[p[1]][k]), fmaxf(vec[p[2]][k], vec[p[3]][k]));
+            cm |= (u >= thr ? 1u : 0u) << k;
+          }
+        }
+      }
+      if (fast) {
+        const int la[4] = {cls, cls, cls, cls};
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int64_t row = static_cast<int64_t>(n) * HW + static_cast<int64_t>(8 * i1 - 4 + r) * W;
+          store_labels4<LABEL_DTYPE>(labels, row + 8 * j1 - 4, la);
+          store_labels4<LABEL_DTYPE>(labels, row + 8 * j1, la);
+        }
+      } else {
+        const int at = atomicAdd(&nslow, 1);
+        slist[at] = static_cast<unsigned short>(tid);
+        scm[at] = cm;
+      }
     }
   }
-  // the compacted taps are per wave (taps[wave], slist[wave]): the wave's own LDS writes land before
-  // its reads (in-order LDS per wave); no block barrier, since waves may have left above
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  // compacted: 8 nslow row tasks dealt over the 64 lanes; a wave of mostly slow blocks (no spatial
-  // coherence) gains little from that, so there each slow lane walks its own 8 rows (the oct
-  // kernel's order) from the same LDS copy
-  const bool compact = nslow <= 40;
-  const int iters = compact ? (8 * nslow + 63) / 64 : 8;
-  for (int it = 0; it < iters; ++it) {
-    const int tk = compact ? it * 64 + lane : 8 * mypos + it;
-    if (compact ? tk >= 8 * nslow : !slow) continue;
-    const int pos = tk >> 3, r = tk & 7;
-    const int sl = slist[wave][pos];
-    const int qs = qb + wave * 64 + sl;
-    int sj1;
-    bool s_vi0, s_vi1, s_vj0, s_vj1;
-    geom(qs, sj1, s_vi0, s_vi1, s_vj0, s_vj1);
+  __syncthreads();
+
+  // ---- 3. the slow windows: 16 tasks each (row r, four-pixel half hh) over the workgroup
+  const int ns = nslow;
+  for (int tk = tid; tk < 16 * ns; tk += 256) {
+    const int e = tk >> 4, r = tk & 7, hh = (tk >> 3) & 1;
+    const int wt = slist[e];
+    const int ti = wt / TJ, tj = wt % TJ;
+    const int i1 = I0 + ti, j1 = J0 + tj;
+    const int q = 2 * j1 - 1 + hh;                   // output columns 4 q .. 4 q + 3
     const int oy = 8 * i1 - 4 + r;
-    if (oy < 0 || oy >= H) continue;
-    float t00[NC], t01[NC], t10[NC], t11[NC];
-    const float4* tp = reinterpret_cast<const float4*>(taps[wave][pos]);
-    float tv[TF];
-#pragma unroll
-    for (int i = 0; i < TF / 4; ++i) {
-      const float4 v = tp[i];
-      tv[4 * i] = v.x;
-      tv[4 * i + 1] = v.y;
-      tv[4 * i + 2] = v.z;
-      tv[4 * i + 3] = v.w;
-    }
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      t00[k] = tv[k];
-      t01[k] = tv[NC + k];
-      t10[k] = tv[2 * NC + k];
-      t11[k] = tv[3 * NC + k];
-    }
+    if (q < 0 || 4 * q >= W || oy < 0 || oy >= H) continue;
+    const int kx1_0 = 4 * q + 4 - 8 * j1;
+    const int64_t pix = static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy) * W + 4 * q;
+    const bool vi0 = i1 - 1 >= 0, vi1 = i1 < h, vj0 = j1 - 1 >= 0, vj1 = j1 < w;
     int arg[4];
-    oct_row_labels<NC>(t00, t01, t10, t11, wk, r, 4 * qs + 4 - 8 * sj1, s_vi0, s_vi1, s_vj0, s_vj1, arg);
-    store_labels4<LABEL_DTYPE>(labels, static_cast<int64_t>(n) * HW + static_cast<int64_t>(oy) * W + 4 * qs, arg);
+    float t[4][NC];
+    if (vi0 && vi1 && vj0 && vj1) {
+      const int p00 = ti * PJ + tj;
+      const uint32_t cm = scm[e];
+      if (cm != 0) {
+        if (oct_row_labels_cand<NC>(vec[p00], vec[p00 + 1], vec[p00 + PJ], vec[p00 + PJ + 1], cm, wk, r, kx1_0, arg)) {
+          store_labels4<LABEL_DTYPE>(labels, pix, arg);
+          continue;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        t[0][k] = vec[p00][k];
+        t[1][k] = vec[p00 + 1][k];
+        t[2][k] = vec[p00 + PJ][k];
+        t[3][k] = vec[p00 + PJ + 1][k];
+      }
+    } else {                                         // border window: the oct kernel's clamped taps
+      const int ci0 = vi0 ? i1 - 1 : 0, ci1 = vi1 ? i1 : 0, cj0 = vj0 ? j1 - 1 : 0, cj1 = vj1 ? j1 : 0;
+      load_px(ci0, cj0, t[0]);
+      load_px(ci0, cj1, t[1]);
+      load_px(ci1, cj0, t[2]);
+      load_px(ci1, cj1, t[3]);
+    }
+    oct_row_labels<NC>(t[0], t[1], t[2], t[3], wk, r, kx1_0, vi0, vi1, vj0, vj1, arg);
+    store_labels4<LABEL_DTYPE>(labels, pix, arg);
   }
 }
 
@@ -842,14 +935,14 @@ extern "C" int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const floa
   if (cs < c || cs % 4 != 0 || (reinterpret_cast<uintptr_t>(logits) & 15) != 0) return DRNMI_EINVAL;
   if (label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64) return DRNMI_EINVAL;
   if (h + 1 > 65535 || n > 65535) return DRNMI_EINVAL;
-  const int W = w * 8;
-  dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
+  const dim3 gt(static_cast<unsigned>((w + kHeadTJ) / kHeadTJ), static_cast<unsigned>((h + kHeadTI) / kHeadTI),
+                static_cast<unsigned>(n));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (label_dtype == DRNMI_I64)
-    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_I64, 0>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs,
+    hipLaunchKernelGGL((up8_labels_tile_kernel<19, DRNMI_I64, 0>), gt, dim3(256), 0, s, logits, up_w, labels, h, w, cs,
                        nullptr, nullptr);
   else
-    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_U8, 0>), go, dim3(256), 0, s, logits, up_w, labels, h, w, cs,
+    hipLaunchKernelGGL((up8_labels_tile_kernel<19, DRNMI_U8, 0>), gt, dim3(256), 0, s, logits, up_w, labels, h, w, cs,
                        nullptr, nullptr);
   return static_cast<int>(hipGetLastError());
 }
@@ -863,14 +956,14 @@ extern "C" int drnmi_up8_labels_seg2(const float* partials, int32_t cs, const fl
   if (cs < 20 || cs % 4 != 0 || (reinterpret_cast<uintptr_t>(partials) & 15) != 0) return DRNMI_EINVAL;
   if (label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64) return DRNMI_EINVAL;
   if (h + 1 > 65535 || n > 65535) return DRNMI_EINVAL;
-  const int W = w * 8;
-  dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
+  const dim3 gt(static_cast<unsigned>((w + kHeadTJ) / kHeadTJ), static_cast<unsigned>((h + kHeadTI) / kHeadTI),
+                static_cast<unsigned>(n));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (label_dtype == DRNMI_I64)
-    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_I64, 1>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
+    hipLaunchKernelGGL((up8_labels_tile_kernel<19, DRNMI_I64, 1>), gt, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
                        bias, nullptr);
   else
-    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_U8, 1>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
+    hipLaunchKernelGGL((up8_labels_tile_kernel<19, DRNMI_U8, 1>), gt, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
                        bias, nullptr);
   return static_cast<int>(hipGetLastError());
 }
@@ -885,14 +978,14 @@ extern "C" int drnmi_up8_labels_seg2_i8(const int32_t* partials, int32_t cs, con
   if (cs < 20 || cs % 4 != 0 || (reinterpret_cast<uintptr_t>(partials) & 15) != 0) return DRNMI_EINVAL;
   if (label_dtype != DRNMI_U8 && label_dtype != DRNMI_I64) return DRNMI_EINVAL;
   if (h + 1 > 65535 || n > 65535) return DRNMI_EINVAL;
-  const int W = w * 8;
-  dim3 go(static_cast<unsigned>((W / 4 + 255) / 256), static_cast<unsigned>(h + 1), static_cast<unsigned>(n));
+  const dim3 gt(static_cast<unsigned>((w + kHeadTJ) / kHeadTJ), static_cast<unsigned>((h + kHeadTI) / kHeadTI),
+                static_cast<unsigned>(n));
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (label_dtype == DRNMI_I64)
-    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_I64, 2>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
+    hipLaunchKernelGGL((up8_labels_tile_kernel<19, DRNMI_I64, 2>), gt, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
                        shift, scale);
   else
-    hipLaunchKernelGGL((up8_labels_fast_kernel<19, DRNMI_U8, 2>), go, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
+    hipLaunchKernelGGL((up8_labels_tile_kernel<19, DRNMI_U8, 2>), gt, dim3(256), 0, s, partials, up_w, labels, h, w, cs,
                        shift, scale);
   return static_cast<int>(hipGetLastError());
 }
