@@ -29,6 +29,10 @@ namespace {
 
 constexpr int kThreads = 256;
 
+inline bool aligned16(const void* a, const void* b, const void* c) {
+  return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(c)) & 15) == 0;
+}
+
 inline unsigned grid_of(int64_t n, int per = kThreads) {
   const int64_t g = (n + per - 1) / per;
   return static_cast<unsigned>(g < 1 ? 1 : (g > 65535 * 16 ? 65535 * 16 : g));
@@ -1321,8 +1325,19 @@ wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int cout, int cin,
     const int tap = k / cs;
     const int ci = k - tap * cs;
     if (ci >= cin) continue;
+    // eight splits' loads in flight at a time, summed in split order (one load per add serialised
+    // the chain on its latency)
     float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += ws[static_cast<int64_t>(z) * cout * K + i];
+    const int64_t zs = static_cast<int64_t>(cout) * K;
+    int z = 0;
+    for (; z + 8 <= splits; z += 8) {
+      float a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = ws[(z + u) * zs + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += a[u];
+    }
+    for (; z < splits; ++z) s += ws[z * zs + i];
     const int64_t o = (static_cast<int64_t>(co) * cin + ci) * ks * ks + tap;   // tap = kh * ks + kw
     dw[o] = acc ? dw[o] + s : s;
   }
@@ -1466,7 +1481,10 @@ zero_insert_kernel(const float* __restrict__ dy, int n, int ho, int wo, int c4, 
 }
 
 // ------------------------------------------------------------------ head backward
-// du[n][c][p] = scale * (g[n][c][p] - exp(lp[n][c][p]) * sum_c' g[n][c'][p])  (LogSoftmax bwd)
+// du[n][c][p] = scale * (g[n][c][p] - exp(lp[n][c][p]) * sum_c' g[n][c'][p])  (LogSoftmax bwd).
+// NC > 0: the class count at compile time (19, the seg head), the pixel's values held in registers
+// (one read of g instead of two); NC = 0: any c.  Same operations in the same order either way.
+template <int NC>
 __global__ void __launch_bounds__(kThreads)
 lsm_bwd_kernel(const float* __restrict__ g, const float* __restrict__ lp, int nimg, int c, int64_t hw, float scale,
                float* __restrict__ du) {
@@ -1475,45 +1493,98 @@ lsm_bwd_kernel(const float* __restrict__ g, const float* __restrict__ lp, int ni
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int64_t b = i / hw, p = i - b * hw;
     const int64_t base = b * c * hw + p;
-    float s = 0.f;
-    for (int k = 0; k < c; ++k) s += g[base + k * hw];
-    for (int k = 0; k < c; ++k) {
-      const int64_t o = base + k * hw;
-      du[o] = scale * (g[o] - expf(lp[o]) * s);
+    if constexpr (NC > 0) {
+      float gv[NC], lv[NC];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        gv[k] = g[base + k * hw];
+        lv[k] = lp[base + k * hw];
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) s += gv[k];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) du[base + k * hw] = scale * (gv[k] - expf(lv[k]) * s);
+    } else {
+      float s = 0.f;
+      for (int k = 0; k < c; ++k) s += g[base + k * hw];
+      for (int k = 0; k < c; ++k) {
+        const int64_t o = base + k * hw;
+        du[o] = scale * (g[o] - expf(lp[o]) * s);
+      }
     }
   }
 }
 
 // dlogits[n][c][i][j] = sum_{ky,kx} W[ky][kx] * du[n][c][8i-4+ky][8j-4+kx] (+ gscale * g_logits); the
 // transpose of ConvTranspose2d(k16, s8, p4) (lmodels/drnseg.py:285-293).  du == NULL: logits-only
-// gradient (no log-prob term).
-__global__ void __launch_bounds__(kThreads)
+// gradient (no log-prob term).  A workgroup owns UBI x UBJ outputs of one plane and stages the
+// (8 UBI + 8) x (8 UBJ + 8) du window they read into LDS once (each du value is read by four
+// outputs' 16 x 16 windows); every output then sums its 256 products in the same ky-major order,
+// skipping the same out-of-image taps: the same result bits as the per-output global gather.
+constexpr int kUbI = 4, kUbJ = 32, kUbThreads = kUbI * kUbJ;   // outputs per workgroup, one per thread
+constexpr int kUbRows = 8 * kUbI + 8, kUbCols = 8 * kUbJ + 8;
+static_assert(kUbCols % 8 == 0, "16-B staging pieces stay inside one skew group");
+// column c of a tile row at c + c / 8: output windows start 8 columns apart, so a wave's 32 lanes
+// of one row read 9 apart -- distinct banks
+constexpr int kUbPitch = kUbCols + kUbCols / 8 + 1;
+__global__ void __launch_bounds__(kUbThreads)
 up8_bwd_kernel(const float* __restrict__ du, const float* __restrict__ upw, const float* __restrict__ glog,
                float gscale, int nc, int h, int w, float* __restrict__ dlog) {
   __shared__ float wk[256];
-  wk[threadIdx.x] = upw[threadIdx.x];
-  __syncthreads();
+  __shared__ float tile[kUbRows * kUbPitch];
+  for (int e = threadIdx.x; e < 256; e += kUbThreads) wk[e] = upw[e];
   const int H = 8 * h, W = 8 * w;
-  const int64_t total = static_cast<int64_t>(nc) * h * w;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int j = static_cast<int>(i % w);
-    const int ii = static_cast<int>((i / w) % h);
-    const int64_t plane = i / (static_cast<int64_t>(w) * h);
+  const int64_t plane = blockIdx.z;
+  const int i0 = blockIdx.y * kUbI, j0 = blockIdx.x * kUbJ;
+  const int y0 = 8 * i0 - 4, x0 = 8 * j0 - 4;        // du window origin
+  if (du != nullptr) {
+    // 16-B pieces (W = 8 w and x0 = 8 j0 - 4 are multiples of 4: a piece is wholly inside or outside
+    // the image), all of a thread's pieces in flight before their LDS writes
     const float* src = du + plane * H * W;
-    float s = 0.f;
-    for (int ky = 0; ky < 16 && du != nullptr; ++ky) {
-      const int y = 8 * ii - 4 + ky;
-      if (static_cast<unsigned>(y) >= static_cast<unsigned>(H)) continue;
-      const float* row = src + static_cast<int64_t>(y) * W;
-      for (int kx = 0; kx < 16; ++kx) {
-        const int x = 8 * j - 4 + kx;
-        if (static_cast<unsigned>(x) < static_cast<unsigned>(W)) s += wk[ky * 16 + kx] * row[x];
+    constexpr int kP4 = kUbCols / 4, kN4 = kUbRows * kP4;
+    constexpr int kB = (kN4 + kUbThreads - 1) / kUbThreads;
+    float4 v[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int e = threadIdx.x + u * kUbThreads;
+      const int r = e / kP4, x = x0 + 4 * (e - r * kP4), y = y0 + r;
+      v[u] = (e < kN4 && static_cast<unsigned>(y) < static_cast<unsigned>(H) &&
+              static_cast<unsigned>(x) < static_cast<unsigned>(W))
+                 ? *reinterpret_cast<const float4*>(src + static_cast<int64_t>(y) * W + x)
+                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int e = threadIdx.x + u * kUbThreads;
+      if (e < kN4) {
+        const int r = e / kP4, cc = 4 * (e - r * kP4);
+        float* t = tile + r * kUbPitch + cc + (cc >> 3);   // the 4 columns share one 8-group
+        t[0] = v[u].x;
+        t[1] = v[u].y;
+        t[2] = v[u].z;
+        t[3] = v[u].w;
       }
     }
-    if (glog != nullptr) s += gscale * glog[i];   // the logits output's gradient, DDP-averaged like du
-    dlog[i] = s;
   }
+  __syncthreads();
+  const int ii = i0 + threadIdx.x / kUbJ, j = j0 + threadIdx.x % kUbJ;
+  if (ii >= h || j >= w) return;
+  const float* t0 = tile + 8 * (threadIdx.x / kUbJ) * kUbPitch + 9 * (threadIdx.x % kUbJ);   // (8 ti, 8 tj)
+  float s = 0.f;
+  for (int ky = 0; ky < 16 && du != nullptr; ++ky) {
+    const int y = 8 * ii - 4 + ky;
+    if (static_cast<unsigned>(y) >= static_cast<unsigned>(H)) continue;
+    const float* row = t0 + ky * kUbPitch;
+#pragma unroll
+    for (int kx = 0; kx < 16; ++kx) {
+      const int x = 8 * j - 4 + kx;
+      if (static_cast<unsigned>(x) < static_cast<unsigned>(W)) s += wk[ky * 16 + kx] * row[kx + (kx >> 3)];
+    }
+  }
+  const int64_t i = (plane * h + ii) * w + j;
+  if (glog != nullptr) s += gscale * glog[i];   // the logits output's gradient, DDP-averaged like du
+  dlog[i] = s;
 }
 
 // Transpose of nn.UpsamplingBilinear2d(scale_factor=8) (align_corners=True, lmodels/drnseg.py:
@@ -1581,6 +1652,36 @@ up8_bilinear_bwd_kernel(const float* __restrict__ du, const float* __restrict__ 
 // semantic_seg.py:817 + :197-198); block partials (sum, count) in fp64, fixed order.
 constexpr int kCeBlocks = 512;
 
+// one pixel's lse(lp) - lp[t]: NC > 0 holds the NC values in registers (one read instead of three),
+// NC = 0 walks any c; same operations in the same order
+template <int NC>
+__device__ __forceinline__ float ce_pixel(const float* v, int c, int64_t hw, int64_t t) {
+  if constexpr (NC > 0) {
+    float x[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) x[k] = v[k * hw];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) mx = fmaxf(mx, x[k]);
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) se += expf(x[k] - mx);
+    const float lse = mx + logf(se);
+    float xt = x[0];
+#pragma unroll
+    for (int k = 1; k < NC; ++k) xt = k == t ? x[k] : xt;
+    return lse - xt;
+  } else {
+    float mx = -INFINITY;
+    for (int k = 0; k < c; ++k) mx = fmaxf(mx, v[k * hw]);
+    float se = 0.f;
+    for (int k = 0; k < c; ++k) se += expf(v[k * hw] - mx);
+    const float lse = mx + logf(se);
+    return lse - v[t * hw];
+  }
+}
+
+template <int NC>
 __global__ void __launch_bounds__(kThreads)
 ce_fwd_kernel(const float* __restrict__ lp, const int64_t* __restrict__ tgt, int nimg, int c, int64_t hw,
               int64_t ignore, double* __restrict__ ws) {
@@ -1592,13 +1693,7 @@ ce_fwd_kernel(const float* __restrict__ lp, const int64_t* __restrict__ tgt, int
     if (t == ignore) continue;
     if (t < 0 || t >= c) { bad += 1; continue; }
     const int64_t b = i / hw, p = i - b * hw;
-    const float* v = lp + b * c * hw + p;
-    float mx = -INFINITY;
-    for (int k = 0; k < c; ++k) mx = fmaxf(mx, v[k * hw]);
-    float se = 0.f;
-    for (int k = 0; k < c; ++k) se += expf(v[k * hw] - mx);
-    const float lse = mx + logf(se);
-    s += static_cast<double>(lse - v[t * hw]);
+    s += static_cast<double>(ce_pixel<NC>(lp + b * c * hw + p, c, hw, t));
     cnt += 1;
   }
   __shared__ double sh[3][kThreads];
@@ -1621,20 +1716,76 @@ ce_fwd_kernel(const float* __restrict__ lp, const int64_t* __restrict__ tgt, int
   }
 }
 
-__global__ void ce_final_kernel(const double* __restrict__ ws, int blocks, float* __restrict__ loss,
-                                float* __restrict__ count) {
+// the block partials summed in block order by one thread, from LDS (the 64 threads stage them:
+// one dependent fp64 add per partial instead of a global load each)
+__global__ void __launch_bounds__(64) ce_final_kernel(const double* __restrict__ ws, int blocks, float* __restrict__ loss,
+                                                      float* __restrict__ count) {
+  __shared__ double sh[3 * kCeBlocks];
+  for (int e = threadIdx.x; e < 3 * kCeBlocks; e += 64) sh[e] = ws[e];
+  __syncthreads();
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   double s = 0, cnt = 0, bad = 0;
   for (int b = 0; b < blocks; ++b) {
-    s += ws[b];
-    cnt += ws[kCeBlocks + b];
-    bad += ws[2 * kCeBlocks + b];
+    s += sh[b];
+    cnt += sh[kCeBlocks + b];
+    bad += sh[2 * kCeBlocks + b];
   }
   // an out-of-range target is an error in the reference (device assert); surface it as NaN
   loss[0] = bad > 0 ? __builtin_nanf("") : static_cast<float>(s / cnt);
   count[0] = static_cast<float>(cnt);
 }
 
+// four consecutive pixels per thread as 16-B pieces (NC > 0, hw % 4 == 0); per-pixel arithmetic
+// as ce_bwd_kernel
+template <int NC>
+__global__ void __launch_bounds__(kThreads)
+ce_bwd_v4_kernel(const float* __restrict__ lp, const int64_t* __restrict__ tgt, int nimg, int c, int64_t hw,
+                 int64_t ignore, const float* __restrict__ dloss, const float* __restrict__ count,
+                 float* __restrict__ glp) {
+  const float sc = dloss[0] / count[0];
+  const int64_t total4 = static_cast<int64_t>(nimg) * hw / 4;
+  const int64_t hw4 = hw / 4;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total4;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t b = i / hw4, p4 = i - b * hw4;
+    const int64_t base4 = b * c * hw4 + p4;
+    const float4* v4 = reinterpret_cast<const float4*>(lp) + base4;
+    float x[4][NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const float4 a = v4[k * hw4];
+      x[0][k] = a.x;
+      x[1][k] = a.y;
+      x[2][k] = a.z;
+      x[3][k] = a.w;
+    }
+    float lse[4];
+    int64_t tt[4];
+    bool live[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      tt[e] = tgt[4 * i + e];
+      live[e] = !(tt[e] == ignore || tt[e] < 0 || tt[e] >= c);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) mx = fmaxf(mx, x[e][k]);
+      float se = 0.f;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) se += expf(x[e][k] - mx);
+      lse[e] = mx + logf(se);
+    }
+    float4* o4 = reinterpret_cast<float4*>(glp) + base4;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = live[e] ? sc * (expf(x[e][k] - lse[e]) - (k == tt[e] ? 1.f : 0.f)) : 0.f;
+      o4[k * hw4] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
+template <int NC>
 __global__ void __launch_bounds__(kThreads)
 ce_bwd_kernel(const float* __restrict__ lp, const int64_t* __restrict__ tgt, int nimg, int c, int64_t hw,
               int64_t ignore, const float* __restrict__ dloss, const float* __restrict__ count,
@@ -1651,12 +1802,27 @@ ce_bwd_kernel(const float* __restrict__ lp, const int64_t* __restrict__ tgt, int
       for (int k = 0; k < c; ++k) o[k * hw] = 0.f;
       continue;
     }
-    float mx = -INFINITY;
-    for (int k = 0; k < c; ++k) mx = fmaxf(mx, v[k * hw]);
-    float se = 0.f;
-    for (int k = 0; k < c; ++k) se += expf(v[k * hw] - mx);
-    const float lse = mx + logf(se);
-    for (int k = 0; k < c; ++k) o[k * hw] = sc * (expf(v[k * hw] - lse) - (k == t ? 1.f : 0.f));
+    if constexpr (NC > 0) {
+      float x[NC];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) x[k] = v[k * hw];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) mx = fmaxf(mx, x[k]);
+      float se = 0.f;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) se += expf(x[k] - mx);
+      const float lse = mx + logf(se);
+#pragma unroll
+      for (int k = 0; k < NC; ++k) o[k * hw] = sc * (expf(x[k] - lse) - (k == t ? 1.f : 0.f));
+    } else {
+      float mx = -INFINITY;
+      for (int k = 0; k < c; ++k) mx = fmaxf(mx, v[k * hw]);
+      float se = 0.f;
+      for (int k = 0; k < c; ++k) se += expf(v[k * hw] - mx);
+      const float lse = mx + logf(se);
+      for (int k = 0; k < c; ++k) o[k * hw] = sc * (expf(v[k * hw] - lse) - (k == t ? 1.f : 0.f));
+    }
   }
 }
 
@@ -2072,18 +2238,20 @@ extern "C" int drnmi_up8_lsm_bwd_f32(const float* g_logprobs, const float* logpr
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t hw = static_cast<int64_t>(64) * h * w;
   if (g_logprobs != nullptr) {
-    hipLaunchKernelGGL(lsm_bwd_kernel, dim3(grid_of(n * hw)), dim3(kThreads), 0, s, g_logprobs, logprobs, n, c, hw,
-                       grad_scale, du_ws);
+    if (c == 19)
+      hipLaunchKernelGGL(lsm_bwd_kernel<19>, dim3(grid_of(n * hw)), dim3(kThreads), 0, s, g_logprobs, logprobs, n, c, hw,
+                         grad_scale, du_ws);
+    else
+      hipLaunchKernelGGL(lsm_bwd_kernel<0>, dim3(grid_of(n * hw)), dim3(kThreads), 0, s, g_logprobs, logprobs, n, c, hw,
+                         grad_scale, du_ws);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);
-    hipLaunchKernelGGL(up8_bwd_kernel, dim3(grid_of(static_cast<int64_t>(n) * c * h * w)), dim3(kThreads), 0, s,
-                       du_ws, up_w, g_logits, grad_scale, n * c, h, w, dlogits);
-  } else {
-    // logits-only gradient: dlogits = grad_scale * g_logits
-    if (g_logits == nullptr) return DRNMI_EINVAL;
-    hipLaunchKernelGGL(up8_bwd_kernel, dim3(grid_of(static_cast<int64_t>(n) * c * h * w)), dim3(kThreads), 0, s,
-                       nullptr, up_w, g_logits, grad_scale, n * c, h, w, dlogits);
+  } else if (g_logits == nullptr) {   // logits-only gradient: dlogits = grad_scale * g_logits
+    return DRNMI_EINVAL;
   }
+  if (static_cast<int64_t>(n) * c > 65535) return DRNMI_EINVAL;   // planes on grid z
+  hipLaunchKernelGGL(up8_bwd_kernel, dim3((w + kUbJ - 1) / kUbJ, (h + kUbI - 1) / kUbI, n * c), dim3(kUbThreads), 0, s,
+                     g_logprobs != nullptr ? du_ws : nullptr, up_w, g_logits, grad_scale, n * c, h, w, dlogits);
   return static_cast<int>(hipGetLastError());
 }
 
@@ -2096,8 +2264,12 @@ extern "C" int drnmi_up8_bilinear_lsm_bwd_f32(const float* g_logprobs, const flo
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t hw = static_cast<int64_t>(64) * h * w;
   if (g_logprobs != nullptr) {
-    hipLaunchKernelGGL(lsm_bwd_kernel, dim3(grid_of(n * hw)), dim3(kThreads), 0, s, g_logprobs, logprobs, n, c, hw,
-                       grad_scale, du_ws);
+    if (c == 19)
+      hipLaunchKernelGGL(lsm_bwd_kernel<19>, dim3(grid_of(n * hw)), dim3(kThreads), 0, s, g_logprobs, logprobs, n, c, hw,
+                         grad_scale, du_ws);
+    else
+      hipLaunchKernelGGL(lsm_bwd_kernel<0>, dim3(grid_of(n * hw)), dim3(kThreads), 0, s, g_logprobs, logprobs, n, c, hw,
+                         grad_scale, du_ws);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return static_cast<int>(e);
   }
@@ -2114,8 +2286,12 @@ extern "C" int drnmi_ce_loss_f32(const float* logprobs, const int64_t* target, i
       c <= 0 || hw <= 0)
     return DRNMI_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(ce_fwd_kernel, dim3(kCeBlocks), dim3(kThreads), 0, s, logprobs, target, n, c, hw, ignore_index,
-                     reinterpret_cast<double*>(ws));
+  if (c == 19)
+    hipLaunchKernelGGL(ce_fwd_kernel<19>, dim3(kCeBlocks), dim3(kThreads), 0, s, logprobs, target, n, c, hw,
+                       ignore_index, reinterpret_cast<double*>(ws));
+  else
+    hipLaunchKernelGGL(ce_fwd_kernel<0>, dim3(kCeBlocks), dim3(kThreads), 0, s, logprobs, target, n, c, hw,
+                       ignore_index, reinterpret_cast<double*>(ws));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return static_cast<int>(e);
   hipLaunchKernelGGL(ce_final_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<const double*>(ws), kCeBlocks, loss,
@@ -2129,9 +2305,18 @@ extern "C" int drnmi_ce_loss_bwd_f32(const float* logprobs, const int64_t* targe
   if (logprobs == nullptr || target == nullptr || dloss == nullptr || count == nullptr || g_logprobs == nullptr ||
       n <= 0 || c <= 0 || hw <= 0)
     return DRNMI_EINVAL;
-  hipLaunchKernelGGL(ce_bwd_kernel, dim3(grid_of(static_cast<int64_t>(n) * hw)), dim3(kThreads), 0,
-                     reinterpret_cast<hipStream_t>(stream), logprobs, target, n, c, hw, ignore_index, dloss, count,
-                     g_logprobs);
+  if (c == 19 && hw % 4 == 0 && aligned16(logprobs, g_logprobs, nullptr))
+    hipLaunchKernelGGL(ce_bwd_v4_kernel<19>, dim3(grid_of(static_cast<int64_t>(n) * hw / 4)), dim3(kThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), logprobs, target, n, c, hw, ignore_index, dloss, count,
+                       g_logprobs);
+  else if (c == 19)
+    hipLaunchKernelGGL(ce_bwd_kernel<19>, dim3(grid_of(static_cast<int64_t>(n) * hw)), dim3(kThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), logprobs, target, n, c, hw, ignore_index, dloss, count,
+                       g_logprobs);
+  else
+    hipLaunchKernelGGL(ce_bwd_kernel<0>, dim3(grid_of(static_cast<int64_t>(n) * hw)), dim3(kThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), logprobs, target, n, c, hw, ignore_index, dloss, count,
+                       g_logprobs);
   return static_cast<int>(hipGetLastError());
 }
 
