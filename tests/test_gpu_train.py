@@ -373,14 +373,18 @@ def test_bn_and_ce_kernels_match_torch():
     assert TC.rel_err(lpd.grad.cpu(), lp.grad) <= 1e-5
 
 
-def test_head_backward_matches_autograd():
+@pytest.mark.parametrize("h,w", [(6, 9), (11, 70)])
+def test_head_backward_matches_autograd(h, w):
+    """LogSoftmax + x8 transpose-conv backward (the LDS-tiled up8_bwd_kernel: 4 x 32 outputs per
+    workgroup, so 11 x 70 has ragged tiles in both directions) against autograd, and the
+    logits-only gradient (no log-prob term)."""
     from drnmi.drnseg import DRNSeg
     from drnmi import _lib
     lib = _lib.load()
     m = DRNSeg("drn_d_22", 19, pretrained=False)
     upw = m.up.weight.detach()
     torch.manual_seed(1)
-    logits = torch.randn(2, 19, 6, 9, requires_grad=True)
+    logits = torch.randn(2, 19, h, w, requires_grad=True)
     lp = F.log_softmax(F.conv_transpose2d(logits, upw, stride=8, padding=4, groups=19), 1)
     g = torch.randn_like(lp)
     gl = torch.randn_like(logits)
@@ -390,10 +394,34 @@ def test_head_backward_matches_autograd():
     du = torch.empty_like(lpd)
     out = torch.empty_like(gld)
     vp = lambda t: ctypes.c_void_p(t.data_ptr())
-    _lib.check(lib.drnmi_up8_lsm_bwd_f32(vp(gd), vp(lpd), vp(gld), vp(upd), 1.0, 2, 19, 6, 9, vp(du),
+    _lib.check(lib.drnmi_up8_lsm_bwd_f32(vp(gd), vp(lpd), vp(gld), vp(upd), 1.0, 2, 19, h, w, vp(du),
                                          vp(out), ctypes.c_void_p(_lib.stream_ptr())), "up8_lsm_bwd")
+    out2 = torch.empty_like(gld)
+    _lib.check(lib.drnmi_up8_lsm_bwd_f32(None, None, vp(gld), vp(upd), 0.5, 2, 19, h, w, None,
+                                         vp(out2), ctypes.c_void_p(_lib.stream_ptr())), "up8_lsm_bwd logits-only")
     torch.cuda.synchronize()
     assert TC.rel_err(out.cpu(), ref) <= 1e-5
+    assert torch.equal(out2.cpu(), 0.5 * gl)
+
+
+@pytest.mark.parametrize("shape", [(2, 24, 40), (1, 23, 41)])
+def test_ce_matches_torch_shapes(shape):
+    """CE forward / backward (register-held classes; hw % 4 == 0 takes the four-pixel backward,
+    23 x 41 the per-pixel one) against torch, ignore_index and all-ignored rows included."""
+    from drnmi.train import CrossEntropyLoss
+    n, h, w = shape
+    g = torch.Generator().manual_seed(h * w)
+    lp = F.log_softmax(torch.randn(n, 19, h, w, generator=g) * 3, 1).requires_grad_(True)
+    t = torch.randint(0, 19, (n, h, w), generator=g)
+    t[torch.rand(t.shape, generator=g) < 0.3] = 255
+    t[0, 0] = 255
+    loss_ref = F.cross_entropy(lp, t, ignore_index=255)
+    loss_ref.backward()
+    lpd = lp.detach().to(DEV).requires_grad_(True)
+    loss = CrossEntropyLoss(ignore_index=255)(lpd, t.to(DEV))
+    loss.backward()
+    assert abs(loss.item() - loss_ref.item()) <= 1e-5 * abs(loss_ref.item())
+    assert TC.rel_err(lpd.grad.cpu(), lp.grad) <= 1e-5
 
 
 @pytest.mark.parametrize("nesterov,damp", [(False, 0.0), (True, 0.0), (False, 0.3)])
