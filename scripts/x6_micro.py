@@ -38,7 +38,7 @@ SEL = os.environ.get("SHAPES")
 if SEL:
     SHAPES = [sh for sh in SHAPES if any(k in sh[0] for k in SEL.split(","))]
 VARIANTS = [(-1 if v == "auto" else int(v)) for v in os.environ.get("VARIANTS", "auto").split(",")]
-# SPLITS=1,2,4: force split-K counts on the split shapes (tile = variant + 5 * splits; the variant
+# SPLITS=1,2,4: force split-K counts on the split shapes (tile = variant + 6 * splits; the variant
 # is the auto one when VARIANTS=auto)
 SPLITS = [int(v) for v in os.environ.get("SPLITS", "0").split(",")]
 lib = _lib.load()
@@ -69,7 +69,7 @@ for name, n, h, w, cin, cout, ks, s, pad, dil, res, split in SHAPES:
     for var, sp in combos:
       a.tile = var
       if sp > 0:
-          a.tile = (var if var >= 0 else 0 if cout % 256 == 0 else 3 if cout % 128 == 0 else 2) + 5 * sp
+          a.tile = (var if var >= 0 else 0 if cout % 256 == 0 else 3 if cout % 128 == 0 else 2) + 6 * sp
       if split:                       # workspace for this launch's own split count
           a.ws, a.ws_bytes = None, 0
           nb = lib.drnmi_conv_workspace_bytes(ctypes.byref(a))

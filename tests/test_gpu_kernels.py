@@ -586,10 +586,10 @@ def test_conv_x6_split_k(case):
 @pytest.mark.parametrize("case", [X6_CASES[0], X6_CASES[2], X6_CASES[4]])
 def test_conv_x6_variants_bit_identical(case):
     """Every conv_x6 tile variant (forced through drnmi_conv_args.tile: 256 / 128 / 64 channels,
-    8- and 4-wave, and the 128 x 128 two-per-CU tile) keeps each accumulator's MFMA order: the
-    outputs are bit-identical to the auto variant's."""
+    8- and 4-wave, and the 128 x 128 / 64 x 128 two-per-CU tiles) keeps each accumulator's MFMA
+    order: the outputs are bit-identical to the auto variant's."""
     outs = {}
-    for v in (-1, 0, 1, 2, 3, 4):
+    for v in (-1, 0, 1, 2, 3, 4, 5):
         y = _x6_case(case, split=False, tile=v, check=v == -1)
         if y is not None:
             outs[v] = y
@@ -599,9 +599,9 @@ def test_conv_x6_variants_bit_identical(case):
 
 
 def test_conv_x6_two_per_cu_split_k():
-    """The two-workgroups-per-CU tile under a forced split-K (tile = 4 + 5 * 2): as accurate as the
+    """The two-workgroups-per-CU tile under a forced split-K (tile = 4 + 6 * 2): as accurate as the
     unsplit kernel."""
-    _x6_case(X6_CASES[0], split=True, tile=4 + 5 * 2)
+    _x6_case(X6_CASES[0], split=True, tile=4 + 6 * 2)
 
 
 @pytest.mark.parametrize("case", [X6_CASES[1], X6_CASES[2], (2, 24, 20, 64, 256, 1, 1, 0, 1, False)])

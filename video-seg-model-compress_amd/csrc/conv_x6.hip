@@ -555,21 +555,26 @@ hipError_t launch_x6(const drnmi_conv_args& p, int splits, hipStream_t s) {
 
 // variants: 0 <K, 128, 2, 4> (256 channels x 256 pixels, 8 waves), 1 <K, 128, 1, 4> (128 x 256, 4
 // waves), 2 <K, 64, 1, 4> (64 x 256, 4 waves), 3 <K, 64, 2, 4> (128 x 256, 8 waves), 4 <K, 64, 2, 2>
-// (128 x 128, 4 waves, two workgroups per CU).  A drnmi_conv_args.tile >= 0 forces variant
-// tile % 5 and, when tile >= 5, tile / 5 split-K partitions (tests, micro-benchmarks; split-K only
-// with a caller workspace).  Every variant keeps each accumulator's MFMA order: bit-identical.
-constexpr int kNumX6 = 5;
-constexpr int kX6Bco[kNumX6] = {256, 128, 64, 128, 128};
-constexpr int kX6Bpx[kNumX6] = {256, 256, 256, 256, 128};
-constexpr int kX6Occ[kNumX6] = {1, 1, 1, 1, 2};
+// (128 x 128, 4 waves, two workgroups per CU), 5 <K, 32, 2, 2> (64 x 128, 4 waves of 32 channels,
+// two per CU).  A drnmi_conv_args.tile >= 0 forces variant tile % 6 and, when tile >= 6, tile / 6
+// split-K partitions (tests, micro-benchmarks; split-K only with a caller workspace).  Every variant
+// keeps each accumulator's MFMA order: bit-identical.
+constexpr int kNumX6 = 6;
+constexpr int kX6Bco[kNumX6] = {256, 128, 64, 128, 128, 64};
+constexpr int kX6Bpx[kNumX6] = {256, 256, 256, 256, 128, 128};
+constexpr int kX6Occ[kNumX6] = {1, 1, 1, 1, 2, 2};
 // seconds per 32-channel K step of one workgroup tile, fitted to scripts/x6_micro.py's sweep on
 // the fine-tune shapes (profiles/r8_finetune/x6_micro_variants.txt): the 256 x 256 tile ~4.3 us,
 // the 8-wave 128 x 256 ~3.0 us, the two-per-CU 128 x 128 ~2.7 us (its 2.1-3.0 us spread tracks
 // how the two resident workgroups overlap; past two rounds the model under-charges it)
-constexpr double kX6Step[kNumX6] = {4.3e-6, 3.6e-6, 2.2e-6, 3.0e-6, 2.7e-6};
+constexpr double kX6Step[kNumX6] = {4.3e-6, 3.6e-6, 2.2e-6, 3.0e-6, 2.7e-6, 2.3e-6};
 // 128-channel layers take the 8-wave tile (two waves per SIMD): D-22 layer4 492 vs 511 us, its 1x1
-// stride-2 downsample 64 vs 83 us at batch 8 (scripts/x6_micro.py, profiles/r7_x6)
-int x6_auto_variant(const drnmi_conv_args& p) { return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 3 : 2; }
+// stride-2 downsample 64 vs 83 us at batch 8 (scripts/x6_micro.py, profiles/r7_x6).  64-channel
+// layers take the two-per-CU 64 x 128 tile (eight waves per CU instead of four): D-22 layer3 3x3
+// 750 -> 660 us at batch 8, the fine-tune's 1x1 256 -> 64 49 -> 37 us (profiles/r9_x6_v5)
+int x6_auto_variant(const drnmi_conv_args& p) {
+  return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 3 : p.cout == 64 ? 5 : 2;
+}
 
 int x6_num_cus() {
   static int cus = 0;
@@ -688,7 +693,8 @@ int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
       case 1: e = launch_x6<2, 128, 1, 4>(p, S, s); break;
       case 2: e = launch_x6<2, 64, 1, 4>(p, S, s); break;
       case 3: e = launch_x6<2, 64, 2, 4>(p, S, s); break;
-      default: e = launch_x6<2, 64, 2, 2>(p, S, s); break;
+      case 4: e = launch_x6<2, 64, 2, 2>(p, S, s); break;
+      default: e = launch_x6<2, 32, 2, 2>(p, S, s); break;
     }
   } else if (p.ks == 3) {
     switch (v) {
@@ -696,7 +702,8 @@ int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
       case 1: e = launch_x6<3, 128, 1, 4>(p, S, s); break;
       case 2: e = launch_x6<3, 64, 1, 4>(p, S, s); break;
       case 3: e = launch_x6<3, 64, 2, 4>(p, S, s); break;
-      default: e = launch_x6<3, 64, 2, 2>(p, S, s); break;
+      case 4: e = launch_x6<3, 64, 2, 2>(p, S, s); break;
+      default: e = launch_x6<3, 32, 2, 2>(p, S, s); break;
     }
   } else {
     switch (v) {
@@ -704,7 +711,8 @@ int x6_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
       case 1: e = launch_x6<1, 128, 1, 4>(p, S, s); break;
       case 2: e = launch_x6<1, 64, 1, 4>(p, S, s); break;
       case 3: e = launch_x6<1, 64, 2, 4>(p, S, s); break;
-      default: e = launch_x6<1, 64, 2, 2>(p, S, s); break;
+      case 4: e = launch_x6<1, 64, 2, 2>(p, S, s); break;
+      default: e = launch_x6<1, 32, 2, 2>(p, S, s); break;
     }
   }
   return static_cast<int>(e);
@@ -714,13 +722,13 @@ const char* x6_conv_name(const drnmi_conv_args& p) {
   if (!x6_conv_supported(p)) return nullptr;
   static const char* n3[kNumX6] = {"conv_x6_kernel<3, 128, 2, 4>", "conv_x6_kernel<3, 128, 1, 4>",
                                    "conv_x6_kernel<3, 64, 1, 4>", "conv_x6_kernel<3, 64, 2, 4>",
-                                   "conv_x6_kernel<3, 64, 2, 2>"};
+                                   "conv_x6_kernel<3, 64, 2, 2>", "conv_x6_kernel<3, 32, 2, 2>"};
   static const char* n1[kNumX6] = {"conv_x6_kernel<1, 128, 2, 4>", "conv_x6_kernel<1, 128, 1, 4>",
                                    "conv_x6_kernel<1, 64, 1, 4>", "conv_x6_kernel<1, 64, 2, 4>",
-                                   "conv_x6_kernel<1, 64, 2, 2>"};
+                                   "conv_x6_kernel<1, 64, 2, 2>", "conv_x6_kernel<1, 32, 2, 2>"};
   static const char* n2[kNumX6] = {"conv_x6_kernel<2, 128, 2, 4>", "conv_x6_kernel<2, 128, 1, 4>",
                                    "conv_x6_kernel<2, 64, 1, 4>", "conv_x6_kernel<2, 64, 2, 4>",
-                                   "conv_x6_kernel<2, 64, 2, 2>"};
+                                   "conv_x6_kernel<2, 64, 2, 2>", "conv_x6_kernel<2, 32, 2, 2>"};
   const int v = x6_plan(p, p.ws != nullptr).v;
   return p.ks == 3 ? n3[v] : p.ks == 2 ? n2[v] : n1[v];
 }
