@@ -33,6 +33,7 @@ SHAPES = [  # name, n, h, w, cin, cout, ks, stride, pad, dil, res, split
     ("ft 3x3 256 d2", 2, 128, 96, 256, 256, 3, 1, 2, 2, False, True),
     ("ft l3 1x1 256-64", 2, 256, 192, 256, 64, 1, 1, 0, 1, False, True),
     ("ft l3 1x1 64-256", 2, 256, 192, 64, 256, 1, 1, 0, 1, True, True),
+    ("seg 1x1 512-19 b8", 8, 128, 256, 512, 19, 1, 1, 0, 1, False, False),
 ]
 SEL = os.environ.get("SHAPES")
 if SEL:

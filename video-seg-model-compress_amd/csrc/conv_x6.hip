@@ -658,7 +658,10 @@ bool x6_conv_supported(const drnmi_conv_args& p) {
          (p.ks == 1 || p.ks == 2 || p.ks == 3) && p.k == p.ks * p.ks * p.cin && p.k_pad == p.k &&
          static_cast<int64_t>(p.n) * p.h * p.w * p.cin < (int64_t(1) << 31) && p.h < 16384 && p.w < 16384 &&
          (p.y_sc != 1 || p.y_sp == p.cout ||
-          (p.y_sr != 0 && p.y_sp % 4 == 0 && p.y_sr % 4 == 0 && p.y_sn % 4 == 0));
+          (p.y_sr != 0 && p.y_sp % 4 == 0 && p.y_sr % 4 == 0 && p.y_sn % 4 == 0) ||
+          // wider NHWC rows (the labels head's 20-float seg logits rows): 16-B aligned, no
+          // residual (a residual is read with the output's own packed layout)
+          (p.y_sp > p.cout && p.y_sp % 4 == 0 && p.y_sn % 4 == 0 && p.res == nullptr));
 }
 
 int64_t x6_conv_workspace_bytes(const drnmi_conv_args& p) {

@@ -655,8 +655,8 @@ class Plan:
 
     # labels-only video path: the seg conv writes fp32 NHWC rows of SEG_NHWC_CS floats (16-B
     # stores instead of 19 strided planes) and drnmi_up8_labels_nhwc reads them; same values,
-    # same labels.  Only where the seg conv runs on conv_big (bf16 input) or on the int8 tile
-    # (int8 nets: store_tile_i8's 16-B fp32 rows) and the 19-class head.
+    # same labels.  Only where the seg conv runs on conv_big (bf16 input), on the int8 tile
+    # (int8 nets: store_tile_i8's 16-B fp32 rows) or on conv_x6 (fp32x) and the 19-class head.
     SEG_NHWC_CS = 20
 
     def _setup_seg_nhwc(self):
@@ -675,7 +675,8 @@ class Plan:
         ctypes.pointer(a)[0] = a0
         a.y_sn, a.y_sp, a.y_sc = lh * lw * cs, cs, 1
         name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))   # (routing does not read a.y)
-        if name is None or not name.decode().startswith(("conv_big_kernel", "conv_i8_kernel", "conv_i8_occ2_kernel")):
+        if name is None or not name.decode().startswith(("conv_big_kernel", "conv_i8_kernel", "conv_i8_occ2_kernel",
+                                                        "conv_x6_kernel")):
             return
         if "logits_nhwc" not in self.bufs:      # only plans whose seg conv writes the NHWC rows
             self.bufs["logits_nhwc"] = torch.empty(self.n * lh * lw * cs, dtype=torch.float32,
