@@ -568,13 +568,15 @@ constexpr int kX6Occ[kNumX6] = {1, 1, 1, 1, 2, 2};
 // the 8-wave 128 x 256 ~3.0 us, the two-per-CU 128 x 128 ~2.7 us (its 2.1-3.0 us spread tracks
 // how the two resident workgroups overlap; past two rounds the model under-charges it)
 constexpr double kX6Step[kNumX6] = {4.3e-6, 3.6e-6, 2.2e-6, 3.0e-6, 2.7e-6, 2.3e-6};
-// 128-channel layers take the 8-wave tile (two waves per SIMD): D-22 layer4 492 vs 511 us, its 1x1
-// stride-2 downsample 64 vs 83 us at batch 8 (scripts/x6_micro.py, profiles/r7_x6).  64-channel
+// 128-channel layers take the two-per-CU 128 x 128 tile: D-22 layer4's five launches 1631-1649 ->
+// 1510-1568 us against the 8-wave 128 x 256 tile, same box, three interleaved runs each
+// (profiles/r9_x6_v5/v4_ab.txt; the 8-wave tile had beaten the 4-wave one, 492 vs 511 us,
+// profiles/r7_x6).  64-channel
 // layers (and the 19-class seg) take the two-per-CU 64 x 128 tile (eight waves per CU instead of
 // four): D-22 layer3 3x3 750 -> 660 us at batch 8, the fine-tune's 1x1 256 -> 64 49 -> 37 us, the
 // seg 1x1 512 -> 19 153 -> 142 us (profiles/r9_x6_v5)
 int x6_auto_variant(const drnmi_conv_args& p) {
-  return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 3 : p.cout <= 64 ? 5 : 2;
+  return p.cout % 256 == 0 ? 0 : p.cout % 128 == 0 ? 4 : p.cout <= 64 ? 5 : 2;
 }
 
 int x6_num_cus() {
