@@ -13,9 +13,11 @@ timing barrier and the max-over-ranks of the elapsed time).
 
 `--gpus N` without a torchrun environment spawns the N rank processes itself (before any GPU
 call; one device each, RCCL rendezvous on 127.0.0.1); under torchrun WORLD_SIZE must equal N.
-The default bf16 line also carries `exact_mode` (the fp32-accurate split-bf16 engine) and
-`exact_mode_fp32` (exact fp32 on the f32 MFMA): the exact-argmax modes on the same weights and
-frames, timed in the same process, each with its own dominant-kernel roofline and parity.
+The default bf16 line also carries `exact_mode` (the fp32-accurate split-bf16 engine),
+`exact_mode_fp32` (exact fp32 on the f32 MFMA) and `int8_mode` (config C5's W8A8): the other
+modes on the same weights and frames, timed in the same process (--exact-steps each), each with
+its own dominant-kernel roofline (HIP-event achieved rate, committed PMC traffic and MFMA-busy),
+time accounting (per-step spread, launch sum vs step) and parity vs the reference.
 
 Prints ONE JSON line (rank 0).
 """
@@ -61,7 +63,8 @@ def parse(argv=None):
                          "the headline value stays HBM-resident)")
     ap.add_argument("--no-exact-mode", action="store_true",
                     help="skip the exact_mode (fp32x) sub-measurement of the default bf16 line")
-    ap.add_argument("--exact-steps", type=int, default=5)
+    ap.add_argument("--exact-steps", type=int, default=20,
+                    help="timed steps of each sub-line (fp32x / fp32 / int8) of the default bf16 line")
     ap.add_argument("--stub-step", action="store_true",
                     help="test hook: no GPU; gloo ranks run a CPU stand-in step through the same launcher, "
                          "seeding, timing and max-over-ranks code (tests/test_bench_launcher.py)")
@@ -115,9 +118,11 @@ def resolve_world(args, environ=os.environ, prog: str = "bench.py"):
     return world, int(environ.get("RANK", "0")), int(environ.get("LOCAL_RANK", "0"))
 
 
-def timed_region(step, steps, world, dev):
+def timed_region(step, steps, world, dev, marks=None):
     """K timed steps bracketed by barrier + device sync on both sides; the slowest rank's
-    elapsed time defines the job (max over ranks).  Returns (job_seconds, own_seconds)."""
+    elapsed time defines the job (max over ranks).  Returns (job_seconds, own_seconds).
+    `marks`: steps + 1 HIP events recorded at the step boundaries (per-step spread; one event
+    per step, on the stream the step launches on)."""
     import torch
     import torch.distributed as dist
     from drnmi.dist import max_over_ranks
@@ -129,14 +134,28 @@ def timed_region(step, steps, world, dev):
     if cuda:
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
+    if marks is not None:
+        marks[0].record()
+    for k in range(steps):
         step(True)
+        if marks is not None:
+            marks[k + 1].record()
     if cuda:
         torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     own = time.perf_counter() - t0
     return max_over_ranks(own, device=dev), own
+
+
+def step_spread(marks):
+    """min / median / max of the per-step durations (ms) between consecutive boundary events."""
+    d = sorted(a.elapsed_time(b) for a, b in zip(marks, marks[1:]))
+    if not d:
+        return None
+    mid = len(d) // 2
+    med = d[mid] if len(d) % 2 else 0.5 * (d[mid - 1] + d[mid])
+    return {"min": round(d[0], 4), "median": round(med, 4), "max": round(d[-1], 4), "steps": len(d)}
 
 
 def gather_ranks(vals, world, dev):
@@ -423,12 +442,34 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
     warm = collect()
     dominant = max(warm, key=lambda k: sum(warm[k]["d"])) if warm else None
     watch[0] = dominant
-    el, own = timed_region(step, steps, world, dev)
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    el, own = timed_region(step, steps, world, dev, marks)
     timed_per = collect()
+    spread = step_spread(marks)
     # per-kernel table: one fully instrumented step after the timed region
     watch[0] = None
     step(True)
+    first_last = (events[0][2], events[-1][2]) if events else None
     per = collect()
+    inst_span = first_last[0].elapsed_time(first_last[1]) if first_last else None
+    # time accounting (per step): the dominant kernel's launches from the timed region, every
+    # other launch from the instrumented step; what the launches do not cover is idle time between
+    # them (host launch gaps, allocator work, a stall) -- the instrumented step's own span vs its
+    # launch sum separates host gaps from a one-off stall in the timed region
+    inst_sum = sum(sum(v["d"]) for v in per.values())
+    dom_timed = sum(timed_per[dominant]["d"]) / steps if dominant in timed_per else 0.0
+    dom_inst = sum(per[dominant]["d"]) if dominant in per else 0.0
+    ksum = inst_sum - dom_inst + dom_timed
+    step_ms = el / steps * 1e3
+    accounting = {"ms_per_step": round(step_ms, 4), "kernel_sum_ms_per_step": round(ksum * 1e3, 4),
+                  "unaccounted_ms_per_step": round(step_ms - ksum * 1e3, 4),
+                  "unaccounted_frac": round(1.0 - ksum * 1e3 / step_ms, 4),
+                  "step_ms": spread,
+                  "instrumented_step": {"span_ms": round(inst_span, 4) if inst_span else None,
+                                        "kernel_sum_ms": round(inst_sum * 1e3, 4)},
+                  "note": "kernel_sum = the dominant kernel's timed-region launches / steps + every other "
+                          "launch of one fully instrumented step after the timed region; step_ms = HIP events "
+                          "at the timed steps' boundaries"}
     # per launch of that step, keyed by the node that opens it (the conv_stag family's launches
     # differ in K and tile count: the weakest shows here, not in the per-kernel average)
     layers = [{"node": nodes[i].name if i < len(nodes) else "head", "kernel": names[i], "us": round(d * 1e6, 1),
@@ -438,7 +479,8 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
         per[dominant] = timed_per[dominant]
     model.timing_hook = None
     return {"el": el, "own": own, "plan": plan, "names": names, "density": density, "per": per,
-            "dominant": dominant, "timed": timed_per.get(dominant), "step": step, "layers": layers}
+            "dominant": dominant, "timed": timed_per.get(dominant), "step": step, "layers": layers,
+            "accounting": accounting}
 
 
 def roofline_block(args, m, precision):
@@ -453,9 +495,27 @@ def roofline_block(args, m, precision):
     ach = avg_f / avg_d / 1e12
     peak = kernel_peak(m["dominant"], m["plan"].packed.base) / 1e12
     traffic, traffic_src = pmc_traffic(args, m["dominant"], precision)
+    mfma = pmc_mfma(args, precision)
+    mk = mfma.get("kernels", {})
+    dom_mfma = mk.get(m["dominant"]) or mk.get(m["dominant"].replace("<f32,", "<float,")) or {}
+    # the step's MFMA-pipe utilisation: every kernel's captured busy fraction weighted by its time in
+    # this run's per-kernel table (kernels without a capture row are reported as uncovered time)
+    wt = cov = 0.0
+    tot = sum(sum(v["d"]) for v in m["per"].values())
+    for k, v in m["per"].items():
+        row = mk.get(k) or mk.get(k.replace("<f32,", "<float,"))
+        if row and row.get("mfma_busy") is not None:
+            wt += row["mfma_busy"] * sum(v["d"])
+            cov += sum(v["d"])
     roof = {"bound": "mfma", "kernel": m["dominant"], "achieved": round(ach, 2), "peak": peak,
             "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": traffic,
             "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+            "mfma_busy": dom_mfma.get("mfma_busy"),
+            "eff_clock_ghz": dom_mfma.get("eff_clock_ghz"),
+            "mfma_busy_step": round(wt / cov, 4) if cov else None,
+            "mfma_busy_step_coverage": round(cov / tot, 4) if tot else None,
+            "mfma_busy_source": mfma.get("source"),
+            "mfma_busy_norm": mfma.get("norm"),
             "dense_equivalent_achieved": round(sum(t["fd"]) / len(durs) / avg_d / 1e12, 2),
             "launches": len(durs), "avg_launch_us": round(avg_d * 1e6, 2),
             "avg_launch_gflop": round(avg_f / 1e9, 3),
@@ -557,26 +617,32 @@ def main(argv=None):
         out["kernels"] = kernels
         out["layers"] = m["layers"]
     out["network_roofline"] = network_block(m, args.steps, B)
+    out["accounting"] = m["accounting"]
     if host is not None:
         out["host_frames"] = host
     exact = {}                               # precision -> (sub-line, model)
     if (world == 1 and args.precision == "bf16" and not args.prune and not args.no_exact_mode
             and not args.no_kernel_events):
-        # exact-argmax modes (north star: labels bit-exact vs the reference), each on the same weights
-        # and frames, timed in this process: fp32x (split-bf16, fp32-accurate) and fp32 (the
-        # reference's own arithmetic on the f32-input MFMA)
-        for prec, arith in EXACT_MODES:
-            xm = build(args.arch, 19, seed=0, device=dev, precision=prec)
-            mx = measure(args, xm, frames, args.exact_steps, 2, world, dev)
+        # the other precision modes on the same weights and frames, timed in this process (each its
+        # own warm-up, >= 20 timed steps, per-step spread and time accounting): the exact-argmax modes
+        # (north star: labels bit-exact vs the reference) fp32x (split-bf16, fp32-accurate) and fp32
+        # (the reference's own arithmetic on the f32-input MFMA), and int8 (config C5's W8A8)
+        for prec, arith in SUB_MODES:
+            xm = build(args.arch, 19, seed=0, device=dev, precision="bf16" if prec == "int8" else prec)
+            if prec == "int8":
+                xm = calibrate(xm, args, dev)
+            mx = measure(args, xm, frames, args.exact_steps, SUB_WARMUP, world, dev)
             xroof, xkern = roofline_block(args, mx, prec)
             exact[prec] = ({"precision": prec, "value": B * args.exact_steps / mx["el"], "unit": "frames/s",
-                            "steps": args.exact_steps, "warmup": 2,
+                            "steps": args.exact_steps, "warmup": SUB_WARMUP,
                             "ms_per_step": mx["el"] / args.exact_steps * 1e3,
                             "roofline": xroof, "network_roofline": network_block(mx, args.exact_steps, B),
-                            "kernels": xkern, "arithmetic": arith}, xm)
+                            "accounting": mx["accounting"], "kernels": xkern, "arithmetic": arith}, xm)
             del mx
+            torch.cuda.empty_cache()
         out["exact_mode"] = exact["fp32x"][0]
         out["exact_mode_fp32"] = exact["fp32"][0]
+        out["int8_mode"] = exact["int8"][0]
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], (bframes, blabels) = cpu_baseline(args, args.cpu_seconds)
         if not args.prune:                   # the oracle runs the unpruned synthetic weights
@@ -589,12 +655,16 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
-EXACT_MODES = (
+SUB_MODES = (
     ("fp32x", "fp32-accurate: exact 3-way bf16 split of weights and activations, the six products above "
               "2^-24 on the bf16 MFMA, fp32 accumulation (peak 2.5 PF / 6)"),
     ("fp32", "exact fp32: f32-input MFMA (v_mfma_f32_16x16x4_f32 = an fmaf chain per output), fp32 "
              "activations, the reference's arithmetic (peak 157.3 TF)"),
+    ("int8", "W8A8 (config C5): per-output-channel int8 weights, per-tensor int8 activations calibrated on "
+             "2 other synthetic frames, int32 accumulation on the i8 MFMA (peak 5 POPS) for cin >= 64 and "
+             "cout >= 256; bf16 below"),
 )
+SUB_WARMUP = 3
 
 
 def host_frames_run(args, model, step, world, dev):
@@ -644,6 +714,28 @@ def host_frames_run(args, model, step, world, dev):
             "h2d_bytes_per_frame": H * W * 3,
             "note": "frames in pinned host memory, H2D on a copy stream overlapped with compute (not the "
                     "headline: the headline times HBM-resident frames)"}
+
+
+def pmc_mfma(args, precision=None):
+    """Per-kernel MFMA-pipe utilisation and held clock from the newest committed capture of this
+    exact workload (profiles/*_pmc_mfma.json, made by scripts/pmc_mfma.sh:
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)); PMC counters cannot be
+    read inside the timed run.  {} when no capture matches."""
+    import glob
+    want = {"arch": args.arch, "height": args.height, "width": args.width, "frames_per_gpu_step": args.batch,
+            "precision": precision or args.precision}
+    here = os.path.dirname(os.path.abspath(__file__))
+    for f in sorted(glob.glob(os.path.join(here, "profiles", "*_pmc_mfma.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") == want and d.get("kernels"):
+            return {"kernels": d["kernels"], "source": os.path.relpath(f, here),
+                    "norm": "per dispatch SQ_VALU_MFMA_BUSY_CYCLES / ((GRBM_GUI_ACTIVE / 8 XCDs) x 1024 SIMDs) "
+                            "in a separate rocprofv3 --pmc pass of this workload; mfma_busy_step = those per-kernel "
+                            "fractions weighted by each kernel's time in this run's per-kernel table"}
+    return {}
 
 
 def pmc_traffic(args, kernel, precision=None):

@@ -117,8 +117,10 @@ typedef struct drnmi_conv_args {
    * split K: drnmi_conv_stats_rows(args) > 0): the epilogue writes per-channel fp64 partial sums
    * of y and y^2, one row per 64-pixel wave slice, as [2][rows][cout] (sums, then sums of
    * squares), in a fixed order.  drnmi_bn_stats_partials_f32 turns them into the batch mean /
-   * invstd exactly as drnmi_bn_stats_f32 would from y (semantic_seg.py:166-230's train-mode
-   * BatchNorm2d after the conv), without reading y again.  NULL: off. */
+   * invstd with the same finalize as drnmi_bn_stats_f32 (mean, biased variance, invstd, running-
+   * stat update; semantic_seg.py:166-230's train-mode BatchNorm2d after the conv), without reading
+   * y again.  The fp64 sums are added in a different fixed order than drnmi_bn_stats_f32's row
+   * splits, so the two agree to fp32 rounding, not bit for bit.  NULL: off. */
   double* stats;
   /* Optional output row stride in elements (F32X3 conv_x6 launches only): y(n, oh, ow, c) =
    * y[n*y_sn + oh*y_sr + ow*y_sp + c*y_sc]; a residual then has y's layout.  0 = rows packed

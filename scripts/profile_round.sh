@@ -16,7 +16,9 @@ for P in int8 fp32x fp32; do
   python3 $R/bench.py --no-cpu-baseline --no-exact-mode --precision $P > $OUT/bench_${P}_under_rocprof.log 2>&1) || { echo "trace $P failed"; exit 1; }
 done
 bash $R/scripts/pmc_traffic.sh $1/pmc_bf16 > /dev/null || exit 1
+bash $R/scripts/pmc_mfma.sh $1/mfma_bf16 || exit 1
 for P in int8 fp32x fp32; do
 bash $R/scripts/pmc_traffic.sh $1/pmc_$P --precision $P > /dev/null || exit 1
+bash $R/scripts/pmc_mfma.sh $1/mfma_$P --precision $P || exit 1
 done
 echo done

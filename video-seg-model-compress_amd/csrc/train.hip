@@ -1969,7 +1969,7 @@ extern "C" int drnmi_bn_stats_partials_f32(const double* partials, int64_t G, in
                                            float momentum, float* mean, float* invstd, float* running_mean,
                                            float* running_var, int64_t* num_batches_tracked, void* stream) {
   if (partials == nullptr || mean == nullptr || invstd == nullptr || G <= 0 || G >= (int64_t(1) << 31) || rows <= 0 ||
-      C <= 0)
+      !pow2_ge4(C))
     return DRNMI_EINVAL;
   if ((running_mean == nullptr) != (running_var == nullptr)) return DRNMI_EINVAL;
   hipLaunchKernelGGL(bn_stats_final_kernel, dim3(fin_grid(C)), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),

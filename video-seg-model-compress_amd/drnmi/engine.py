@@ -559,7 +559,7 @@ def _fused_init_route(nd: ConvNode, cin_stride: int) -> bool:
         a.out_dtype, a.y_sp, a.y_sc = _lib.DRNMI_BF16, c.out_channels, 1
     a.tile, a.algo = -1, _lib.ALGO_IGEMM
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
-    return name is not None and name.decode().startswith(("conv_big", "conv_pp", "conv_halo", "conv_seg"))
+    return name is not None and name.decode().startswith(("conv_big", "conv_pp", "conv_halo"))
 
 
 def _conv_out(h, k, s, p, d):

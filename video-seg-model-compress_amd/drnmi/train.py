@@ -377,6 +377,8 @@ class TrainRunner:
             mean = torch.empty(cs, dtype=torch.float32, device=dev)
             invstd = torch.empty(cs, dtype=torch.float32, device=dev)
             if g_rows > 0:
+                # the epilogue wrote [2][g_rows][cout] partials (row stride = cout); cs == cout here
+                # (checked above), so the finalize reads them with the same channel count
                 _lib.check(lib.drnmi_bn_stats_partials_f32(
                     _vp(self._st_ws), g_rows, rows, cs, float(bn.eps), float(bn.momentum), _vp(mean), _vp(invstd),
                     _vp(bn.running_mean), _vp(bn.running_var), _vp(bn.num_batches_tracked), ctypes.c_void_p(stream)),
@@ -518,11 +520,12 @@ class TrainRunner:
             if self.grad_ready is not None and done:
                 self.grad_ready(done)
             # data gradient (not needed for the network input)
-            if nd.src != "input" and s == 2 and S2_CLASS_DGRAD and self._s2_classes(nd, st, dev, sp) is not None:
+            classes = (self._s2_classes(nd, st, dev, sp) if nd.src != "input" and s == 2 and S2_CLASS_DGRAD
+                       else None)
+            if classes is not None:
                 # stride 2: four parity-class convs of dy itself, no zero-inserted copy
                 cs_src = self.cstride[nd.src]
                 prev = grads.get(nd.src)
-                classes = self._s2_classes(nd, st, dev, sp)
                 if prev is not None:
                     out = prev
                 elif len(classes) < 4:          # pixels no tap reaches keep a zero gradient
