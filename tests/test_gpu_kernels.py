@@ -502,6 +502,35 @@ def test_stag_kernel_bit_identical(n, h, w, cin, cout, dil, with_res, fold):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout,dil,with_res", [
+    (2, 9, 256, 256, 256, 2, True), (1, 5, 512, 512, 512, 4, True), (2, 6, 256, 128, 256, 2, False),
+    (1, 4, 256, 512, 512, 1, False), (1, 2, 768, 256, 512, 1, True), (1, 3, 256, 128, 256, 3, True)])
+def test_w1_kernel_bit_identical(n, h, w, cin, cout, dil, with_res):
+    """conv_w1_kernel (tile 22: the stag256 tile as 4 waves of 128 x 128, one wave per SIMD, one
+    barrier per K step) == conv_stag_kernel (tile 19) bit for bit: same K order, same MFMA order per
+    accumulator, same accumulator start and epilogue.  Borders and dil 1..4 as in the strip test."""
+    g = torch.Generator().manual_seed(390 + h * w + cin)
+    x = torch.randn(n, h, w, cin, generator=g).bfloat16().to(DEV)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (9 * cout)) ** 0.5).to(DEV)
+    sc = (torch.rand(cout, generator=g) + 0.5).to(DEV)
+    sh = (torch.rand(cout, generator=g) - 0.5).to(DEV)
+    res = torch.randn(n, h, w, cout, generator=g).bfloat16().to(DEV) if with_res else None
+    kw = dict(stride=1, padding=dil, dilation=dil, relu=True, fold_scale=True)
+    a = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=19, **kw)
+    b = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=22, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
+def test_w1_kernel_refuses_unfolded_scale():
+    """tile 22 serves only the BN-scale-folded launches (accumulators start from shift + residual)."""
+    x = torch.randn(1, 4, 256, 256, device=DEV).bfloat16()
+    wt = torch.randn(256, 256, 3, 3, device=DEV) * 0.02
+    sc = torch.rand(256, device=DEV) + 0.5
+    with pytest.raises(RuntimeError, match="ENOTSUP"):
+        ops.conv2d_bn_act(x, wt, sc, None, None, padding=1, dilation=1, tile=22, fold_scale=False)
+
+
 @pytest.mark.parametrize("n,h,w,dil,with_res", [(2, 5, 256, 1, True), (1, 4, 512, 1, False), (1, 6, 256, 2, True)])
 def test_stag128_matches_halo_bit_identical(n, h, w, dil, with_res):
     """128 -> 128 3x3 (D-22 layer4) on the staggered 128-channel tile (conv_stag128_kernel, tile

@@ -660,9 +660,12 @@ hipError_t launch_strip(const drnmi_conv_args& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// Routing is fixed (no environment switches): auto-picked strip launches run conv_stag_kernel
-// when cin % 128 == 0 (measured 5-6 % faster, bit-identical), else conv_strip_kernel; the other
-// tiles stay reachable through an explicit drnmi_conv_args.tile for the bit-identity tests.
+// Routing is fixed (no environment switches): auto-picked strip launches run conv_w1_kernel (one
+// wave per SIMD, 128 x 128 per wave) when the launch is a plain 256-channel-block one with the
+// folded-scale bf16 epilogue (1-5 % faster than conv_stag on the D-22 layer5-8 shapes, bit-identical),
+// else conv_stag_kernel when cin % 128 == 0 (5-6 % faster than the strip tile, bit-identical),
+// else conv_strip_kernel; the other tiles stay reachable through an explicit drnmi_conv_args.tile
+// for the bit-identity tests.
 
 // a 256-pixel tile is a run of one output row, the strip of 256 + 2 dil rows fits its buffer
 bool strip_ok(const drnmi_conv_args& p) {
@@ -711,7 +714,14 @@ constexpr int kStrip = 14;  // conv_strip_kernel (tile id 18); auto routes varia
 constexpr int kStag = 15;   // conv_stag_kernel (tile id 19): the strip tile with staggered SIMD partners
 constexpr int kS2Row = 16;  // conv_s2row_kernel (tile id 20): stride-2 3x3 32 -> 64 / 64 -> 128, row walk
 constexpr int kS1X2Row = 17;  // conv_s1x2row_kernel (tile id 21): stride-1 3x3 64 -> 64 + 1x1 s2 downsample 32 -> 64
+constexpr int kW1 = 18;      // conv_w1_kernel (tile id 22): the stag256 tile as 4 waves of 128 x 128, one per SIMD
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+// conv_w1 (conv_w1.hip): the staggered tile's shapes without the fused downsample, 256-channel blocks
+bool w1_ok(const drnmi_conv_args& p) {
+  return stag_ok(p) && p.x2 == nullptr && p.cout % 256 == 0 && p.scale == nullptr && p.out_dtype == DRNMI_BF16 &&
+         p.y_sc == 1 && p.y_sp == p.cout && p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
+}
 
 template <int KS, bool PERSIST>
 hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
@@ -932,14 +942,24 @@ bool big_conv_supported(const drnmi_conv_args& p) {
 int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   if (variant == kS2Row || (variant < 0 && s2row_auto(p))) return s2row_conv_dispatch(p, s);
   if (variant == kS1X2Row || (variant < 0 && s1x2row_auto(p))) return s1x2row_conv_dispatch(p, s);
+  if (variant == kW1) {
+    if (!big_conv_supported(p) || !w1_ok(p)) return DRNMI_ENOTSUP;
+    const hipError_t e = launch_w1(p, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
   // the halo kernel (cin/cout 64-128) stays dense: it beats unit skipping on those shapes
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_dispatch(p, s);
   if (!big_conv_supported(p)) return DRNMI_ENOTSUP;
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
   if (auto_pick) {
-    if (stag_ok(p)) variant = kStag;
+    if (w1_ok(p)) variant = kW1;
+    else if (stag_ok(p)) variant = kStag;
     else if (variant == 1 && strip_ok(p)) variant = kStrip;
+  }
+  if (variant == kW1) {
+    const hipError_t e = launch_w1(p, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
   }
   if (variant == kStrip || variant == kStag) {
     if (variant == kStag ? !stag_ok(p) : (!strip_ok(p) || p.cin < 64)) return DRNMI_ENOTSUP;
@@ -980,13 +1000,16 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   if (variant == kS2Row || (variant < 0 && s2row_auto(p))) return s2row_conv_name(p);
   if (variant == kS1X2Row || (variant < 0 && s1x2row_auto(p))) return s1x2row_conv_name(p);
+  if (variant == kW1) return big_conv_supported(p) && w1_ok(p) ? "conv_w1_kernel" : nullptr;
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_name(p);
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
   if (auto_pick) {
-    if (stag_ok(p)) variant = kStag;
+    if (w1_ok(p)) variant = kW1;
+    else if (stag_ok(p)) variant = kStag;
     else if (variant == 1 && strip_ok(p)) variant = kStrip;
   }
+  if (variant == kW1) return "conv_w1_kernel";
   if (variant == kStag) {
     if (!stag_ok(p)) return nullptr;
     if (p.cout <= 128) return p.x2 != nullptr ? "conv_stag128_x2_kernel" : "conv_stag128_kernel";

@@ -1,0 +1,416 @@
+// One-wave-per-SIMD strip conv (bf16): conv_w1_kernel.  Own translation unit (its 400-register
+// allocation must not be perturbed by the other tiles, cdna_hip_programming.md §5.4 rule 19).
+//
+// Same tile (256 output channels x one 256-pixel run of an output row, 3x3 stride 1, cin % 128 ==
+// 0), same LDS image (two 32-KB weight stages, two 33-KB input strips; DMA'd as in conv_stag), same
+// K order and per-accumulator MFMA order as conv_stag_kernel -- so the output is bit-identical to
+// it -- but 4 waves of 128 channels x 128 pixels instead of 8 waves of 128 x 64:
+//
+//   * per 32-deep substep a wave reads 8 A + 8 B fragments (16 KB) for 64 MFMAs; the 8-wave tile
+//     reads 8 A + 4 B per wave for 32 MFMAs, so the LDS read bytes per MFMA drop by a third (the
+//     chip holds its clock under load: LDS read energy per MFMA is one of the levers,
+//     cdna_hip_programming.md §5.4 rule 28);
+//   * accumulators 8 x 8 x 4 = 256 registers (AGPRs), fragments double-buffered (128 VGPRs);
+//   * with no partner wave to fill the matrix pipe, each wave hides its own latencies: one barrier
+//     per K step, placed in the middle of the second substep (the MFMAs before it drain while the
+//     waves meet), every LDS read issued at least two MFMA groups before its use (counted
+//     lgkmcnt), every DMA piece issued a whole K step before the barrier that publishes it.
+//
+// Schedule of K step t (stage t & 1, strip buffer g & 1, t = 3 g + kw), B_t = the barrier that
+// publishes step t's weights (and, for kw = 0, group g's strip):
+//   X  groups 0..7 (substep 0): wait for a0[fm] (all b0 landed), issue 2 reads of substep 1
+//      (b1[0..7] first, then a1[0..7]), 8 MFMAs acc[fm][*] += a0[fm] x b0[*];
+//   Y  groups 0..3 (substep 1): wait for a1[fm], 8 MFMAs;
+//      vmcnt(0) lgkmcnt(0) s_barrier = B_{t+1}: every wave's DMA for step t + 1 has landed and
+//      every wave has finished reading stage t & 1 and (kw = 2) strip g;
+//   Y  groups 4..7: issue the 16 reads of step t + 1's substep 0 (b0 first) and the DMA of step
+//      t + 2's weights (into stage t & 1, just released; past the last step a re-fetch) and of one
+//      third of the next strip
+//      (group g' + 1 for t + 1 = 3 g' + k': its buffer was last read in step 3 g' - 1, before
+//      B_{3 g'}); 8 MFMAs each.
+// Reference: lmodels/drn.py:27-29 (conv3x3, dilation = padding), :49-65 (BasicBlock convs).
+#include "common.h"
+#include "conv_tile.h"
+#include "kernels.h"
+
+namespace drnmi {
+namespace {
+
+// 2 A stages + 2 strips (130 KB) + 1 KB sink: the strip pieces past the strip (share 8 of waves
+// 1-3) land there, so every wave issues the same DMA sequence without a branch
+constexpr int kW1Sink = 2 * 256 * 128 + 2 * kStripBytes;
+constexpr int kW1Lds = kW1Sink + 1024;
+
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+conv_w1_kernel(const drnmi_conv_args p) {
+  constexpr int BK = 64, FM = 8, FN = 8, WCO = 128, BCO = 256, CE = 8, ESZ = 2;
+  constexpr int AB = BCO * 128;                      // 32 KB per A stage
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wave >> 1;                          // channel half (128 channels)
+  const int wp = wave & 1;                           // pixel half (128 pixels)
+  const int M = p.n * p.ho * p.wo;
+  const int hw_o = p.ho * p.wo;
+  const int nco = (p.cout + BCO - 1) / BCO;
+  const int ntiles = (M / kBPX) * nco;
+  const int cin = p.cin;
+  const int lc = 31 - __builtin_clz(cin);
+  const int H = p.h, W = p.w, dil = p.dil;
+  const int nk = 9 * cin / BK;
+  const int ngroups = nk / 3;                        // even: cin % 128 == 0
+  const int fr = lane & 15;
+  const int fq = lane >> 4;
+  const int lrow = lane >> 3;
+  const int lslot = lane & 7;
+
+  const int tile = xcd_remap2(blockIdx.x, ntiles);   // XCD-major deal, as conv_stag
+  const int px0 = (tile / nco) * kBPX;
+  const int co0 = (tile % nco) * BCO;
+  const int s_n = px0 / hw_o;
+  const int s_q = px0 - s_n * hw_o;
+  const int s_oh = s_q / p.wo;
+  const int s_ow0 = s_q - s_oh * p.wo;
+  const int xbytes = p.n * H * W * cin * ESZ;        // < 2^31 (big_conv_supported)
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.x), 0, xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(p.wgt), 0, p.cout_pad * p.k_pad * ESZ, 0x00020000);
+  typedef __attribute__((address_space(3))) void lds_t;
+  auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, int soff, int lds_byte) __attribute__((always_inline)) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, 0);
+  };
+  // weight piece i (rows (wave*8 + i)*8 .. +8, 1 KB) of K step kt; the swizzle depends on i only
+  // through its parity
+  uint32_t a_off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (wave * 8 + i) * 8 + lrow;
+    a_off[i] = ((co0 + r) * p.k_pad + swzb<128>(r, lslot) * CE) * ESZ;
+  }
+  constexpr uint32_t kOOB = 0x80000000u;             // beyond every buffer (sizes < 2^31)
+  auto issue_a = [&](int kt, int stage, int i) __attribute__((always_inline)) {
+    const int cb = kt / 9;
+    const int tap = kt - cb * 9;
+    const int k0 = (tap << lc) + cb * BK;
+    dma(rs_w, a_off[i & 1], ((i & ~1) * 8 * p.k_pad + k0) * ESZ, stage * AB + (wave * 8 + i) * 1024);
+  };
+  // strip share sh (0..8) of group g (channel block g / 3, tap row g % 3): piece j = wave + 4 sh
+  auto issue_strip = [&](int g, int buf, int sh) __attribute__((always_inline)) {
+    const int j = wave + 4 * sh;
+    if (j >= kStripPieces) return;                   // wave-uniform
+    const int R = j * 8 + lrow;
+    const int cb = g / 3, kh = g - cb * 3;
+    const int ih = s_oh - p.pad + kh * dil;
+    const int iw = s_ow0 - p.pad + R;
+    const bool ok = R < kBPX + 2 * dil && static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+    const bool row_ok = static_cast<unsigned>(ih) < static_cast<unsigned>(H);   // wave-uniform
+    const uint32_t voff = ok && row_ok ? static_cast<uint32_t>((iw * cin + (lslot ^ (R & 7)) * CE) * ESZ) : kOOB;
+    const int soff = row_ok ? ((s_n * H + ih) * W * cin + cb * BK) * ESZ : 0;
+    dma(rs_x, voff, soff, 2 * AB + buf * kStripBytes + j * 1024);
+  };
+
+  // fragment-read byte offsets (the swizzles of a lane group's 16 rows do not depend on the
+  // fragment index): A rows wc*128 + 16 fm + fr, B strip rows wp*128 + 16 fn + fr + kw*dil
+  uint32_t a_base[2], b_base[3][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = wc * WCO + fr;
+    a_base[u] = r * 128 + (swzb<128>(r, u * 4 + fq) << 4);
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int R = wp * 128 + fr + kw * dil;
+      b_base[kw][u] = 2 * AB + R * 128 + (((u * 4 + fq) ^ (R & 7)) << 4);
+    }
+  }
+
+  f32x4 acc[FM][FN];
+  bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+  // The MFMAs are inline asm with the accumulator as an AGPR operand: the 256 accumulator
+  // registers stay in the AGPR file for the whole loop (compiler-selected MFMAs shuffled them
+  // between the files and spilled: the 128 fragment VGPRs plus addressing leave no room for a
+  // second copy).  Hand-placed waits cover the hazards the compiler cannot see through asm: the
+  // accumulators are written by v_accvgpr_write before the first MFMA (s_nop after the init) and
+  // read by the epilogue after the last one (s_nop after the loop); consecutive MFMAs on one
+  // accumulator are 64 MFMAs apart.
+  auto mma = [&](f32x4& c, const bf16x8& a, const bf16x8& b) __attribute__((always_inline)) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  };
+  auto rd = [&](bf16x8& dst, uint32_t base, auto off_c) __attribute__((always_inline)) {
+    constexpr int OFF = decltype(off_c)::value;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(OFF));
+  };
+  // read n of a substep's list (b[0..7] then a[0..7]) of stage ST / strip buffer BF / tap column KW
+  auto rd_item = [&](bf16x8 (&a)[FM], bf16x8 (&b)[FN], auto n_c, auto st_c, auto bf_c, auto kw_c, auto u_c)
+                     __attribute__((always_inline)) {
+    constexpr int N = decltype(n_c)::value, ST = decltype(st_c)::value, BF = decltype(bf_c)::value;
+    constexpr int KW = decltype(kw_c)::value, U = decltype(u_c)::value;
+    if constexpr (N < 8) rd(b[N], b_base[KW][U], std::integral_constant<int, BF * kStripBytes + N * 2048>{});
+    else rd(a[N - 8], a_base[U], std::integral_constant<int, ST * AB + (N - 8) * 2048>{});
+  };
+
+  // accumulator start: shift (+ residual), as conv_stag's split_init (the dispatch, w1_ok, admits
+  // only BN-scale-folded launches with a dense bf16 NHWC output: shift + residual start the
+  // accumulators, the epilogue is store_tile_x4); loads before the prologue DMA
+  {
+    uint4 rv[FM / 2][FN];
+    float4 shv[FM];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) shv[fm] = *reinterpret_cast<const float4*>(p.shift + co0 + wc * WCO + fm * 16 + fq * 4);
+    if (p.res != nullptr) load_residual<FM, WCO, FN>(p, rv, px0, co0, wc, wp, fr, fq);
+    // prologue: step 0's weights and group 0's whole strip
+#pragma unroll
+    for (int i = 0; i < 8; ++i) issue_a(0, 0, i);
+#pragma unroll
+    for (int sh = 0; sh < 9; ++sh) issue_strip(0, 0, sh);
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) acc[fm][fn] = f32x4{shv[fm].x, shv[fm].y, shv[fm].z, shv[fm].w};
+    if (p.res != nullptr) add_residual(acc, rv, fr);
+  }
+  // the accumulator starts are in their AGPRs before the wait states below (an empty asm that
+  // redefines each one: the compiler cannot sink a v_accvgpr_write past it to just before the
+  // first MFMA, whose hazard it cannot see through the asm)
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+a"(acc[fm][fn]));
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");   // B_0
+  __builtin_amdgcn_sched_barrier(0);
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using F = std::false_type;
+  using T_ = std::true_type;
+  // after B_0: step 0's substep-0 fragments (b0 first), step 1's weights (stage 1), share set 0
+  // of group 1's strip (buffer 1)
+  {
+    auto r16 = [&](auto n_c) __attribute__((always_inline)) { rd_item(a0, b0, n_c, I0{}, I0{}, I0{}, I0{}); };
+    r16(std::integral_constant<int, 0>{});  r16(std::integral_constant<int, 1>{});
+    r16(std::integral_constant<int, 2>{});  r16(std::integral_constant<int, 3>{});
+    r16(std::integral_constant<int, 4>{});  r16(std::integral_constant<int, 5>{});
+    r16(std::integral_constant<int, 6>{});  r16(std::integral_constant<int, 7>{});
+    r16(std::integral_constant<int, 8>{});  r16(std::integral_constant<int, 9>{});
+    r16(std::integral_constant<int, 10>{}); r16(std::integral_constant<int, 11>{});
+    r16(std::integral_constant<int, 12>{}); r16(std::integral_constant<int, 13>{});
+    r16(std::integral_constant<int, 14>{}); r16(std::integral_constant<int, 15>{});
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) issue_a(1, 1, i);
+#pragma unroll
+  for (int sh = 0; sh < 3; ++sh) issue_strip(1, 1, sh);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // K step t = 3 g + KW of strip buffer GP; LAST: the final step (no barrier, reads or DMA after it)
+  // one MFMA group: acc[FMI][0..7] += a[FMI] x b[0..7], with fill(k) issued in the gap after MFMA k
+  // (k = 0..6): with one wave per SIMD every other instruction of the step must sit in the shadow
+  // of an MFMA (a 16-cycle issue gap holds about three), or the matrix pipe idles while it issues
+  auto mgroup = [&](auto fm_c, bf16x8 (&a)[FM], bf16x8 (&b)[FN], auto&& fill) __attribute__((always_inline)) {
+    constexpr int FMI = decltype(fm_c)::value;
+    mma(acc[FMI][0], a[FMI], b[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    fill(std::integral_constant<int, 0>{});
+    __builtin_amdgcn_sched_barrier(0);
+    mma(acc[FMI][1], a[FMI], b[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    fill(std::integral_constant<int, 1>{});
+    __builtin_amdgcn_sched_barrier(0);
+    mma(acc[FMI][2], a[FMI], b[2]);
+    __builtin_amdgcn_sched_barrier(0);
+    fill(std::integral_constant<int, 2>{});
+    __builtin_amdgcn_sched_barrier(0);
+    mma(acc[FMI][3], a[FMI], b[3]);
+    __builtin_amdgcn_sched_barrier(0);
+    fill(std::integral_constant<int, 3>{});
+    __builtin_amdgcn_sched_barrier(0);
+    mma(acc[FMI][4], a[FMI], b[4]);
+    __builtin_amdgcn_sched_barrier(0);
+    fill(std::integral_constant<int, 4>{});
+    __builtin_amdgcn_sched_barrier(0);
+    mma(acc[FMI][5], a[FMI], b[5]);
+    __builtin_amdgcn_sched_barrier(0);
+    fill(std::integral_constant<int, 5>{});
+    __builtin_amdgcn_sched_barrier(0);
+    mma(acc[FMI][6], a[FMI], b[6]);
+    __builtin_amdgcn_sched_barrier(0);
+    fill(std::integral_constant<int, 6>{});
+    __builtin_amdgcn_sched_barrier(0);
+    mma(acc[FMI][7], a[FMI], b[7]);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // A fragment set stays allocated until the end of the phase that consumes it (a use the compiler
+  // sees): a read issued in the shadow of an MFMA must never be given the registers of that
+  // MFMA's own operands (the compiler would reuse them right after their last asm use, while the
+  // MFMA may still be reading them); the new reads take the registers of the previous generation
+  auto keep = [&](bf16x8 (&a)[FM], bf16x8 (&b)[FN]) __attribute__((always_inline)) {
+    asm volatile("" :: "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]));
+    asm volatile("" :: "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]));
+  };
+  // weight-piece offsets of the 4 row pairs (i & ~1) * 8 rows, in SGPRs for the loop
+  const int a_row = 16 * p.k_pad * ESZ;              // byte offset of 2 x 8 weight rows
+
+  // K step t = 3 g + KW of strip buffer GP; LAST: the final step (no barrier, reads or DMA after it)
+  auto step = [&](auto kw_c, auto gp_c, auto last_c, int g) __attribute__((always_inline)) {
+    constexpr int KW = decltype(kw_c)::value;
+    constexpr int GP = decltype(gp_c)::value;
+    constexpr bool LAST = decltype(last_c)::value;
+    constexpr int ST = (GP + KW) & 1;                // stage of step t
+    constexpr int KWN = KW == 2 ? 0 : KW + 1;        // step t + 1: tap column, strip buffer
+    constexpr int GPN = KW == 2 ? GP ^ 1 : GP;
+    constexpr int SGB = KW == 2 ? GP : GP ^ 1;       // buffer of the strip DMA'd after B_{t+1}
+    const int t = 3 * g + KW;
+    using IST = std::integral_constant<int, ST>;
+    using IKW = std::integral_constant<int, KW>;
+    using IGP = std::integral_constant<int, GP>;
+    auto nofill = [](auto) {};
+    // ---- X: substep 0; the substep-1 reads (b1 first) in the first two gaps of each group
+    auto xgroup = [&](auto fm_c) __attribute__((always_inline)) {
+      constexpr int FMI = decltype(fm_c)::value;
+      asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(7 + FMI) : "memory");   // a0[FMI] (b0 already)
+      __builtin_amdgcn_sched_barrier(0);
+      mgroup(fm_c, a0, b0, [&](auto k_c) __attribute__((always_inline)) {
+        constexpr int KK = decltype(k_c)::value;
+        if constexpr (KK < 2) rd_item(a1, b1, std::integral_constant<int, 2 * FMI + KK>{}, IST{}, IGP{}, IKW{}, I1{});
+      });
+    };
+    xgroup(std::integral_constant<int, 0>{});
+    xgroup(std::integral_constant<int, 1>{});
+    xgroup(std::integral_constant<int, 2>{});
+    xgroup(std::integral_constant<int, 3>{});
+    xgroup(std::integral_constant<int, 4>{});
+    xgroup(std::integral_constant<int, 5>{});
+    xgroup(std::integral_constant<int, 6>{});
+    xgroup(std::integral_constant<int, 7>{});
+    keep(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- Y: substep 1.  The scalars of the DMA after B_{t+1} (t + 1 = 3 g' + k': step t + 2's
+    // weights into stage ST, share set k' of group g' + 1's strip into buffer SGB) are computed in
+    // the head groups' gaps and pinned there
+    const int gn = KW == 2 ? g + 1 : g;              // g'
+    int sa = 0, ss = 0, s_ok = 0;
+    auto ygroup_head = [&](auto fm_c) __attribute__((always_inline)) {
+      constexpr int FMI = decltype(fm_c)::value;
+      asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(7 - FMI) : "memory");   // a1[FMI] (b1 already)
+      __builtin_amdgcn_sched_barrier(0);
+      mgroup(fm_c, a1, b1, [&](auto k_c) __attribute__((always_inline)) {
+        constexpr int KK = decltype(k_c)::value;
+        if constexpr (!LAST && FMI == 0 && KK == 1) {
+          const int kt = t + 2 < nk ? t + 2 : nk - 1;   // past the end: re-fetch into the idle stage
+          const int cb = kt / 9;
+          sa = __builtin_amdgcn_readfirstlane((((kt - cb * 9) << lc) + cb * BK) * ESZ);
+          __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (!LAST && FMI == 0 && KK == 3) {
+          const int g2 = gn + 1 < ngroups ? gn + 1 : ngroups - 1;   // past the end: a buffer never read again
+          const int cb = g2 / 3, kh = g2 - cb * 3;
+          const int ih = s_oh - p.pad + kh * dil;
+          s_ok = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(ih) < static_cast<unsigned>(H) ? 1 : 0);
+          ss = __builtin_amdgcn_readfirstlane(s_ok ? ((s_n * H + ih) * W * cin + cb * BK) * ESZ : 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
+    };
+    ygroup_head(std::integral_constant<int, 0>{});
+    ygroup_head(std::integral_constant<int, 1>{});
+    ygroup_head(std::integral_constant<int, 2>{});
+    ygroup_head(std::integral_constant<int, 3>{});
+    if constexpr (LAST) {
+      ygroup_head(std::integral_constant<int, 4>{});
+      ygroup_head(std::integral_constant<int, 5>{});
+      ygroup_head(std::integral_constant<int, 6>{});
+      ygroup_head(std::integral_constant<int, 7>{});
+      (void)nofill;
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_{t+1}
+      __builtin_amdgcn_sched_barrier(0);
+      using ISTN = std::integral_constant<int, ST ^ 1>;
+      using IKWN = std::integral_constant<int, KWN>;
+      using IGPN = std::integral_constant<int, GPN>;
+      // 27 items over the 28 gaps of groups 4..7: b0[0..7] alternating with the 8 weight pieces,
+      // then a0[0..7] with the 3 strip pieces after the first three
+      auto item = [&](auto n_c) __attribute__((always_inline)) {
+        constexpr int N = decltype(n_c)::value;
+        if constexpr (N < 16) {
+          if constexpr (N % 2 == 0) {
+            rd_item(a0, b0, std::integral_constant<int, N / 2>{}, ISTN{}, IGPN{}, IKWN{}, I0{});
+          } else {
+            constexpr int I = N / 2;
+            dma(rs_w, a_off[I & 1], sa + (I >> 1) * a_row, ST * AB + (wave * 8 + I) * 1024);
+          }
+        } else if constexpr (N < 22) {
+          if constexpr (N % 2 == 0) {
+            rd_item(a0, b0, std::integral_constant<int, 8 + (N - 16) / 2>{}, ISTN{}, IGPN{}, IKWN{}, I0{});
+          } else {
+            constexpr int SH = (N - 17) / 2;               // 0..2 of the share set
+            const int sh = 3 * KWN + SH;
+            const int j = wave + 4 * sh;
+            // branch-free: a piece past the strip (j >= 33: share 8 of waves 1-3) reads nothing and
+            // lands in the sink
+            const bool inside = j < kStripPieces;
+            const int R = j * 8 + lrow;
+            const int iw = s_ow0 - p.pad + R;
+            const bool ok = inside && s_ok && R < kBPX + 2 * dil && static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+            const uint32_t voff = ok ? static_cast<uint32_t>((iw * cin + (lslot ^ (R & 7)) * CE) * ESZ) : kOOB;
+            dma(rs_x, voff, ss, inside ? 2 * AB + SGB * kStripBytes + j * 1024 : kW1Sink);
+          }
+        } else {
+          rd_item(a0, b0, std::integral_constant<int, 11 + (N - 22)>{}, ISTN{}, IGPN{}, IKWN{}, I0{});
+        }
+      };
+      auto ygroup_tail = [&](auto fm_c) __attribute__((always_inline)) {
+        constexpr int FMI = decltype(fm_c)::value;
+        constexpr int N0 = 7 * (FMI - 4);
+        mgroup(fm_c, a1, b1, [&](auto k_c) __attribute__((always_inline)) {
+          constexpr int N = N0 + decltype(k_c)::value;
+          if constexpr (N < 27) item(std::integral_constant<int, N>{});
+        });
+      };
+      ygroup_tail(std::integral_constant<int, 4>{});
+      ygroup_tail(std::integral_constant<int, 5>{});
+      ygroup_tail(std::integral_constant<int, 6>{});
+      ygroup_tail(std::integral_constant<int, 7>{});
+    }
+    keep(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto group = [&](auto gp_c, auto lastg_c, int g) __attribute__((always_inline)) {
+    step(I0{}, gp_c, F{}, g);
+    step(I1{}, gp_c, F{}, g);
+    step(I2{}, gp_c, lastg_c, g);
+  };
+  for (int g = 0; g < ngroups - 2; g += 2) {
+    group(I0{}, F{}, g);
+    group(I1{}, F{}, g + 1);
+  }
+  group(I0{}, F{}, ngroups - 2);
+  group(I1{}, T_{}, ngroups - 1);
+  // the last MFMAs' results: wait states, then an empty asm that redefines every accumulator, so
+  // no epilogue read of an AGPR can be scheduled before the wait (the compiler had hoisted the
+  // read of acc[1][0] to right after its last MFMA, which it does not know is one: that read
+  // missed the final K step)
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+#pragma unroll
+  for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+a"(acc[fm][fn]));
+  store_tile_x4<FM, WCO, FN>(p, acc, px0, co0, wc, wp, fr, fq);
+}
+
+}  // namespace
+
+hipError_t launch_w1(const drnmi_conv_args& p, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_w1_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kW1Lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const dim3 grid(static_cast<unsigned>((M / kBPX) * ((p.cout + 255) / 256)));
+  hipLaunchKernelGGL(conv_w1_kernel, grid, dim3(256), kW1Lds, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace drnmi
