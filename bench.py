@@ -372,7 +372,8 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
     names = [launched_name(i) for i in range(len(plan.args))]
     path = plan.labels_path()
     if path == "seg2":                         # the seg classifier in the last conv's epilogue (drnmi_conv_stag_seg)
-        names[plan.seg_fused["conv"]] = "conv_i8_stag_seg_kernel" if plan.seg_fused["i8"] else "conv_stag_seg_kernel"
+        names[plan.seg_fused["conv"]] = lib.drnmi_conv_stag_seg_kernel_name(
+            ctypes.byref(plan.args[plan.seg_fused["conv"]])).decode()
         names[plan.seg_idx] = ""
     # the head launch (index len(nodes), DRNSeg._segment_impl): up x8 + argmax -> uint8 labels
     # (ops.hip drnmi_up8_labels_seg2 / _seg2_i8 / _nhwc launch the tiled uniform-window kernel; NCHW

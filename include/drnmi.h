@@ -295,6 +295,8 @@ int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const float* up_w, vo
  * seg_scale[k] + seg_shift[k] (drnmi_up8_labels_seg2_i8). */
 int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, int32_t seg_k_pad, int32_t seg_rows,
                         void* partials, void* stream);
+/* The kernel drnmi_conv_stag_seg launches for these arguments (as rocprofv3 names it), or NULL. */
+const char* drnmi_conv_stag_seg_kernel_name(const drnmi_conv_args* a);
 
 /* Labels from those partials: logit[k] = (bias[k] + partial_0[k]) + partial_1[k] (bias: >= cs
  * floats), then the labels-only head's arithmetic (drnmi_up8_labels_nhwc).  partials: [2][n][h][w][cs]. */

@@ -217,6 +217,34 @@ def test_segment_seg_fused_into_last_conv(arch, n):
     assert agree >= 0.9995
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_seg_fused_w1_matches_stag_bit_identical(n):
+    """The seg-fused layer8 launch on the one-wave-per-SIMD tile (conv_w1_seg_kernel, the default)
+    == the staggered tile's (conv_stag_seg_kernel, forced with tile 19): same K order and MFMA order
+    per accumulator, the same seg MFMAs per partial and the same wc 0 + wc 1 order, so the partial
+    logits are equal bit for bit."""
+    m = drnseg.build("drn_d_22", 19, seed=7, device=torch.device(DEV), precision="bf16").eval()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    frames = torch.randint(0, 256, (n, 1024, 2048, 3), dtype=torch.uint8, device=DEV, generator=g)
+    got = m.segment(frames, INFO_MEAN, INFO_STD, False).clone()
+    plan = next(iter(m._plans.values()))
+    assert plan.labels_path() == "seg2"
+    j = plan.seg_fused["conv"]
+    lib = _lib.load()
+    assert lib.drnmi_conv_stag_seg_kernel_name(ctypes.byref(plan.args[j])).decode() == "conv_w1_seg_kernel"
+    part_w1 = plan.bufs["seg_part"].clone()
+    plan.args[j].tile = 19
+    try:
+        assert lib.drnmi_conv_stag_seg_kernel_name(ctypes.byref(plan.args[j])).decode() == "conv_stag_seg_kernel"
+        ref = m.segment(frames, INFO_MEAN, INFO_STD, False)
+        part_stag = plan.bufs["seg_part"].clone()
+    finally:
+        plan.args[j].tile = -1
+    torch.cuda.synchronize()
+    assert torch.equal(part_w1, part_stag)
+    assert torch.equal(got, ref)
+
+
 def test_segment_labels_nhwc_identical_int8():
     """int8 nets (C5): the int8 seg conv writes the same fp32 values as NHWC rows (store_tile_i8's
     16-B path) -- labels identical to the NCHW-planes head."""

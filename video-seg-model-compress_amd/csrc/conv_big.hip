@@ -1092,6 +1092,14 @@ extern "C" int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, 
   if (!(big_conv_supported(p) && stag_ok(p)) || p.x2 != nullptr ||
       p.scale != nullptr || p.res != nullptr || p.cout % 256 != 0 || p.cout_pad < p.cout)
     return DRNMI_ENOTSUP;
-  const hipError_t e = launch_stag_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream));
+  // the one-wave-per-SIMD tile (conv_w1_seg_kernel); tile 19 forces the staggered one (the same
+  // partial logits, bit for bit: the bit-identity test)
+  const hipError_t e = p.tile == 4 + kStag ? launch_stag_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream))
+                                           : launch_w1_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream));
   return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+}
+
+extern "C" const char* drnmi_conv_stag_seg_kernel_name(const drnmi_conv_args* a) {
+  if (a == nullptr) return nullptr;
+  return a->dtype == DRNMI_I8 ? "conv_i8_stag_seg_kernel" : a->tile == 4 + kStag ? "conv_stag_seg_kernel" : "conv_w1_seg_kernel";
 }

@@ -41,8 +41,19 @@ namespace {
 constexpr int kW1Sink = 2 * 256 * 128 + 2 * kStripBytes;
 constexpr int kW1Lds = kW1Sink + 1024;
 
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
-conv_w1_kernel(const drnmi_conv_args p) {
+// SEGF (the labels-only video path's last conv, drnmi_conv_stag_seg): the activation is not stored;
+// as in conv_stag's SEGF epilogue it becomes the B operand of the seg classifier (1x1 512 -> 19 +
+// bias, lmodels/drnseg.py:278-284) and each 256-channel block writes partial logits
+// part[block][pixel][20] (wc 0 + wc 1, bias added by the head)
+struct W1Seg {
+  const void* w;        // seg weights, packed bf16 [>= 32 rows][k_pad] (scale folded), rows 19.. zero
+  int k_pad;
+  void* part;           // fp32 [cout / 256][n ho wo][20]
+};
+constexpr int kW1SegCS = 20;
+
+template <bool SEGF>
+__device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1Seg& sf) {
   constexpr int BK = 64, FM = 8, FN = 8, WCO = 128, BCO = 256, CE = 8, ESZ = 2;
   constexpr int AB = BCO * 128;                      // 32 KB per A stage
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -394,19 +405,120 @@ conv_w1_kernel(const drnmi_conv_args p) {
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+a"(acc[fm][fn]));
-  store_tile_x4<FM, WCO, FN>(p, acc, px0, co0, wc, wp, fr, fq);
+  if constexpr (!SEGF) {
+    store_tile_x4<FM, WCO, FN>(p, acc, px0, co0, wc, wp, fr, fq);
+  } else {
+    // the activation as store_tile_x4 would store it (ReLU, RNE to bf16, 16-B pieces: lane (fr, fq)
+    // holds channels 8 s(fq) .. +7 of 32-channel group f2 of pixel fr) times the matching seg weight
+    // columns, the same MFMA order per partial as conv_stag's SEGF: the same partial logits
+    bf16x8 aw[2][FM / 2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int f2 = 0; f2 < FM / 2; ++f2)
+        aw[mt][f2] = *reinterpret_cast<const bf16x8*>(static_cast<const uint16_t*>(sf.w) +
+                                                      static_cast<int64_t>(16 * mt + fr) * sf.k_pad + co0 + wc * WCO +
+                                                      32 * f2 + chunk_of_row(fq) * 8);
+    const bool relu = p.relu != 0;
+    f32x4 pacc[2][FN];
+#pragma unroll
+    for (int fn = 0; fn < FN; ++fn) {
+      pacc[0][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      pacc[1][fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int f2 = 0; f2 < FM / 2; ++f2) {
+        uint32_t w[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v[4] = {acc[2 * f2 + h][fn][0], acc[2 * f2 + h][fn][1], acc[2 * f2 + h][fn][2], acc[2 * f2 + h][fn][3]};
+          if (relu) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+          }
+          w[2 * h] = static_cast<uint32_t>(f32_to_bf16(v[0])) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+          w[2 * h + 1] = static_cast<uint32_t>(f32_to_bf16(v[2])) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+        }
+        uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
+        swap_halves(o);
+        const bf16x8 b = __builtin_bit_cast(bf16x8, o);
+        pacc[0][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0][f2], b, pacc[0][fn], 0, 0, 0);
+        pacc[1][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1][f2], b, pacc[1][fn], 0, 0, 0);
+      }
+    }
+    // the two channel halves (wc 0 + wc 1) through LDS stage 1 (32 KB): the last steps' clamped
+    // re-fetches target stage 0 and strip buffer 0 (nk and the group count are even), and every
+    // wave is past its last fragment read after the barrier
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float4* xch = reinterpret_cast<float4*>(smem + AB) + (wp * 64 + lane) * (2 * FN);
+    if (wc == 1) {
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          xch[mt * FN + fn] = make_float4(pacc[mt][fn][0], pacc[mt][fn][1], pacc[mt][fn][2], pacc[mt][fn][3]);
+    }
+    __syncthreads();
+    if (wc == 0) {
+      float* __restrict__ part = static_cast<float*>(sf.part) + static_cast<int64_t>(co0 / BCO) * M * kW1SegCS;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int cls = 16 * mt + 4 * fq;
+        if (cls >= kW1SegCS) continue;
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+          const float4 o = xch[mt * FN + fn];
+          const int64_t m = px0 + wp * 128 + fn * 16 + fr;
+          *reinterpret_cast<float4*>(part + m * kW1SegCS + cls) =
+              make_float4(pacc[mt][fn][0] + o.x, pacc[mt][fn][1] + o.y, pacc[mt][fn][2] + o.z, pacc[mt][fn][3] + o.w);
+        }
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+conv_w1_kernel(const drnmi_conv_args p) {
+  conv_w1_body<false>(p, W1Seg{nullptr, 0, nullptr});
+}
+
+struct W1SegArgs {
+  drnmi_conv_args p;
+  W1Seg sf;
+};
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+conv_w1_seg_kernel(const W1SegArgs a) {
+  conv_w1_body<true>(a.p, a.sf);
 }
 
 }  // namespace
 
-hipError_t launch_w1(const drnmi_conv_args& p, hipStream_t s) {
+static hipError_t w1_attrs() {
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_w1_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kW1Lds);
-    if (e != hipSuccess) return e;
+    for (const void* f : {reinterpret_cast<const void*>(&conv_w1_kernel), reinterpret_cast<const void*>(&conv_w1_seg_kernel)}) {
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kW1Lds);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
+  return hipSuccess;
+}
+
+hipError_t launch_w1_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_pad, void* part, hipStream_t s) {
+  const hipError_t e = w1_attrs();
+  if (e != hipSuccess) return e;
+  W1SegArgs a;
+  a.p = p;
+  a.sf = W1Seg{seg_w, seg_k_pad, part};
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  hipLaunchKernelGGL(conv_w1_seg_kernel, dim3(static_cast<unsigned>((M / kBPX) * ((p.cout + 255) / 256))), dim3(256),
+                     kW1Lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_w1(const drnmi_conv_args& p, hipStream_t s) {
+  const hipError_t e0 = w1_attrs();
+  if (e0 != hipSuccess) return e0;
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const dim3 grid(static_cast<unsigned>((M / kBPX) * ((p.cout + 255) / 256)));
   hipLaunchKernelGGL(conv_w1_kernel, grid, dim3(256), kW1Lds, s, p);

@@ -85,6 +85,7 @@ SIGNATURES = {
     "drnmi_up8_labels_nhwc": (ctypes.c_int, [_VP, _I32, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_up8_labels_seg2": (ctypes.c_int, [_VP, _I32, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_conv_stag_seg": (ctypes.c_int, [ctypes.POINTER(ConvArgs), _VP, _I32, _I32, _VP, _VP]),
+    "drnmi_conv_stag_seg_kernel_name": (ctypes.c_char_p, [ctypes.POINTER(ConvArgs)]),
     "drnmi_up8_labels_seg2_i8": (ctypes.c_int, [_VP, _I32, _VP, _VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_up8_bilinear_logsoftmax_argmax": (ctypes.c_int, [_VP, _VP, _VP, _I32, _I32, _I32, _I32, _I32, _VP]),
     "drnmi_resize_workspace_bytes": (ctypes.c_int64, [_I32, _I32, _I32, _I32, _I32, _I32]),
