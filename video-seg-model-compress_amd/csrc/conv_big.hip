@@ -661,8 +661,7 @@ hipError_t launch_strip(const drnmi_conv_args& p, hipStream_t s) {
 }
 
 // Routing is fixed (no environment switches): auto-picked strip launches run conv_w1_kernel (one
-// wave per SIMD, 128 x 128 per wave) when the launch is a plain 256-channel-block one with the
-// folded-scale bf16 epilogue (1-5 % faster than conv_stag on the D-22 layer5-8 shapes, bit-identical),
+// wave per SIMD, 128 x 128 per wave, bit-identical) on the long-K residual-free launches (w1_auto),
 // else conv_stag_kernel when cin % 128 == 0 (5-6 % faster than the strip tile, bit-identical),
 // else conv_strip_kernel; the other tiles stay reachable through an explicit drnmi_conv_args.tile
 // for the bit-identity tests.
@@ -722,6 +721,11 @@ bool w1_ok(const drnmi_conv_args& p) {
   return stag_ok(p) && p.x2 == nullptr && p.cout % 256 == 0 && p.scale == nullptr && p.out_dtype == DRNMI_BF16 &&
          p.y_sc == 1 && p.y_sp == p.cout && p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
 }
+// auto-routed where it measured no slower inside the network (same-box interleaved bench A/B,
+// profiles/r10m_w1_ab): the long-K residual-free launches (D-22 layer6.1 conv1, layer7).  At
+// cin 128 / 256 (18 / 36 K steps) and with a residual its per-tile prologue and epilogue, issued
+// by 4 waves instead of 8, cost more than the loop saves (layer5.0 conv1 145 vs 130 us)
+bool w1_auto(const drnmi_conv_args& p) { return w1_ok(p) && p.cin >= 512 && p.res == nullptr; }
 
 template <int KS, bool PERSIST>
 hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
@@ -953,7 +957,7 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
   if (auto_pick) {
-    if (w1_ok(p)) variant = kW1;
+    if (w1_auto(p)) variant = kW1;
     else if (stag_ok(p)) variant = kStag;
     else if (variant == 1 && strip_ok(p)) variant = kStrip;
   }
@@ -1005,7 +1009,7 @@ const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
   if (auto_pick) {
-    if (w1_ok(p)) variant = kW1;
+    if (w1_auto(p)) variant = kW1;
     else if (stag_ok(p)) variant = kStag;
     else if (variant == 1 && strip_ok(p)) variant = kStrip;
   }

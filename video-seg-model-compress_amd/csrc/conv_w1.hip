@@ -333,7 +333,11 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
       ygroup_head(std::integral_constant<int, 7>{});
       (void)nofill;
     } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // B_{t+1}
+      // B_{t+1}: step t + 1's weights (issued after B_t, before the strip pieces) must have landed;
+      // the 3 strip pieces issued after them are needed only when step t + 1 opens a new tap group
+      // (KW == 2), else they may stay in flight (their buffer is not read before B_{3 g' + 3})
+      if constexpr (KW == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       using ISTN = std::integral_constant<int, ST ^ 1>;
       using IKWN = std::integral_constant<int, KWN>;
