@@ -126,7 +126,10 @@ def timed_region(step, steps, world, dev, marks=None):
     import torch
     import torch.distributed as dist
     from drnmi.dist import max_over_ranks
+    import gc
     cuda = dev.type == "cuda"
+    gc.collect()                 # no collector pause inside the timed steps (re-enabled after them)
+    gc.disable()
     if cuda:
         torch.cuda.synchronize(dev)
     if world > 1:
@@ -145,17 +148,24 @@ def timed_region(step, steps, world, dev, marks=None):
     if world > 1:
         dist.barrier()
     own = time.perf_counter() - t0
+    gc.enable()
     return max_over_ranks(own, device=dev), own
 
 
 def step_spread(marks):
-    """min / median / max of the per-step durations (ms) between consecutive boundary events."""
-    d = sorted(a.elapsed_time(b) for a, b in zip(marks, marks[1:]))
-    if not d:
+    """min / median / max of the per-step durations (ms) between consecutive boundary events, the
+    slowest step's index, and the time steps spent beyond 1.5x the median (one-off stalls: a 20-40
+    ms stall inside one step is what made the 5-step exact-mode line of BENCH_r05 read 4 ms/step
+    slower than its kernels)."""
+    raw = [a.elapsed_time(b) for a, b in zip(marks, marks[1:])]
+    if not raw:
         return None
+    d = sorted(raw)
     mid = len(d) // 2
     med = d[mid] if len(d) % 2 else 0.5 * (d[mid - 1] + d[mid])
-    return {"min": round(d[0], 4), "median": round(med, 4), "max": round(d[-1], 4), "steps": len(d)}
+    stall = sum(x - med for x in raw if x > 1.5 * med)
+    return {"min": round(d[0], 4), "median": round(med, 4), "max": round(d[-1], 4), "steps": len(d),
+            "max_at_step": raw.index(d[-1]), "stall_ms": round(stall, 3)}
 
 
 def gather_ranks(vals, world, dev):
@@ -619,6 +629,8 @@ def main(argv=None):
         out["layers"] = m["layers"]
     out["network_roofline"] = network_block(m, args.steps, B)
     out["accounting"] = m["accounting"]
+    sp = m["accounting"]["step_ms"] or {}
+    out["value_at_median_step"] = round(world * B / sp["median"] * 1e3, 2) if sp.get("median") else None
     if host is not None:
         out["host_frames"] = host
     exact = {}                               # precision -> (sub-line, model)
@@ -634,7 +646,9 @@ def main(argv=None):
                 xm = calibrate(xm, args, dev)
             mx = measure(args, xm, frames, args.exact_steps, SUB_WARMUP, world, dev)
             xroof, xkern = roofline_block(args, mx, prec)
+            sp = mx["accounting"]["step_ms"] or {}
             exact[prec] = ({"precision": prec, "value": B * args.exact_steps / mx["el"], "unit": "frames/s",
+                            "value_at_median_step": round(B / sp["median"] * 1e3, 2) if sp.get("median") else None,
                             "steps": args.exact_steps, "warmup": SUB_WARMUP,
                             "ms_per_step": mx["el"] / args.exact_steps * 1e3,
                             "roofline": xroof, "network_roofline": network_block(mx, args.exact_steps, B),
@@ -717,6 +731,18 @@ def host_frames_run(args, model, step, world, dev):
                     "headline: the headline times HBM-resident frames)"}
 
 
+def newest_first(pattern):
+    """Committed capture files, the latest round first: names start r<round><letters>_ (r9zz_ <
+    r10a_ < r10p_), which plain string order gets wrong across the r9 -> r10 boundary."""
+    import glob
+    import re
+
+    def key(f):
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), m.group(2)) if m else (-1, "")
+    return sorted(glob.glob(pattern), key=key, reverse=True)
+
+
 def pmc_mfma(args, precision=None):
     """Per-kernel MFMA-pipe utilisation and held clock from the newest committed capture of this
     exact workload (profiles/*_pmc_mfma.json, made by scripts/pmc_mfma.sh:
@@ -726,7 +752,7 @@ def pmc_mfma(args, precision=None):
     want = {"arch": args.arch, "height": args.height, "width": args.width, "frames_per_gpu_step": args.batch,
             "precision": precision or args.precision}
     here = os.path.dirname(os.path.abspath(__file__))
-    for f in sorted(glob.glob(os.path.join(here, "profiles", "*_pmc_mfma.json")), reverse=True):
+    for f in newest_first(os.path.join(here, "profiles", "*_pmc_mfma.json")):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -747,7 +773,7 @@ def pmc_traffic(args, kernel, precision=None):
     want = {"arch": args.arch, "height": args.height, "width": args.width, "frames_per_gpu_step": args.batch,
             "precision": precision or args.precision}
     here = os.path.dirname(os.path.abspath(__file__))
-    for f in sorted(glob.glob(os.path.join(here, "profiles", "*_pmc_traffic.json")), reverse=True):
+    for f in newest_first(os.path.join(here, "profiles", "*_pmc_traffic.json")):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
