@@ -118,11 +118,14 @@ def resolve_world(args, environ=os.environ, prog: str = "bench.py"):
     return world, int(environ.get("RANK", "0")), int(environ.get("LOCAL_RANK", "0"))
 
 
-def timed_region(step, steps, world, dev, marks=None):
+def timed_region(step, steps, world, dev, marks=None, lead=None):
     """K timed steps bracketed by barrier + device sync on both sides; the slowest rank's
     elapsed time defines the job (max over ranks).  Returns (job_seconds, own_seconds).
     `marks`: steps + 1 HIP events recorded at the step boundaries (per-step spread; one event
-    per step, on the stream the step launches on)."""
+    per step, on the stream the step launches on).  `lead`: the last untimed warm-up step, run
+    after the host-side bookkeeping (collector pass, event collection), so the device is busy up
+    to the bracketing sync instead of idling through it (an idle device starts the first timed
+    step at a lower clock: +1.5 ms on the first of 20 bf16 steps, BENCH step_ms.max_at_step 0)."""
     import torch
     import torch.distributed as dist
     from drnmi.dist import max_over_ranks
@@ -130,6 +133,8 @@ def timed_region(step, steps, world, dev, marks=None):
     cuda = dev.type == "cuda"
     gc.collect()                 # no collector pause inside the timed steps (re-enabled after them)
     gc.disable()
+    if lead is not None:
+        lead()
     if cuda:
         torch.cuda.synchronize(dev)
     if world > 1:
@@ -444,17 +449,18 @@ def measure(args, model, frames, steps, warmup, world, dev, kernel_events=True):
         events.clear()
         return per_
 
-    for _ in range(max(warmup - 1, 0)):
+    for _ in range(max(warmup - 2, 0)):
         step(False)
-    # last warm-up step instrumented: it names the dominant kernel (the template instance, as
-    # rocprofv3 names it, with the largest total time); inside the timed region only that
-    # kernel's launches carry HIP events (events around all ~25 launches cost ~2.7 % per step)
+    # the next-to-last warm-up step instrumented: it names the dominant kernel (the template
+    # instance, as rocprofv3 names it, with the largest total time); inside the timed region only
+    # that kernel's launches carry HIP events (events around all ~25 launches cost ~2.7 % per step);
+    # the last warm-up step runs inside timed_region, ahead of its opening sync
     step(True)
     warm = collect()
     dominant = max(warm, key=lambda k: sum(warm[k]["d"])) if warm else None
     watch[0] = dominant
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
-    el, own = timed_region(step, steps, world, dev, marks)
+    el, own = timed_region(step, steps, world, dev, marks, lead=(lambda: step(False)) if warmup >= 2 else None)
     timed_per = collect()
     spread = step_spread(marks)
     # per-kernel table: one fully instrumented step after the timed region
