@@ -522,6 +522,25 @@ def test_w1_kernel_bit_identical(n, h, w, cin, cout, dil, with_res):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("n,h,w,cin,cout,dil,with_res", [
+    (2, 5, 256, 128, 128, 1, True), (1, 6, 512, 128, 128, 1, False), (1, 4, 256, 128, 128, 2, True),
+    (2, 3, 256, 256, 256, 4, True), (1, 4, 256, 512, 256, 3, False)])
+def test_w1h_kernel_bit_identical(n, h, w, cin, cout, dil, with_res):
+    """conv_w1h_kernel (tile 23: 128 x 128 tiles of 4 waves of 64 x 64, two workgroups per CU) ==
+    conv_stag128 / conv_stag (tile 19) bit for bit: the same K order and accumulator start."""
+    g = torch.Generator().manual_seed(490 + h * w + cin + cout)
+    x = torch.randn(n, h, w, cin, generator=g).bfloat16().to(DEV)
+    wt = (torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (9 * cout)) ** 0.5).to(DEV)
+    sc = (torch.rand(cout, generator=g) + 0.5).to(DEV)
+    sh = (torch.rand(cout, generator=g) - 0.5).to(DEV)
+    res = torch.randn(n, h, w, cout, generator=g).bfloat16().to(DEV) if with_res else None
+    kw = dict(stride=1, padding=dil, dilation=dil, relu=True, fold_scale=True)
+    a = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=19, **kw)
+    b = ops.conv2d_bn_act(x, wt, sc, sh, res, tile=23, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
 def test_w1_kernel_refuses_unfolded_scale():
     """tile 22 serves only the BN-scale-folded launches (accumulators start from shift + residual)."""
     x = torch.randn(1, 4, 256, 256, device=DEV).bfloat16()

@@ -267,6 +267,7 @@ constexpr TileDesc kTiles[] = {
     {64, 64, "s2row"},                                     // conv_s2row.hip: stride-2 3x3 32->64 / 64->128 row walk
     {64, 64, "s1x2row"},                                   // conv_s2row.hip: stride-1 3x3 64->64 + 1x1 s2 downsample
     {256, 256, "w1stag256"},                               // conv_w1.hip: the stag256 tile as 4 waves of 128 x 128
+    {128, 128, "w1h128"},                                  // conv_w1.hip: 128 x 128 tile, 4 waves of 64 x 64, 2 per CU
 };
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 

@@ -36,10 +36,39 @@
 namespace drnmi {
 namespace {
 
-// 2 A stages + 2 strips (130 KB) + 1 KB sink: the strip pieces past the strip (share 8 of waves
-// 1-3) land there, so every wave issues the same DMA sequence without a branch
-constexpr int kW1Sink = 2 * 256 * 128 + 2 * kStripBytes;
-constexpr int kW1Lds = kW1Sink + 1024;
+// Tile = 2 WCO output channels x 2 (16 FN) pixels (a run of one output row), 4 waves: wc = channel
+// half, wp = pixel half.  conv_w1: WCO 128, FN 8 (256 x 256, one wave per SIMD); conv_w1h: WCO 64,
+// FN 4 (128 x 128, 67 KB of LDS: two workgroups per CU, so two waves per SIMD from different tiles).
+template <int WCO, int FN>
+struct W1Cfg {
+  static constexpr int FM = WCO / 16;
+  static constexpr int BCO = 2 * WCO;
+  static constexpr int PXW = 16 * FN;             // pixels per wave
+  static constexpr int TPX = 2 * PXW;             // pixels per tile
+  static constexpr int AB = BCO * 128;            // one A stage: BCO rows x 64 bf16 channels
+  static constexpr int AI = BCO / 32;             // 1-KB weight pieces per wave per K step
+  static constexpr int NSP = TPX / 8 + 1;         // strip pieces: TPX + 2 dil rows, dil <= 4
+  static constexpr int SB = NSP * 1024;           // one strip buffer
+  static constexpr int SH = (NSP + 3) / 4;        // strip shares per wave per tap group
+  static constexpr int SPS = (SH + 2) / 3;        // shares per wave per K step (3 steps per group)
+  static constexpr int NR = FM + FN;              // fragment reads per wave per substep
+  static constexpr int RX = NR / FM;              // substep-1 reads per X group
+  // 2 A stages + 2 strips + a 1-KB sink: strip pieces past the strip (j >= NSP) land there, so every
+  // wave issues the same DMA sequence without a branch
+  static constexpr int SINK = 2 * AB + 2 * SB;
+  static constexpr int LDS = SINK + 1024;
+  static constexpr int GT = (FM / 2) * (FN - 1);  // MFMA gaps of the Y tail (after the barrier)
+  static constexpr int NI = NR + AI + SPS;        // reads + DMA pieces issued in them
+  static_assert(AI == FN && RX * FM == NR && RX <= FN - 1 && SPS <= FM && 3 * SPS >= SH && AI % 2 == 0, "w1 geometry");
+};
+
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
 
 // SEGF (the labels-only video path's last conv, drnmi_conv_stag_seg): the activation is not stored;
 // as in conv_stag's SEGF epilogue it becomes the B operand of the seg classifier (1x1 512 -> 19 +
@@ -52,21 +81,24 @@ struct W1Seg {
 };
 constexpr int kW1SegCS = 20;
 
-template <bool SEGF>
+template <int WCO, int FN, bool SEGF>
 __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1Seg& sf) {
-  constexpr int BK = 64, FM = 8, FN = 8, WCO = 128, BCO = 256, CE = 8, ESZ = 2;
-  constexpr int AB = BCO * 128;                      // 32 KB per A stage
+  using C = W1Cfg<WCO, FN>;
+  constexpr int BK = 64, FM = C::FM, BCO = C::BCO, CE = 8, ESZ = 2;
+  constexpr int AB = C::AB, AI = C::AI, TPX = C::TPX, PXW = C::PXW, NSP = C::NSP, SB = C::SB, SPS = C::SPS;
+  constexpr int NR = C::NR, RX = C::RX;
+  static_assert(!SEGF || WCO == 128, "seg fusion: the 256-channel tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wave >> 1;                          // channel half (128 channels)
-  const int wp = wave & 1;                           // pixel half (128 pixels)
+  const int wc = wave >> 1;                          // channel half (WCO channels)
+  const int wp = wave & 1;                           // pixel half (PXW pixels)
   const int M = p.n * p.ho * p.wo;
   const int hw_o = p.ho * p.wo;
   const int nco = (p.cout + BCO - 1) / BCO;
-  const int ntiles = (M / kBPX) * nco;
+  const int ntiles = (M / TPX) * nco;
   const int cin = p.cin;
   const int lc = 31 - __builtin_clz(cin);
   const int H = p.h, W = p.w, dil = p.dil;
@@ -78,7 +110,7 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   const int lslot = lane & 7;
 
   const int tile = xcd_remap2(blockIdx.x, ntiles);   // XCD-major deal, as conv_stag
-  const int px0 = (tile / nco) * kBPX;
+  const int px0 = (tile / nco) * TPX;
   const int co0 = (tile % nco) * BCO;
   const int s_n = px0 / hw_o;
   const int s_q = px0 - s_n * hw_o;
@@ -92,12 +124,12 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, uint32_t voff, int soff, int lds_byte) __attribute__((always_inline)) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t*)(smem + lds_byte), 16, voff, soff, 0, 0);
   };
-  // weight piece i (rows (wave*8 + i)*8 .. +8, 1 KB) of K step kt; the swizzle depends on i only
-  // through its parity
+  // weight piece i (rows (wave*AI + i)*8 .. +8, 1 KB) of K step kt; the swizzle depends on i only
+  // through its parity (AI even)
   uint32_t a_off[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int r = (wave * 8 + i) * 8 + lrow;
+    const int r = (wave * AI + i) * 8 + lrow;
     a_off[i] = ((co0 + r) * p.k_pad + swzb<128>(r, lslot) * CE) * ESZ;
   }
   constexpr uint32_t kOOB = 0x80000000u;             // beyond every buffer (sizes < 2^31)
@@ -105,25 +137,26 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     const int cb = kt / 9;
     const int tap = kt - cb * 9;
     const int k0 = (tap << lc) + cb * BK;
-    dma(rs_w, a_off[i & 1], ((i & ~1) * 8 * p.k_pad + k0) * ESZ, stage * AB + (wave * 8 + i) * 1024);
+    dma(rs_w, a_off[i & 1], ((i & ~1) * 8 * p.k_pad + k0) * ESZ, stage * AB + (wave * AI + i) * 1024);
   };
-  // strip share sh (0..8) of group g (channel block g / 3, tap row g % 3): piece j = wave + 4 sh
+  // strip share sh of group g (channel block g / 3, tap row g % 3): piece j = wave + 4 sh; past the
+  // strip (j >= NSP) it reads nothing into the sink, so every wave issues the same count
   auto issue_strip = [&](int g, int buf, int sh) __attribute__((always_inline)) {
     const int j = wave + 4 * sh;
-    if (j >= kStripPieces) return;                   // wave-uniform
+    const bool inside = j < NSP;
     const int R = j * 8 + lrow;
     const int cb = g / 3, kh = g - cb * 3;
     const int ih = s_oh - p.pad + kh * dil;
     const int iw = s_ow0 - p.pad + R;
-    const bool ok = R < kBPX + 2 * dil && static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+    const bool ok = inside && R < TPX + 2 * dil && static_cast<unsigned>(iw) < static_cast<unsigned>(W);
     const bool row_ok = static_cast<unsigned>(ih) < static_cast<unsigned>(H);   // wave-uniform
     const uint32_t voff = ok && row_ok ? static_cast<uint32_t>((iw * cin + (lslot ^ (R & 7)) * CE) * ESZ) : kOOB;
     const int soff = row_ok ? ((s_n * H + ih) * W * cin + cb * BK) * ESZ : 0;
-    dma(rs_x, voff, soff, 2 * AB + buf * kStripBytes + j * 1024);
+    dma(rs_x, voff, soff, inside ? 2 * AB + buf * SB + j * 1024 : C::SINK);
   };
 
   // fragment-read byte offsets (the swizzles of a lane group's 16 rows do not depend on the
-  // fragment index): A rows wc*128 + 16 fm + fr, B strip rows wp*128 + 16 fn + fr + kw*dil
+  // fragment index): A rows wc*WCO + 16 fm + fr, B strip rows wp*PXW + 16 fn + fr + kw*dil
   uint32_t a_base[2], b_base[3][2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -131,7 +164,7 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     a_base[u] = r * 128 + (swzb<128>(r, u * 4 + fq) << 4);
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
-      const int R = wp * 128 + fr + kw * dil;
+      const int R = wp * PXW + fr + kw * dil;
       b_base[kw][u] = 2 * AB + R * 128 + (((u * 4 + fq) ^ (R & 7)) << 4);
     }
   }
@@ -152,13 +185,13 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     constexpr int OFF = decltype(off_c)::value;
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(OFF));
   };
-  // read n of a substep's list (b[0..7] then a[0..7]) of stage ST / strip buffer BF / tap column KW
+  // read n of a substep's list (b[0..FN) then a[0..FM)) of stage ST / strip buffer BF / tap column KW
   auto rd_item = [&](bf16x8 (&a)[FM], bf16x8 (&b)[FN], auto n_c, auto st_c, auto bf_c, auto kw_c, auto u_c)
                      __attribute__((always_inline)) {
     constexpr int N = decltype(n_c)::value, ST = decltype(st_c)::value, BF = decltype(bf_c)::value;
     constexpr int KW = decltype(kw_c)::value, U = decltype(u_c)::value;
-    if constexpr (N < 8) rd(b[N], b_base[KW][U], std::integral_constant<int, BF * kStripBytes + N * 2048>{});
-    else rd(a[N - 8], a_base[U], std::integral_constant<int, ST * AB + (N - 8) * 2048>{});
+    if constexpr (N < FN) rd(b[N], b_base[KW][U], std::integral_constant<int, BF * SB + N * 2048>{});
+    else rd(a[N - FN], a_base[U], std::integral_constant<int, ST * AB + (N - FN) * 2048>{});
   };
 
   // accumulator start: shift (+ residual), as conv_stag's split_init (the dispatch, w1_ok, admits
@@ -172,9 +205,9 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     if (p.res != nullptr) load_residual<FM, WCO, FN>(p, rv, px0, co0, wc, wp, fr, fq);
     // prologue: step 0's weights and group 0's whole strip
 #pragma unroll
-    for (int i = 0; i < 8; ++i) issue_a(0, 0, i);
+    for (int i = 0; i < AI; ++i) issue_a(0, 0, i);
 #pragma unroll
-    for (int sh = 0; sh < 9; ++sh) issue_strip(0, 0, sh);
+    for (int sh = 0; sh < C::SH; ++sh) issue_strip(0, 0, sh);
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
@@ -197,67 +230,38 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   using T_ = std::true_type;
   // after B_0: step 0's substep-0 fragments (b0 first), step 1's weights (stage 1), share set 0
   // of group 1's strip (buffer 1)
-  {
-    auto r16 = [&](auto n_c) __attribute__((always_inline)) { rd_item(a0, b0, n_c, I0{}, I0{}, I0{}, I0{}); };
-    r16(std::integral_constant<int, 0>{});  r16(std::integral_constant<int, 1>{});
-    r16(std::integral_constant<int, 2>{});  r16(std::integral_constant<int, 3>{});
-    r16(std::integral_constant<int, 4>{});  r16(std::integral_constant<int, 5>{});
-    r16(std::integral_constant<int, 6>{});  r16(std::integral_constant<int, 7>{});
-    r16(std::integral_constant<int, 8>{});  r16(std::integral_constant<int, 9>{});
-    r16(std::integral_constant<int, 10>{}); r16(std::integral_constant<int, 11>{});
-    r16(std::integral_constant<int, 12>{}); r16(std::integral_constant<int, 13>{});
-    r16(std::integral_constant<int, 14>{}); r16(std::integral_constant<int, 15>{});
-  }
+  static_for<NR>([&](auto n_c) __attribute__((always_inline)) { rd_item(a0, b0, n_c, I0{}, I0{}, I0{}, I0{}); });
 #pragma unroll
-  for (int i = 0; i < 8; ++i) issue_a(1, 1, i);
+  for (int i = 0; i < AI; ++i) issue_a(1, 1, i);
 #pragma unroll
-  for (int sh = 0; sh < 3; ++sh) issue_strip(1, 1, sh);
+  for (int sh = 0; sh < SPS; ++sh) issue_strip(1, 1, sh);
   __builtin_amdgcn_sched_barrier(0);
 
   // K step t = 3 g + KW of strip buffer GP; LAST: the final step (no barrier, reads or DMA after it)
-  // one MFMA group: acc[FMI][0..7] += a[FMI] x b[0..7], with fill(k) issued in the gap after MFMA k
-  // (k = 0..6): with one wave per SIMD every other instruction of the step must sit in the shadow
+  // one MFMA group: acc[FMI][0..FN) += a[FMI] x b[0..FN), with fill(k) issued in the gap after MFMA
+  // k (k < FN - 1): with one wave per SIMD every other instruction of the step must sit in the shadow
   // of an MFMA (a 16-cycle issue gap holds about three), or the matrix pipe idles while it issues
   auto mgroup = [&](auto fm_c, bf16x8 (&a)[FM], bf16x8 (&b)[FN], auto&& fill) __attribute__((always_inline)) {
     constexpr int FMI = decltype(fm_c)::value;
-    mma(acc[FMI][0], a[FMI], b[0]);
-    __builtin_amdgcn_sched_barrier(0);
-    fill(std::integral_constant<int, 0>{});
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc[FMI][1], a[FMI], b[1]);
-    __builtin_amdgcn_sched_barrier(0);
-    fill(std::integral_constant<int, 1>{});
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc[FMI][2], a[FMI], b[2]);
-    __builtin_amdgcn_sched_barrier(0);
-    fill(std::integral_constant<int, 2>{});
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc[FMI][3], a[FMI], b[3]);
-    __builtin_amdgcn_sched_barrier(0);
-    fill(std::integral_constant<int, 3>{});
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc[FMI][4], a[FMI], b[4]);
-    __builtin_amdgcn_sched_barrier(0);
-    fill(std::integral_constant<int, 4>{});
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc[FMI][5], a[FMI], b[5]);
-    __builtin_amdgcn_sched_barrier(0);
-    fill(std::integral_constant<int, 5>{});
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc[FMI][6], a[FMI], b[6]);
-    __builtin_amdgcn_sched_barrier(0);
-    fill(std::integral_constant<int, 6>{});
-    __builtin_amdgcn_sched_barrier(0);
-    mma(acc[FMI][7], a[FMI], b[7]);
-    __builtin_amdgcn_sched_barrier(0);
+    static_for<FN>([&](auto k_c) __attribute__((always_inline)) {
+      constexpr int K = decltype(k_c)::value;
+      mma(acc[FMI][K], a[FMI], b[K]);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (K < FN - 1) {
+        fill(k_c);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
   };
   // A fragment set stays allocated until the end of the phase that consumes it (a use the compiler
   // sees): a read issued in the shadow of an MFMA must never be given the registers of that
   // MFMA's own operands (the compiler would reuse them right after their last asm use, while the
   // MFMA may still be reading them); the new reads take the registers of the previous generation
   auto keep = [&](bf16x8 (&a)[FM], bf16x8 (&b)[FN]) __attribute__((always_inline)) {
-    asm volatile("" :: "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]));
-    asm volatile("" :: "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]));
+#pragma unroll
+    for (int i = 0; i < FM; ++i) asm volatile("" :: "v"(a[i]));
+#pragma unroll
+    for (int i = 0; i < FN; ++i) asm volatile("" :: "v"(b[i]));
   };
   // weight-piece offsets of the 4 row pairs (i & ~1) * 8 rows, in SGPRs for the loop
   const int a_row = 16 * p.k_pad * ESZ;              // byte offset of 2 x 8 weight rows
@@ -276,24 +280,17 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     using IKW = std::integral_constant<int, KW>;
     using IGP = std::integral_constant<int, GP>;
     auto nofill = [](auto) {};
-    // ---- X: substep 0; the substep-1 reads (b1 first) in the first two gaps of each group
-    auto xgroup = [&](auto fm_c) __attribute__((always_inline)) {
+    // ---- X: substep 0; the substep-1 reads (b1 first) in the first RX gaps of each group
+    static_for<FM>([&](auto fm_c) __attribute__((always_inline)) {
       constexpr int FMI = decltype(fm_c)::value;
-      asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(7 + FMI) : "memory");   // a0[FMI] (b0 already)
+      // a0[FMI] (b0 already): the reads after it are a0[FMI + 1 ..] and this phase's RX x FMI
+      asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(FM - 1 - FMI + RX * FMI) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       mgroup(fm_c, a0, b0, [&](auto k_c) __attribute__((always_inline)) {
         constexpr int KK = decltype(k_c)::value;
-        if constexpr (KK < 2) rd_item(a1, b1, std::integral_constant<int, 2 * FMI + KK>{}, IST{}, IGP{}, IKW{}, I1{});
+        if constexpr (KK < RX) rd_item(a1, b1, std::integral_constant<int, RX * FMI + KK>{}, IST{}, IGP{}, IKW{}, I1{});
       });
-    };
-    xgroup(std::integral_constant<int, 0>{});
-    xgroup(std::integral_constant<int, 1>{});
-    xgroup(std::integral_constant<int, 2>{});
-    xgroup(std::integral_constant<int, 3>{});
-    xgroup(std::integral_constant<int, 4>{});
-    xgroup(std::integral_constant<int, 5>{});
-    xgroup(std::integral_constant<int, 6>{});
-    xgroup(std::integral_constant<int, 7>{});
+    });
     keep(a0, b0);
     __builtin_amdgcn_sched_barrier(0);
     // ---- Y: substep 1.  The scalars of the DMA after B_{t+1} (t + 1 = 3 g' + k': step t + 2's
@@ -303,16 +300,16 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     int sa = 0, ss = 0, s_ok = 0;
     auto ygroup_head = [&](auto fm_c) __attribute__((always_inline)) {
       constexpr int FMI = decltype(fm_c)::value;
-      asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(7 - FMI) : "memory");   // a1[FMI] (b1 already)
+      asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(FM - 1 - FMI) : "memory");   // a1[FMI] (b1 already)
       __builtin_amdgcn_sched_barrier(0);
       mgroup(fm_c, a1, b1, [&](auto k_c) __attribute__((always_inline)) {
         constexpr int KK = decltype(k_c)::value;
-        if constexpr (!LAST && FMI == 0 && KK == 1) {
+        if constexpr (!LAST && FMI == 0 && KK == (FN >= 8 ? 1 : 0)) {
           const int kt = t + 2 < nk ? t + 2 : nk - 1;   // past the end: re-fetch into the idle stage
           const int cb = kt / 9;
           sa = __builtin_amdgcn_readfirstlane((((kt - cb * 9) << lc) + cb * BK) * ESZ);
           __builtin_amdgcn_sched_barrier(0);
-        } else if constexpr (!LAST && FMI == 0 && KK == 3) {
+        } else if constexpr (!LAST && FMI == 0 && KK == (FN >= 8 ? 3 : 1)) {
           const int g2 = gn + 1 < ngroups ? gn + 1 : ngroups - 1;   // past the end: a buffer never read again
           const int cb = g2 / 3, kh = g2 - cb * 3;
           const int ih = s_oh - p.pad + kh * dil;
@@ -322,69 +319,60 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
         }
       });
     };
-    ygroup_head(std::integral_constant<int, 0>{});
-    ygroup_head(std::integral_constant<int, 1>{});
-    ygroup_head(std::integral_constant<int, 2>{});
-    ygroup_head(std::integral_constant<int, 3>{});
+    static_for<(LAST ? FM : FM / 2)>(ygroup_head);
     if constexpr (LAST) {
-      ygroup_head(std::integral_constant<int, 4>{});
-      ygroup_head(std::integral_constant<int, 5>{});
-      ygroup_head(std::integral_constant<int, 6>{});
-      ygroup_head(std::integral_constant<int, 7>{});
       (void)nofill;
     } else {
       // B_{t+1}: step t + 1's weights (issued after B_t, before the strip pieces) must have landed;
-      // the 3 strip pieces issued after them are needed only when step t + 1 opens a new tap group
-      // (KW == 2), else they may stay in flight (their buffer is not read before B_{3 g' + 3})
+      // the SPS strip pieces issued after them are needed only when step t + 1 opens a new tap
+      // group (KW == 2), else they may stay in flight (their buffer is not read before B_{3 g' + 3})
       if constexpr (KW == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(3) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(SPS) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       using ISTN = std::integral_constant<int, ST ^ 1>;
       using IKWN = std::integral_constant<int, KWN>;
       using IGPN = std::integral_constant<int, GPN>;
-      // 27 items over the 28 gaps of groups 4..7: b0[0..7] alternating with the 8 weight pieces,
-      // then a0[0..7] with the 3 strip pieces after the first three
+      // NI items over the GT gaps of the groups after the barrier: b0[0..FN) alternating with the AI
+      // (= FN) weight pieces, then a0[0..FM) with the SPS strip pieces after the first SPS of them;
+      // gap G issues items [ceil(G NI / GT), ceil((G + 1) NI / GT))
       auto item = [&](auto n_c) __attribute__((always_inline)) {
         constexpr int N = decltype(n_c)::value;
-        if constexpr (N < 16) {
+        if constexpr (N < 2 * FN) {
           if constexpr (N % 2 == 0) {
             rd_item(a0, b0, std::integral_constant<int, N / 2>{}, ISTN{}, IGPN{}, IKWN{}, I0{});
           } else {
             constexpr int I = N / 2;
-            dma(rs_w, a_off[I & 1], sa + (I >> 1) * a_row, ST * AB + (wave * 8 + I) * 1024);
+            dma(rs_w, a_off[I & 1], sa + (I >> 1) * a_row, ST * AB + (wave * AI + I) * 1024);
           }
-        } else if constexpr (N < 22) {
+        } else if constexpr (N < 2 * FN + 2 * SPS) {
           if constexpr (N % 2 == 0) {
-            rd_item(a0, b0, std::integral_constant<int, 8 + (N - 16) / 2>{}, ISTN{}, IGPN{}, IKWN{}, I0{});
+            rd_item(a0, b0, std::integral_constant<int, FN + (N - 2 * FN) / 2>{}, ISTN{}, IGPN{}, IKWN{}, I0{});
           } else {
-            constexpr int SH = (N - 17) / 2;               // 0..2 of the share set
-            const int sh = 3 * KWN + SH;
+            constexpr int SH = (N - 2 * FN - 1) / 2;       // 0..SPS-1 of the share set
+            const int sh = SPS * KWN + SH;
             const int j = wave + 4 * sh;
-            // branch-free: a piece past the strip (j >= 33: share 8 of waves 1-3) reads nothing and
-            // lands in the sink
-            const bool inside = j < kStripPieces;
+            // branch-free: a piece past the strip reads nothing and lands in the sink
+            const bool inside = j < NSP;
             const int R = j * 8 + lrow;
             const int iw = s_ow0 - p.pad + R;
-            const bool ok = inside && s_ok && R < kBPX + 2 * dil && static_cast<unsigned>(iw) < static_cast<unsigned>(W);
+            const bool ok = inside && s_ok && R < TPX + 2 * dil && static_cast<unsigned>(iw) < static_cast<unsigned>(W);
             const uint32_t voff = ok ? static_cast<uint32_t>((iw * cin + (lslot ^ (R & 7)) * CE) * ESZ) : kOOB;
-            dma(rs_x, voff, ss, inside ? 2 * AB + SGB * kStripBytes + j * 1024 : kW1Sink);
+            dma(rs_x, voff, ss, inside ? 2 * AB + SGB * SB + j * 1024 : C::SINK);
           }
         } else {
-          rd_item(a0, b0, std::integral_constant<int, 11 + (N - 22)>{}, ISTN{}, IGPN{}, IKWN{}, I0{});
+          rd_item(a0, b0, std::integral_constant<int, FN + SPS + (N - 2 * FN - 2 * SPS)>{}, ISTN{}, IGPN{}, IKWN{}, I0{});
         }
       };
-      auto ygroup_tail = [&](auto fm_c) __attribute__((always_inline)) {
-        constexpr int FMI = decltype(fm_c)::value;
-        constexpr int N0 = 7 * (FMI - 4);
-        mgroup(fm_c, a1, b1, [&](auto k_c) __attribute__((always_inline)) {
-          constexpr int N = N0 + decltype(k_c)::value;
-          if constexpr (N < 27) item(std::integral_constant<int, N>{});
+      static_for<FM - FM / 2>([&](auto q_c) __attribute__((always_inline)) {
+        constexpr int FMI = FM / 2 + decltype(q_c)::value;
+        mgroup(std::integral_constant<int, FMI>{}, a1, b1, [&](auto k_c) __attribute__((always_inline)) {
+          constexpr int G = (FMI - FM / 2) * (FN - 1) + decltype(k_c)::value;
+          constexpr int LO = (G * C::NI + C::GT - 1) / C::GT, HI = ((G + 1) * C::NI + C::GT - 1) / C::GT;
+          static_for<HI - LO>([&](auto d_c) __attribute__((always_inline)) {
+            item(std::integral_constant<int, LO + decltype(d_c)::value>{});
+          });
         });
-      };
-      ygroup_tail(std::integral_constant<int, 4>{});
-      ygroup_tail(std::integral_constant<int, 5>{});
-      ygroup_tail(std::integral_constant<int, 6>{});
-      ygroup_tail(std::integral_constant<int, 7>{});
+      });
     }
     keep(a1, b1);
     __builtin_amdgcn_sched_barrier(0);
@@ -471,7 +459,7 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
           const float4 o = xch[mt * FN + fn];
-          const int64_t m = px0 + wp * 128 + fn * 16 + fr;
+          const int64_t m = px0 + wp * PXW + fn * 16 + fr;
           *reinterpret_cast<float4*>(part + m * kW1SegCS + cls) =
               make_float4(pacc[mt][fn][0] + o.x, pacc[mt][fn][1] + o.y, pacc[mt][fn][2] + o.z, pacc[mt][fn][3] + o.w);
         }
@@ -480,9 +468,19 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   }
 }
 
+using W1 = W1Cfg<128, 8>;
+using W1H = W1Cfg<64, 4>;
+
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 conv_w1_kernel(const drnmi_conv_args p) {
-  conv_w1_body<false>(p, W1Seg{nullptr, 0, nullptr});
+  conv_w1_body<128, 8, false>(p, W1Seg{nullptr, 0, nullptr});
+}
+
+// the 128 x 128 tile (D-22 layer4, 128 -> 128 at K = 1152: 18 K steps per tile); two workgroups per
+// CU, so one tile's prologue strip and epilogue overlap the other's MFMAs
+__global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
+conv_w1h_kernel(const drnmi_conv_args p) {
+  conv_w1_body<64, 4, false>(p, W1Seg{nullptr, 0, nullptr});
 }
 
 struct W1SegArgs {
@@ -491,7 +489,7 @@ struct W1SegArgs {
 };
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 conv_w1_seg_kernel(const W1SegArgs a) {
-  conv_w1_body<true>(a.p, a.sf);
+  conv_w1_body<128, 8, true>(a.p, a.sf);
 }
 
 }  // namespace
@@ -500,9 +498,12 @@ static hipError_t w1_attrs() {
   static bool attr_set = false;
   if (!attr_set) {
     for (const void* f : {reinterpret_cast<const void*>(&conv_w1_kernel), reinterpret_cast<const void*>(&conv_w1_seg_kernel)}) {
-      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kW1Lds);
+      const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, W1::LDS);
       if (e != hipSuccess) return e;
     }
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_w1h_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, W1H::LDS);
+    if (e != hipSuccess) return e;
     attr_set = true;
   }
   return hipSuccess;
@@ -515,8 +516,8 @@ hipError_t launch_w1_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_
   a.p = p;
   a.sf = W1Seg{seg_w, seg_k_pad, part};
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
-  hipLaunchKernelGGL(conv_w1_seg_kernel, dim3(static_cast<unsigned>((M / kBPX) * ((p.cout + 255) / 256))), dim3(256),
-                     kW1Lds, s, a);
+  hipLaunchKernelGGL(conv_w1_seg_kernel, dim3(static_cast<unsigned>((M / W1::TPX) * ((p.cout + 255) / 256))), dim3(256),
+                     W1::LDS, s, a);
   return hipGetLastError();
 }
 
@@ -524,8 +525,17 @@ hipError_t launch_w1(const drnmi_conv_args& p, hipStream_t s) {
   const hipError_t e0 = w1_attrs();
   if (e0 != hipSuccess) return e0;
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
-  const dim3 grid(static_cast<unsigned>((M / kBPX) * ((p.cout + 255) / 256)));
-  hipLaunchKernelGGL(conv_w1_kernel, grid, dim3(256), kW1Lds, s, p);
+  const dim3 grid(static_cast<unsigned>((M / W1::TPX) * ((p.cout + 255) / 256)));
+  hipLaunchKernelGGL(conv_w1_kernel, grid, dim3(256), W1::LDS, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_w1h(const drnmi_conv_args& p, hipStream_t s) {
+  const hipError_t e0 = w1_attrs();
+  if (e0 != hipSuccess) return e0;
+  const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
+  const dim3 grid(static_cast<unsigned>((M / W1H::TPX) * ((p.cout + 127) / 128)));
+  hipLaunchKernelGGL(conv_w1h_kernel, grid, dim3(256), W1H::LDS, s, p);
   return hipGetLastError();
 }
 

@@ -39,6 +39,8 @@ hipError_t launch_stag(const drnmi_conv_args& p, hipStream_t s);
 // The same strip tile as 4 waves of 128 x 128 (one wave per SIMD, conv_w1.hip): bf16, no x2,
 // cout % 256 == 0; bit-identical to conv_stag_kernel.
 hipError_t launch_w1(const drnmi_conv_args& p, hipStream_t s);
+// ... as a 128 x 128 tile (conv_w1h_kernel: 4 waves of 64 x 64, two workgroups per CU)
+hipError_t launch_w1h(const drnmi_conv_args& p, hipStream_t s);
 // ... with the seg classifier in its epilogue (conv_w1_seg_kernel; bf16, partials as launch_stag_seg's)
 hipError_t launch_w1_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_pad, void* part, hipStream_t s);
 hipError_t launch_stag_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_pad, void* part, hipStream_t s);
