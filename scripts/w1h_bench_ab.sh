@@ -1,24 +1,32 @@
 #!/bin/bash
-# Same-box A/B of the bf16 bench line: the shipped library (conv_w1h routed on the short-K
-# launches) vs the previous routing (diag/libdrnmi_base.so), interleaved.  usage: bash scripts/w1h_bench_ab.sh OUT
+# Same-box A/B of the bf16 bench line, interleaved: the shipped library (conv_w1h on the short-K
+# launches of the routing under test) vs diag/libdrnmi_base.so (round-6 r10 routing).  usage: bash scripts/w1h_bench_ab.sh OUT
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$1; mkdir -p $O
-for i in 1 2 3; do
-  timeout -k 10 120 python3 bench.py --steps 40 --no-cpu-baseline --no-exact-mode > $O/w1h_$i.json 2>/dev/null || exit 1
-  DRNMI_LIB=$R/diag/libdrnmi_base.so timeout -k 10 120 python3 bench.py --steps 40 --no-cpu-baseline --no-exact-mode > $O/base_$i.json 2>/dev/null || exit 1
+timeout -k 10 240 python -u -m pytest $R/tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread \
+  -k "w1 or stag or fused_downsample" > $O/pytest.log 2>&1
+rc=$?; tail -2 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
+run() {  # tag lib
+  if [ "$2" = "-" ]; then timeout -k 10 120 python3 bench.py --steps 40 --no-cpu-baseline --no-exact-mode > $O/$1.json 2>/dev/null
+  else DRNMI_LIB=$R/diag/$2 timeout -k 10 120 python3 bench.py --steps 40 --no-cpu-baseline --no-exact-mode > $O/$1.json 2>/dev/null; fi
+}
+# ABBA order, so neither library always runs on the warmer box
+for i in 1 2; do
+  run full_a$i - || exit 1; run base_a$i libdrnmi_base.so || exit 1
+  run base_b$i libdrnmi_base.so || exit 1; run full_b$i - || exit 1
 done
 python3 - $O <<'PY'
 import json, sys, glob
 rows = {}
-for tag in ("w1h", "base"):
+tags = ("full", "base")
+for tag in tags:
     for f in sorted(glob.glob(f"{sys.argv[1]}/{tag}_*.json")):
         d = json.loads(open(f).read().strip().splitlines()[-1])
-        ls = {l["node"]: l["us"] for l in d["layers"]}
-        rows.setdefault(tag, []).append(ls)
+        rows.setdefault(tag, []).append({l["node"]: l["us"] for l in d["layers"]})
         print(tag, round(d["value"], 1), "ms", round(d["ms_per_step"], 3), d["roofline"]["kernel"], d["roofline"]["frac"],
               "net", d.get("network_roofline", {}).get("frac"))
-for k in rows["w1h"][0]:
-    a = min(r[k] for r in rows["w1h"]); b = min(r[k] for r in rows["base"])
-    if abs(a - b) > 1: print(f"  {k:24s} w1h {a:8.1f}  base {b:8.1f}")
+for k in rows["base"][0]:
+    v = [min(r[k] for r in rows[t]) for t in tags]
+    if max(v) - min(v) > 1: print(f"  {k:24s} " + "  ".join(f"{t} {x:8.1f}" for t, x in zip(tags, v)))
 PY

@@ -813,6 +813,8 @@ def test_conv_fused_downsample(case):
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
     stag = ks == 3 and wo % 256 == 0 and cin % 128 == 0 and kp == k1 + cin2
     s1x2 = halo and cin == 64 and cout == 64 and cin2 == 32 and s2 == 2 and dil == 1   # conv_s1x2row_kernel
+    # whole-row strip shapes: the staggered x2 tiles (the conv_w1 / conv_w1h x2 forms, bit-identical,
+    # measured slower inside the network: profiles/r11_w1h)
     assert name.startswith("conv_stag128_x2_kernel" if stag and cout <= 128 else "conv_stag_x2_kernel" if stag
                            else "conv_s1x2row_kernel" if s1x2 else "conv_halo_kernel" if halo else "conv_big_kernel"), name
     _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds")
@@ -826,6 +828,15 @@ def test_conv_fused_downsample(case):
         _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds big")
         torch.cuda.synchronize()
         assert torch.equal(yb, y)
+        # the staggered x2 tiles (tile 19: conv_stag128_x2 / conv_stag_x2) and both conv_w1 forms
+        for t in (19, 22, 23):
+            if t == 22 and cout % 256:
+                continue
+            a.y, a.tile = yb.data_ptr(), t
+            yb.zero_()
+            _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), f"x2 tile {t}")
+            torch.cuda.synchronize()
+            assert torch.equal(yb, y), t
         a.y, a.tile = y.data_ptr(), -1
     if halo and kp == k1 + cin2:          # conv_big takes it too (tile 4: the 128 x 256 X2 form)
         yb = torch.empty_like(y)

@@ -717,22 +717,22 @@ constexpr int kW1 = 18;      // conv_w1_kernel (tile id 22): the stag256 tile as
 constexpr int kW1H = 19;     // conv_w1h_kernel (tile id 23): 128 x 128 tiles of 4 waves of 64 x 64, two per CU
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-// conv_w1 (conv_w1.hip): the staggered tile's shapes without the fused downsample, 256-channel blocks
+// conv_w1 (conv_w1.hip): the staggered tile's shapes (+ the fused downsample: conv_w1_x2), 256-channel blocks
 bool w1_ok(const drnmi_conv_args& p) {
-  return stag_ok(p) && p.x2 == nullptr && p.cout % 256 == 0 && p.scale == nullptr && p.out_dtype == DRNMI_BF16 &&
+  return stag_ok(p) && p.cout % 256 == 0 && p.scale == nullptr && p.out_dtype == DRNMI_BF16 &&
          p.y_sc == 1 && p.y_sp == p.cout && p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
 }
 // auto-routed where it measured no slower inside the network (same-box interleaved bench A/B,
 // profiles/r10m_w1_ab): the long-K residual-free launches (D-22 layer6.1 conv1, layer7).  At
 // cin 128 / 256 (18 / 36 K steps) and with a residual its per-tile prologue and epilogue, issued
 // by 4 waves instead of 8, cost more than the loop saves (layer5.0 conv1 145 vs 130 us)
-bool w1_auto(const drnmi_conv_args& p) { return w1_ok(p) && p.cin >= 512 && p.res == nullptr; }
+bool w1_auto(const drnmi_conv_args& p) { return w1_ok(p) && p.x2 == nullptr && p.cin >= 512 && p.res == nullptr; }
 // conv_w1h: the same shapes at 128-channel blocks (a 128-pixel run: wo % 128 == 0 follows from stag_ok)
 bool w1h_ok(const drnmi_conv_args& p) {
-  return stag_ok(p) && p.x2 == nullptr && p.cout % 128 == 0 && p.scale == nullptr && p.out_dtype == DRNMI_BF16 &&
+  return stag_ok(p) && p.cout % 128 == 0 && p.scale == nullptr && p.out_dtype == DRNMI_BF16 &&
          p.y_sc == 1 && p.y_sp == p.cout && p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
 }
-bool w1h_auto(const drnmi_conv_args& p) { return w1h_ok(p) && p.cin <= 256 && p.cout <= 256; }
+bool w1h_auto(const drnmi_conv_args& p) { return w1h_ok(p) && p.x2 == nullptr && p.cout <= 128; }
 
 template <int KS, bool PERSIST>
 hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
@@ -1012,8 +1012,11 @@ int big_conv_dispatch(const drnmi_conv_args& p, int variant, hipStream_t s) {
 const char* big_conv_name(const drnmi_conv_args& p, int variant) {
   if (variant == kS2Row || (variant < 0 && s2row_auto(p))) return s2row_conv_name(p);
   if (variant == kS1X2Row || (variant < 0 && s1x2row_auto(p))) return s1x2row_conv_name(p);
-  if (variant == kW1) return big_conv_supported(p) && w1_ok(p) ? "conv_w1_kernel" : nullptr;
-  if (variant == kW1H) return big_conv_supported(p) && w1h_ok(p) ? "conv_w1h_kernel" : nullptr;
+  if (variant == kW1 || variant == kW1H) {
+    if (!big_conv_supported(p) || !(variant == kW1 ? w1_ok(p) : w1h_ok(p))) return nullptr;
+    if (variant == kW1) return p.x2 != nullptr ? "conv_w1_x2_kernel" : "conv_w1_kernel";
+    return p.x2 != nullptr ? "conv_w1h_x2_kernel" : "conv_w1h_kernel";
+  }
   if (variant == kHalo || (variant < 0 && halo_conv_supported(p) && halo_preferred(p))) return halo_conv_name(p);
   const bool auto_pick = variant < 0;
   if (variant < 0) variant = auto_variant(p);
@@ -1023,8 +1026,8 @@ const char* big_conv_name(const drnmi_conv_args& p, int variant) {
     else if (stag_ok(p)) variant = kStag;
     else if (variant == 1 && strip_ok(p)) variant = kStrip;
   }
-  if (variant == kW1) return "conv_w1_kernel";
-  if (variant == kW1H) return "conv_w1h_kernel";
+  if (variant == kW1) return p.x2 != nullptr ? "conv_w1_x2_kernel" : "conv_w1_kernel";
+  if (variant == kW1H) return p.x2 != nullptr ? "conv_w1h_x2_kernel" : "conv_w1h_kernel";
   if (variant == kStag) {
     if (!stag_ok(p)) return nullptr;
     if (p.cout <= 128) return p.x2 != nullptr ? "conv_stag128_x2_kernel" : "conv_stag128_kernel";

@@ -81,13 +81,14 @@ struct W1Seg {
 };
 constexpr int kW1SegCS = 20;
 
-template <int WCO, int FN, bool SEGF>
+template <int WCO, int FN, bool SEGF, bool X2 = false>
 __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1Seg& sf) {
   using C = W1Cfg<WCO, FN>;
   constexpr int BK = 64, FM = C::FM, BCO = C::BCO, CE = 8, ESZ = 2;
   constexpr int AB = C::AB, AI = C::AI, TPX = C::TPX, PXW = C::PXW, NSP = C::NSP, SB = C::SB, SPS = C::SPS;
   constexpr int NR = C::NR, RX = C::RX;
   static_assert(!SEGF || WCO == 128, "seg fusion: the 256-channel tile");
+  static_assert(!(SEGF && X2), "one epilogue extension at a time");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
@@ -388,6 +389,56 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   }
   group(I0{}, F{}, ngroups - 2);
   group(I1{}, T_{}, ngroups - 1);
+  if constexpr (X2) {
+    // the fused 1x1 downsample (x2 != NULL: D-22 layer4.0 / 5.0 / 6.0 conv2) as cin2 / 64 more K
+    // steps after the taps, in conv_stag_x2's order (so the same bits): step e reads weight
+    // columns 9 cin + 64 e and, as its B strip, pixel R of the tile sampled at stride2 in x2
+    // (strip row R, read at tap column 0).  Not pipelined across steps (2-4 per tile): the other
+    // workgroup of the CU (conv_w1h) or the partner waves' MFMAs cover the DMA latency
+    const int nx2 = p.cin2 / BK;
+    const __amdgpu_buffer_rsrc_t rs_x2 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(p.x2), 0, p.n * p.h2 * p.w2 * p.cin2 * ESZ, 0x00020000);
+    const int x2_row = (s_n * p.h2 + s_oh * p.stride2) * p.w2 * p.cin2 * ESZ;
+    auto issue_x2 = [&](int e, int st) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i)
+        dma(rs_w, a_off[i & 1], ((i & ~1) * 8 * p.k_pad + 9 * cin + e * BK) * ESZ, st * AB + (wave * AI + i) * 1024);
+#pragma unroll
+      for (int sh = 0; sh < C::SH; ++sh) {
+        const int j = wave + 4 * sh;
+        const bool inside = j < NSP;
+        const int R = j * 8 + lrow;
+        const uint32_t voff = inside && R < TPX
+                                  ? static_cast<uint32_t>(((s_ow0 + R) * p.stride2 * p.cin2 + (lslot ^ (R & 7)) * CE) * ESZ)
+                                  : kOOB;
+        dma(rs_x2, voff, x2_row + e * BK * ESZ, inside ? 2 * AB + st * SB + j * 1024 : C::SINK);
+      }
+    };
+    // every wave is past the loop's last reads; the clamped re-fetches have landed
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    issue_x2(0, 0);
+    for (int e = 0; e < nx2; ++e) {
+      const int st = e & 1;
+      // step e's pieces have landed everywhere, and every wave is done with step e - 1's buffers
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (e + 1 < nx2) issue_x2(e + 1, st ^ 1);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        bf16x8 bx[FN], ax[FM];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+          bx[fn] = *reinterpret_cast<const bf16x8*>(smem + b_base[0][u] + st * SB + fn * 2048);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) ax[fm] = *reinterpret_cast<const bf16x8*>(smem + a_base[u] + st * AB + fm * 2048);
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+          for (int fn = 0; fn < FN; ++fn) mma(acc[fm][fn], ax[fm], bx[fn]);
+      }
+    }
+  }
   // the last MFMAs' results: wait states, then an empty asm that redefines every accumulator, so
   // no epilogue read of an AGPR can be scheduled before the wait (the compiler had hoisted the
   // read of acc[1][0] to right after its last MFMA, which it does not know is one: that read
@@ -483,6 +534,16 @@ conv_w1h_kernel(const drnmi_conv_args p) {
   conv_w1_body<64, 4, false>(p, W1Seg{nullptr, 0, nullptr});
 }
 
+// + the fused 1x1 downsample (x2 != NULL)
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+conv_w1_x2_kernel(const drnmi_conv_args p) {
+  conv_w1_body<128, 8, false, true>(p, W1Seg{nullptr, 0, nullptr});
+}
+__global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
+conv_w1h_x2_kernel(const drnmi_conv_args p) {
+  conv_w1_body<64, 4, false, true>(p, W1Seg{nullptr, 0, nullptr});
+}
+
 struct W1SegArgs {
   drnmi_conv_args p;
   W1Seg sf;
@@ -501,9 +562,13 @@ static hipError_t w1_attrs() {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, W1::LDS);
       if (e != hipSuccess) return e;
     }
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_w1h_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, W1H::LDS);
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_w1_x2_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, W1::LDS);
     if (e != hipSuccess) return e;
+    for (const void* f : {reinterpret_cast<const void*>(&conv_w1h_kernel), reinterpret_cast<const void*>(&conv_w1h_x2_kernel)}) {
+      const hipError_t e2 = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, W1H::LDS);
+      if (e2 != hipSuccess) return e2;
+    }
     attr_set = true;
   }
   return hipSuccess;
@@ -526,7 +591,8 @@ hipError_t launch_w1(const drnmi_conv_args& p, hipStream_t s) {
   if (e0 != hipSuccess) return e0;
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const dim3 grid(static_cast<unsigned>((M / W1::TPX) * ((p.cout + 255) / 256)));
-  hipLaunchKernelGGL(conv_w1_kernel, grid, dim3(256), W1::LDS, s, p);
+  if (p.x2 != nullptr) hipLaunchKernelGGL(conv_w1_x2_kernel, grid, dim3(256), W1::LDS, s, p);
+  else hipLaunchKernelGGL(conv_w1_kernel, grid, dim3(256), W1::LDS, s, p);
   return hipGetLastError();
 }
 
@@ -535,7 +601,8 @@ hipError_t launch_w1h(const drnmi_conv_args& p, hipStream_t s) {
   if (e0 != hipSuccess) return e0;
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const dim3 grid(static_cast<unsigned>((M / W1H::TPX) * ((p.cout + 127) / 128)));
-  hipLaunchKernelGGL(conv_w1h_kernel, grid, dim3(256), W1H::LDS, s, p);
+  if (p.x2 != nullptr) hipLaunchKernelGGL(conv_w1h_x2_kernel, grid, dim3(256), W1H::LDS, s, p);
+  else hipLaunchKernelGGL(conv_w1h_kernel, grid, dim3(256), W1H::LDS, s, p);
   return hipGetLastError();
 }
 
