@@ -245,6 +245,34 @@ def test_seg_fused_w1_matches_stag_bit_identical(n):
     assert torch.equal(got, ref)
 
 
+def test_seg_fused_int8_w1_matches_stag():
+    """int8 nets: the seg-fused layer8 launch on the one-wave-per-SIMD int8 tile
+    (conv_w1_i8_seg_kernel, the default) == the staggered one (conv_i8_stag_seg_kernel, tile 19):
+    integer partials, so equal bit for bit."""
+    m = drnseg.build("drn_d_22", 19, seed=8, device=torch.device(DEV))
+    g = torch.Generator(device=DEV).manual_seed(13)
+    frames = torch.randint(0, 256, (2, 256, 2048, 3), dtype=torch.uint8, device=DEV, generator=g)
+    m.calibrate_int8(frames[:1])
+    m.set_precision("int8")
+    got = m.segment(frames, INFO_MEAN, INFO_STD, False).clone()
+    plan = [p for k, p in m._plans.items() if k[0] == "int8"][0]
+    assert plan.labels_path() == "seg2" and plan.seg_fused["i8"]
+    j = plan.seg_fused["conv"]
+    lib = _lib.load()
+    assert lib.drnmi_conv_stag_seg_kernel_name(ctypes.byref(plan.args[j])).decode() == "conv_w1_i8_seg_kernel"
+    part_w1 = plan.bufs["seg_part"].clone()
+    plan.args[j].tile = 19
+    try:
+        assert lib.drnmi_conv_stag_seg_kernel_name(ctypes.byref(plan.args[j])).decode() == "conv_i8_stag_seg_kernel"
+        ref = m.segment(frames, INFO_MEAN, INFO_STD, False)
+        part_stag = plan.bufs["seg_part"].clone()
+    finally:
+        plan.args[j].tile = -1
+    torch.cuda.synchronize()
+    assert torch.equal(part_w1, part_stag)
+    assert torch.equal(got, ref)
+
+
 def test_segment_labels_nhwc_identical_int8():
     """int8 nets (C5): the int8 seg conv writes the same fp32 values as NHWC rows (store_tile_i8's
     16-B path) -- labels identical to the NCHW-planes head."""

@@ -68,6 +68,9 @@ CONV_CASES = [
     (2, 3, 512, 128, 256, 3, 1, 4, 4, False, "bf16"),
     (1, 4, 512, 512, 512, 3, 1, 4, 4, True, "i8"),
     (2, 3, 256, 256, 512, 3, 1, 1, 1, False, "bf16"),
+    # long K, no residual, int8 out (conv_w1_i8_kernel's shapes: forced below, not auto-routed)
+    (1, 4, 512, 512, 512, 3, 1, 2, 2, False, "i8"),
+    (2, 3, 256, 1024, 256, 3, 1, 1, 1, False, "i8"),
 ]
 
 
@@ -136,6 +139,19 @@ def test_conv_i8_matches_oracle(case):
     else:
         np.testing.assert_array_equal(got, ref)
         assert np.abs(ref.astype(np.int32)).max() < 127 or (ref == 127).mean() < 0.5   # not all saturated
+    if strip and cin % 256 == 0:
+        # both int8 strip tiles, forced: tile 19 (conv_i8_stag_kernel) and, with an int8 output,
+        # tile 22 (conv_w1_i8_kernel) -- the same oracle bits
+        for t in (19, 22) if out == "i8" else (19,):
+            a.tile = t
+            y.fill_(0)
+            L.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), _stream()), f"conv i8 tile {t}")
+            torch.cuda.synchronize()
+            got = y.cpu().numpy()
+            if out == "f32":
+                got = got.transpose(0, 2, 3, 1)
+            np.testing.assert_array_equal(got.view(np.uint16) if out == "bf16" else got, ref)
+        a.tile = -1
 
 
 def test_conv_i8_rejects_bad_args():

@@ -909,12 +909,28 @@ bool i8_stag_ok(const drnmi_conv_args& p) {
   return i8_strip_ok(p) && p.cin % 256 == 0 && p.x2 == nullptr;
 }
 
+// int8 conv_w1 (conv_w1_i8_kernel): the staggered int8 tile's shapes at 256-channel blocks with a
+// dense int8 NHWC output (its 16-B epilogue).  Not auto-routed: on the long-K residual-free int8
+// launches it measured no faster inside the network (profiles/r11_w1i8: layer6.1 conv1 460 vs 450
+// us); the seg-fused layer8 launch (drnmi_conv_stag_seg) takes its SEGF form (431 vs 456 us)
+bool i8_w1_ok(const drnmi_conv_args& p) {
+  return i8_stag_ok(p) && p.cout % 256 == 0 && p.out_dtype == DRNMI_I8 && p.y_sc == 1 && p.y_sp == p.cout &&
+         p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
+}
+bool i8_w1_auto(const drnmi_conv_args& p) { return false && i8_w1_ok(p); }
+// tile ids 19 / 22 force the staggered / one-wave-per-SIMD int8 tile (the bit-identity tests)
+bool i8_w1_pick(const drnmi_conv_args& p) {
+  return p.tile == 4 + kW1 ? true : p.tile == 4 + kStag ? false : i8_w1_auto(p);
+}
+
 int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!i8_conv_supported(p)) return DRNMI_ENOTSUP;
   const int v = i8_variant(p);
   if ((p.cout + kI8Variants[v].bco - 1) / kI8Variants[v].bco * kI8Variants[v].bco > p.cout_pad) return DRNMI_EINVAL;
   if (p.ks == 3 && i8_stag_ok(p)) {
-    const hipError_t e = launch_stag(p, s);
+    const bool w1 = i8_w1_pick(p);
+    if (w1 && !i8_w1_ok(p)) return DRNMI_ENOTSUP;
+    const hipError_t e = w1 ? launch_w1(p, s) : launch_stag(p, s);
     return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
   }
   if (p.ks == 3 && i8_strip_ok(p)) {
@@ -928,7 +944,7 @@ int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
 const char* i8_conv_name(const drnmi_conv_args& p) {
   if (!i8_conv_supported(p)) return nullptr;
   const int v = i8_variant(p);
-  if (p.ks == 3 && i8_stag_ok(p)) return "conv_i8_stag_kernel";
+  if (p.ks == 3 && i8_stag_ok(p)) return !i8_w1_pick(p) ? "conv_i8_stag_kernel" : i8_w1_ok(p) ? "conv_w1_i8_kernel" : nullptr;
   if (p.ks == 3 && i8_strip_ok(p)) return "conv_i8_strip_kernel";
   return p.ks == 3 ? kI8Variants[v].name3 : kI8Variants[v].name1;
 }
@@ -1098,7 +1114,9 @@ extern "C" int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, 
     if (!(i8_conv_supported(p) && p.ks == 3 && i8_stag_ok(p)) || p.res != nullptr || p.cout % 256 != 0 ||
         p.cout_pad < p.cout)
       return DRNMI_ENOTSUP;
-    const hipError_t e = launch_stag_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream));
+    // the one-wave-per-SIMD int8 tile (conv_w1_i8_seg_kernel); tile 19 forces the staggered one
+    const hipError_t e = p.tile == 4 + kStag ? launch_stag_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream))
+                                             : launch_w1_seg(p, seg_w, seg_k_pad, partials, reinterpret_cast<hipStream_t>(stream));
     return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
   }
   if (p.dtype != DRNMI_BF16 || p.out_dtype != DRNMI_BF16) return DRNMI_EINVAL;
@@ -1119,5 +1137,6 @@ extern "C" int drnmi_conv_stag_seg(const drnmi_conv_args* a, const void* seg_w, 
 
 extern "C" const char* drnmi_conv_stag_seg_kernel_name(const drnmi_conv_args* a) {
   if (a == nullptr) return nullptr;
-  return a->dtype == DRNMI_I8 ? "conv_i8_stag_seg_kernel" : a->tile == 4 + kStag ? "conv_stag_seg_kernel" : "conv_w1_seg_kernel";
+  if (a->dtype == DRNMI_I8) return a->tile == 4 + kStag ? "conv_i8_stag_seg_kernel" : "conv_w1_i8_seg_kernel";
+  return a->tile == 4 + kStag ? "conv_stag_seg_kernel" : "conv_w1_seg_kernel";
 }

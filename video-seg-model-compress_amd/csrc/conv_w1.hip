@@ -81,14 +81,95 @@ struct W1Seg {
 };
 constexpr int kW1SegCS = 20;
 
-template <int WCO, int FN, bool SEGF, bool X2 = false>
+// int8 nets: the seg classifier on the int8 copy of the last conv's output, as conv_stag's
+// stag_seg_i8 (the same quantisation, the same fixed permutation of K, integer partial sums: the
+// same partials) for a wave of FN pixel groups; xch: a free 2 x 64 x 2 FN x 16-B LDS area
+template <int FM, int FN>
+__device__ __forceinline__ void w1_seg_i8(const drnmi_conv_args& p, const i32x4 (&acc)[FM][FN], int px0, int co0, int wc,
+                                          int wp, int fr, int fq, int lane, const W1Seg& sf, char* xbase) {
+#pragma clang fp contract(off)
+  static_assert(FM % 4 == 0, "64-channel groups");
+  constexpr int NG = FM / 4;
+  const int8_t* sw = static_cast<const int8_t*>(sf.w);
+  const int cw = co0 + wc * 16 * FM;                 // the wave's first channel
+  i32x4 aw[2][NG];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        aw[mt][g][m] = *reinterpret_cast<const int*>(sw + static_cast<int64_t>(16 * mt + fr) * sf.k_pad + cw + 64 * g +
+                                                     16 * m + 4 * fq);
+  const bool relu = p.relu != 0;
+  i32x4 pacc[2][FN];
+#pragma unroll
+  for (int fn = 0; fn < FN; ++fn) {
+    pacc[0][fn] = i32x4{0, 0, 0, 0};
+    pacc[1][fn] = i32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      i32x4 b;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int fm = 4 * g + m;
+        const int co = cw + 16 * fm + 4 * fq;
+        const float4 sc = *reinterpret_cast<const float4*>(p.scale + co);   // padded to cout_pad
+        const float4 sh = *reinterpret_cast<const float4*>(p.shift + co);
+        const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+        uint32_t o = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = static_cast<float>(acc[fm][fn][e]) * scv[e] + shv[e];
+          if (relu) v = fmaxf(v, 0.f);
+          const float t = fminf(fmaxf(rintf(v * p.out_scale), -127.f), 127.f);
+          o |= static_cast<uint32_t>(static_cast<uint8_t>(static_cast<int8_t>(static_cast<int>(t)))) << (8 * e);
+        }
+        b[m] = static_cast<int>(o);
+      }
+      pacc[0][fn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw[0][g], b, pacc[0][fn], 0, 0, 0);
+      pacc[1][fn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(aw[1][g], b, pacc[1][fn], 0, 0, 0);
+    }
+  }
+  // the two channel halves of the tile (waves wc = 0, 1), added through LDS
+  i32x4* xch = reinterpret_cast<i32x4*>(xbase) + (wp * 64 + lane) * (2 * FN);
+  if (wc == 1) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) xch[mt * FN + fn] = pacc[mt][fn];
+  }
+  __syncthreads();
+  if (wc == 0) {
+    const int M = p.n * p.ho * p.wo;
+    int* __restrict__ part = static_cast<int*>(sf.part) + static_cast<int64_t>(co0 / (32 * FM)) * M * kW1SegCS;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int cls = 16 * mt + 4 * fq;
+      if (cls >= kW1SegCS) continue;
+#pragma unroll
+      for (int fn = 0; fn < FN; ++fn) {
+        const i32x4 o = xch[mt * FN + fn];
+        const int64_t m = px0 + wp * 16 * FN + fn * 16 + fr;
+        *reinterpret_cast<int4*>(part + m * kW1SegCS + cls) =
+            make_int4(pacc[mt][fn][0] + o[0], pacc[mt][fn][1] + o[1], pacc[mt][fn][2] + o[2], pacc[mt][fn][3] + o[3]);
+      }
+    }
+  }
+}
+
+template <typename T, int WCO, int FN, bool SEGF, bool X2 = false>
 __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1Seg& sf) {
   using C = W1Cfg<WCO, FN>;
-  constexpr int BK = 64, FM = C::FM, BCO = C::BCO, CE = 8, ESZ = 2;
+  using K = KT<T>;                                   // bf16 / int8: the same 128-B rows (conv_tile.h)
+  using FR = typename K::frag;
+  using AC = typename K::acc;
+  constexpr int ESZ = K::ESZ, BK = 128 / ESZ, CE = 16 / ESZ, FM = C::FM, BCO = C::BCO;
   constexpr int AB = C::AB, AI = C::AI, TPX = C::TPX, PXW = C::PXW, NSP = C::NSP, SB = C::SB, SPS = C::SPS;
   constexpr int NR = C::NR, RX = C::RX;
   static_assert(!SEGF || WCO == 128, "seg fusion: the 256-channel tile");
   static_assert(!(SEGF && X2), "one epilogue extension at a time");
+  static_assert(!X2 || ESZ == 2, "the fused downsample: bf16 nets");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
@@ -117,7 +198,7 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   const int s_q = px0 - s_n * hw_o;
   const int s_oh = s_q / p.wo;
   const int s_ow0 = s_q - s_oh * p.wo;
-  const int xbytes = p.n * H * W * cin * ESZ;        // < 2^31 (big_conv_supported)
+  const int xbytes = p.n * H * W * cin * ESZ;        // < 2^31 (big_conv_supported / i8_conv_supported)
   const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.x), 0, xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.wgt), 0, p.cout_pad * p.k_pad * ESZ, 0x00020000);
@@ -170,8 +251,8 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     }
   }
 
-  f32x4 acc[FM][FN];
-  bf16x8 a0[FM], b0[FN], a1[FM], b1[FN];
+  AC acc[FM][FN];
+  FR a0[FM], b0[FN], a1[FM], b1[FN];
   // The MFMAs are inline asm with the accumulator as an AGPR operand: the 256 accumulator
   // registers stay in the AGPR file for the whole loop (compiler-selected MFMAs shuffled them
   // between the files and spilled: the 128 fragment VGPRs plus addressing leave no room for a
@@ -179,15 +260,16 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   // accumulators are written by v_accvgpr_write before the first MFMA (s_nop after the init) and
   // read by the epilogue after the last one (s_nop after the loop); consecutive MFMAs on one
   // accumulator are 64 MFMAs apart.
-  auto mma = [&](f32x4& c, const bf16x8& a, const bf16x8& b) __attribute__((always_inline)) {
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+  auto mma = [&](AC& c, const FR& a, const FR& b) __attribute__((always_inline)) {
+    if constexpr (ESZ == 2) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+    else asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
   };
-  auto rd = [&](bf16x8& dst, uint32_t base, auto off_c) __attribute__((always_inline)) {
+  auto rd = [&](FR& dst, uint32_t base, auto off_c) __attribute__((always_inline)) {
     constexpr int OFF = decltype(off_c)::value;
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(base), "i"(OFF));
   };
   // read n of a substep's list (b[0..FN) then a[0..FM)) of stage ST / strip buffer BF / tap column KW
-  auto rd_item = [&](bf16x8 (&a)[FM], bf16x8 (&b)[FN], auto n_c, auto st_c, auto bf_c, auto kw_c, auto u_c)
+  auto rd_item = [&](FR (&a)[FM], FR (&b)[FN], auto n_c, auto st_c, auto bf_c, auto kw_c, auto u_c)
                      __attribute__((always_inline)) {
     constexpr int N = decltype(n_c)::value, ST = decltype(st_c)::value, BF = decltype(bf_c)::value;
     constexpr int KW = decltype(kw_c)::value, U = decltype(u_c)::value;
@@ -195,10 +277,17 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     else rd(a[N - FN], a_base[U], std::integral_constant<int, ST * AB + (N - FN) * 2048>{});
   };
 
-  // accumulator start: shift (+ residual), as conv_stag's split_init (the dispatch, w1_ok, admits
-  // only BN-scale-folded launches with a dense bf16 NHWC output: shift + residual start the
-  // accumulators, the epilogue is store_tile_x4); loads before the prologue DMA
-  {
+  // accumulator start: bf16, shift (+ residual), as conv_stag's split_init (the dispatch, w1_ok,
+  // admits only BN-scale-folded launches with a dense bf16 NHWC output: shift + residual start the
+  // accumulators, the epilogue is store_tile_x4), loads before the prologue DMA; int8, zero (the
+  // W8A8 epilogue applies scale, shift and residual)
+  if constexpr (ESZ == 1) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) issue_a(0, 0, i);
+#pragma unroll
+    for (int sh = 0; sh < C::SH; ++sh) issue_strip(0, 0, sh);
+    zero_tile(acc);
+  } else {
     uint4 rv[FM / 2][FN];
     float4 shv[FM];
 #pragma unroll
@@ -242,7 +331,7 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   // one MFMA group: acc[FMI][0..FN) += a[FMI] x b[0..FN), with fill(k) issued in the gap after MFMA
   // k (k < FN - 1): with one wave per SIMD every other instruction of the step must sit in the shadow
   // of an MFMA (a 16-cycle issue gap holds about three), or the matrix pipe idles while it issues
-  auto mgroup = [&](auto fm_c, bf16x8 (&a)[FM], bf16x8 (&b)[FN], auto&& fill) __attribute__((always_inline)) {
+  auto mgroup = [&](auto fm_c, FR (&a)[FM], FR (&b)[FN], auto&& fill) __attribute__((always_inline)) {
     constexpr int FMI = decltype(fm_c)::value;
     static_for<FN>([&](auto k_c) __attribute__((always_inline)) {
       constexpr int K = decltype(k_c)::value;
@@ -258,7 +347,7 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   // sees): a read issued in the shadow of an MFMA must never be given the registers of that
   // MFMA's own operands (the compiler would reuse them right after their last asm use, while the
   // MFMA may still be reading them); the new reads take the registers of the previous generation
-  auto keep = [&](bf16x8 (&a)[FM], bf16x8 (&b)[FN]) __attribute__((always_inline)) {
+  auto keep = [&](FR (&a)[FM], FR (&b)[FN]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < FM; ++i) asm volatile("" :: "v"(a[i]));
 #pragma unroll
@@ -426,12 +515,11 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
       if (e + 1 < nx2) issue_x2(e + 1, st ^ 1);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        bf16x8 bx[FN], ax[FM];
+        FR bx[FN], ax[FM];
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-          bx[fn] = *reinterpret_cast<const bf16x8*>(smem + b_base[0][u] + st * SB + fn * 2048);
+        for (int fn = 0; fn < FN; ++fn) bx[fn] = *reinterpret_cast<const FR*>(smem + b_base[0][u] + st * SB + fn * 2048);
 #pragma unroll
-        for (int fm = 0; fm < FM; ++fm) ax[fm] = *reinterpret_cast<const bf16x8*>(smem + a_base[u] + st * AB + fm * 2048);
+        for (int fm = 0; fm < FM; ++fm) ax[fm] = *reinterpret_cast<const FR*>(smem + a_base[u] + st * AB + fm * 2048);
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
@@ -448,7 +536,15 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
     for (int fn = 0; fn < FN; ++fn) asm volatile("" : "+a"(acc[fm][fn]));
-  if constexpr (!SEGF) {
+  if constexpr (ESZ == 1) {
+    if constexpr (SEGF) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // the LDS is free
+      w1_seg_i8<FM, FN>(p, acc, px0, co0, wc, wp, fr, fq, lane, sf, smem + AB);
+    } else {
+      // the dispatch (i8_w1_ok) admits only a dense int8 NHWC output: 16-B pieces
+      store_tile_i8_x4<FM, WCO, FN>(p, acc, px0, co0, wc, wp, fr, fq);
+    }
+  } else if constexpr (!SEGF) {
     store_tile_x4<FM, WCO, FN>(p, acc, px0, co0, wc, wp, fr, fq);
   } else {
     // the activation as store_tile_x4 would store it (ReLU, RNE to bf16, 16-B pieces: lane (fr, fq)
@@ -524,24 +620,24 @@ using W1H = W1Cfg<64, 4>;
 
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 conv_w1_kernel(const drnmi_conv_args p) {
-  conv_w1_body<128, 8, false>(p, W1Seg{nullptr, 0, nullptr});
+  conv_w1_body<uint16_t, 128, 8, false>(p, W1Seg{nullptr, 0, nullptr});
 }
 
 // the 128 x 128 tile (D-22 layer4, 128 -> 128 at K = 1152: 18 K steps per tile); two workgroups per
 // CU, so one tile's prologue strip and epilogue overlap the other's MFMAs
 __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
 conv_w1h_kernel(const drnmi_conv_args p) {
-  conv_w1_body<64, 4, false>(p, W1Seg{nullptr, 0, nullptr});
+  conv_w1_body<uint16_t, 64, 4, false>(p, W1Seg{nullptr, 0, nullptr});
 }
 
 // + the fused 1x1 downsample (x2 != NULL)
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 conv_w1_x2_kernel(const drnmi_conv_args p) {
-  conv_w1_body<128, 8, false, true>(p, W1Seg{nullptr, 0, nullptr});
+  conv_w1_body<uint16_t, 128, 8, false, true>(p, W1Seg{nullptr, 0, nullptr});
 }
 __global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
 conv_w1h_x2_kernel(const drnmi_conv_args p) {
-  conv_w1_body<64, 4, false, true>(p, W1Seg{nullptr, 0, nullptr});
+  conv_w1_body<uint16_t, 64, 4, false, true>(p, W1Seg{nullptr, 0, nullptr});
 }
 
 struct W1SegArgs {
@@ -550,7 +646,18 @@ struct W1SegArgs {
 };
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 conv_w1_seg_kernel(const W1SegArgs a) {
-  conv_w1_body<128, 8, true>(a.p, a.sf);
+  conv_w1_body<uint16_t, 128, 8, true>(a.p, a.sf);
+}
+
+// W8A8 (config C5): int8 rows of 128 channels are the bf16 tile's 128-B rows; v_mfma_i32_16x16x64_i8,
+// the W8A8 epilogue (bit-exact against oracle/int8_oracle.py like conv_i8_stag_kernel)
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+conv_w1_i8_kernel(const drnmi_conv_args p) {
+  conv_w1_body<int8_t, 128, 8, false>(p, W1Seg{nullptr, 0, nullptr});
+}
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+conv_w1_i8_seg_kernel(const W1SegArgs a) {
+  conv_w1_body<int8_t, 128, 8, true>(a.p, a.sf);
 }
 
 }  // namespace
@@ -558,7 +665,8 @@ conv_w1_seg_kernel(const W1SegArgs a) {
 static hipError_t w1_attrs() {
   static bool attr_set = false;
   if (!attr_set) {
-    for (const void* f : {reinterpret_cast<const void*>(&conv_w1_kernel), reinterpret_cast<const void*>(&conv_w1_seg_kernel)}) {
+    for (const void* f : {reinterpret_cast<const void*>(&conv_w1_kernel), reinterpret_cast<const void*>(&conv_w1_seg_kernel),
+                          reinterpret_cast<const void*>(&conv_w1_i8_kernel), reinterpret_cast<const void*>(&conv_w1_i8_seg_kernel)}) {
       const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, W1::LDS);
       if (e != hipSuccess) return e;
     }
@@ -581,8 +689,9 @@ hipError_t launch_w1_seg(const drnmi_conv_args& p, const void* seg_w, int seg_k_
   a.p = p;
   a.sf = W1Seg{seg_w, seg_k_pad, part};
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
-  hipLaunchKernelGGL(conv_w1_seg_kernel, dim3(static_cast<unsigned>((M / W1::TPX) * ((p.cout + 255) / 256))), dim3(256),
-                     W1::LDS, s, a);
+  const dim3 grid(static_cast<unsigned>((M / W1::TPX) * ((p.cout + 255) / 256)));
+  if (p.dtype == DRNMI_I8) hipLaunchKernelGGL(conv_w1_i8_seg_kernel, grid, dim3(256), W1::LDS, s, a);
+  else hipLaunchKernelGGL(conv_w1_seg_kernel, grid, dim3(256), W1::LDS, s, a);
   return hipGetLastError();
 }
 
@@ -591,7 +700,8 @@ hipError_t launch_w1(const drnmi_conv_args& p, hipStream_t s) {
   if (e0 != hipSuccess) return e0;
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const dim3 grid(static_cast<unsigned>((M / W1::TPX) * ((p.cout + 255) / 256)));
-  if (p.x2 != nullptr) hipLaunchKernelGGL(conv_w1_x2_kernel, grid, dim3(256), W1::LDS, s, p);
+  if (p.dtype == DRNMI_I8) hipLaunchKernelGGL(conv_w1_i8_kernel, grid, dim3(256), W1::LDS, s, p);
+  else if (p.x2 != nullptr) hipLaunchKernelGGL(conv_w1_x2_kernel, grid, dim3(256), W1::LDS, s, p);
   else hipLaunchKernelGGL(conv_w1_kernel, grid, dim3(256), W1::LDS, s, p);
   return hipGetLastError();
 }

@@ -713,7 +713,7 @@ class Plan:
             return
         name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a))
         # (a plain 512-channel launch runs conv_w1 unfused; fused, drnmi_conv_stag_seg's staggered tile)
-        if name is None or name.decode() not in (("conv_i8_stag_kernel",) if i8 else ("conv_stag_kernel", "conv_w1_kernel")):
+        if name is None or name.decode() not in (("conv_i8_stag_kernel", "conv_w1_i8_kernel") if i8 else ("conv_stag_kernel", "conv_w1_kernel")):
             return
         lh, lw = self.shapes[seg.dst]
         if "seg_part" not in self.bufs:
