@@ -71,6 +71,10 @@ CONV_CASES = [
     # long K, no residual, int8 out (conv_w1_i8_kernel's shapes: forced below, not auto-routed)
     (1, 4, 512, 512, 512, 3, 1, 2, 2, False, "i8"),
     (2, 3, 256, 1024, 256, 3, 1, 1, 1, False, "i8"),
+    # 128 -> 128 on whole rows, int8 out: the int8 128 x 128 tile (conv_w1h_i8_kernel; cin 128 =
+    # 9 K steps, an odd tap-group count), D-22 layer4.1 in int8 nets
+    (2, 3, 256, 128, 128, 3, 1, 1, 1, True, "i8"),
+    (1, 4, 512, 128, 128, 3, 1, 2, 2, False, "i8"),
 ]
 
 
@@ -118,7 +122,9 @@ def test_conv_i8_matches_oracle(case):
     a.res_scale, a.out_scale = res_scale, out_scale
     name = lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
     strip = wo % 256 == 0 and ks == 3 and st == 1 and cin >= 128 and cout % 256 == 0
-    assert name.startswith(("conv_i8_stag_kernel" if cin % 256 == 0 else "conv_i8_strip_kernel") if strip
+    w1h = wo % 256 == 0 and ks == 3 and st == 1 and cin % 128 == 0 and cout == 128 and out == "i8"
+    assert name.startswith("conv_w1h_i8_kernel" if w1h else
+                           ("conv_i8_stag_kernel" if cin % 256 == 0 else "conv_i8_strip_kernel") if strip
                            else ("conv_i8_kernel<", "conv_i8_occ2_kernel<")), name
     if ks == 1:   # 1x1 launches take the two-workgroups-per-CU tile
         assert name.startswith("conv_i8_occ2_kernel<"), name
@@ -139,10 +145,10 @@ def test_conv_i8_matches_oracle(case):
     else:
         np.testing.assert_array_equal(got, ref)
         assert np.abs(ref.astype(np.int32)).max() < 127 or (ref == 127).mean() < 0.5   # not all saturated
-    if strip and cin % 256 == 0:
-        # both int8 strip tiles, forced: tile 19 (conv_i8_stag_kernel) and, with an int8 output,
-        # tile 22 (conv_w1_i8_kernel) -- the same oracle bits
-        for t in (19, 22) if out == "i8" else (19,):
+    if (strip and cin % 256 == 0) or w1h:
+        # the int8 strip tiles, forced: tile 19 (conv_i8_stag_kernel) and, with an int8 output,
+        # tiles 22 (conv_w1_i8_kernel) and 23 (conv_w1h_i8_kernel) -- the same oracle bits
+        for t in (23,) if w1h else (19, 22, 23) if out == "i8" else (19,):
             a.tile = t
             y.fill_(0)
             L.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), _stream()), f"conv i8 tile {t}")

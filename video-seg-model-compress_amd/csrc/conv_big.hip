@@ -918,6 +918,16 @@ bool i8_w1_ok(const drnmi_conv_args& p) {
          p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
 }
 bool i8_w1_auto(const drnmi_conv_args& p) { return false && i8_w1_ok(p); }
+// int8 conv_w1h (conv_w1h_i8_kernel: 128 x 128 tiles, two workgroups per CU, odd tap-group counts
+// too): whole-row strip geometry, cin % 128 == 0, 128-channel blocks, dense int8 NHWC output;
+// auto-routed at 128 output channels (D-22 layer4.1 in int8 nets)
+bool i8_w1h_ok(const drnmi_conv_args& p) {
+  return strip_ok(p) && p.cin % 128 == 0 && p.cout % 128 == 0 && p.out_dtype == DRNMI_I8 && p.y_sc == 1 &&
+         p.y_sp == p.cout && p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
+}
+bool i8_w1h_pick(const drnmi_conv_args& p) {
+  return p.tile == 4 + kW1H || (p.tile < 0 && i8_w1h_ok(p) && p.cout <= 128);
+}
 // tile ids 19 / 22 force the staggered / one-wave-per-SIMD int8 tile (the bit-identity tests)
 bool i8_w1_pick(const drnmi_conv_args& p) {
   return p.tile == 4 + kW1 ? true : p.tile == 4 + kStag ? false : i8_w1_auto(p);
@@ -927,6 +937,11 @@ int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!i8_conv_supported(p)) return DRNMI_ENOTSUP;
   const int v = i8_variant(p);
   if ((p.cout + kI8Variants[v].bco - 1) / kI8Variants[v].bco * kI8Variants[v].bco > p.cout_pad) return DRNMI_EINVAL;
+  if (p.ks == 3 && i8_w1h_pick(p)) {
+    if (!i8_w1h_ok(p)) return DRNMI_ENOTSUP;
+    const hipError_t e = launch_w1h(p, s);
+    return e == hipErrorInvalidValue ? DRNMI_ENOTSUP : static_cast<int>(e);
+  }
   if (p.ks == 3 && i8_stag_ok(p)) {
     const bool w1 = i8_w1_pick(p);
     if (w1 && !i8_w1_ok(p)) return DRNMI_ENOTSUP;
@@ -944,6 +959,7 @@ int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
 const char* i8_conv_name(const drnmi_conv_args& p) {
   if (!i8_conv_supported(p)) return nullptr;
   const int v = i8_variant(p);
+  if (p.ks == 3 && i8_w1h_pick(p)) return i8_w1h_ok(p) ? "conv_w1h_i8_kernel" : nullptr;
   if (p.ks == 3 && i8_stag_ok(p)) return !i8_w1_pick(p) ? "conv_i8_stag_kernel" : i8_w1_ok(p) ? "conv_w1_i8_kernel" : nullptr;
   if (p.ks == 3 && i8_strip_ok(p)) return "conv_i8_strip_kernel";
   return p.ks == 3 ? kI8Variants[v].name3 : kI8Variants[v].name1;

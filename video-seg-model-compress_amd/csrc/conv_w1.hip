@@ -158,7 +158,8 @@ __device__ __forceinline__ void w1_seg_i8(const drnmi_conv_args& p, const i32x4 
   }
 }
 
-template <typename T, int WCO, int FN, bool SEGF, bool X2 = false>
+// ODDOK: also an odd number of tap groups (int8 at cin 128: 9 K steps of 128 channels)
+template <typename T, int WCO, int FN, bool SEGF, bool X2 = false, bool ODDOK = false>
 __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1Seg& sf) {
   using C = W1Cfg<WCO, FN>;
   using K = KT<T>;                                   // bf16 / int8: the same 128-B rows (conv_tile.h)
@@ -185,7 +186,7 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
   const int lc = 31 - __builtin_clz(cin);
   const int H = p.h, W = p.w, dil = p.dil;
   const int nk = 9 * cin / BK;
-  const int ngroups = nk / 3;                        // even: cin % 128 == 0
+  const int ngroups = nk / 3;                        // even (bf16: cin % 128 == 0), or ODDOK
   const int fr = lane & 15;
   const int fq = lane >> 4;
   const int lrow = lane >> 3;
@@ -472,12 +473,22 @@ __device__ __forceinline__ void conv_w1_body(const drnmi_conv_args& p, const W1S
     step(I1{}, gp_c, F{}, g);
     step(I2{}, gp_c, lastg_c, g);
   };
-  for (int g = 0; g < ngroups - 2; g += 2) {
-    group(I0{}, F{}, g);
-    group(I1{}, F{}, g + 1);
+  if (ODDOK && (ngroups & 1)) {
+    // odd: pairs, then the last group alone (buffer 0; its clamped strip re-fetches land in
+    // buffer 1, which the pair before it finished reading at B_{3 (ngroups - 1)})
+    for (int g = 0; g < ngroups - 1; g += 2) {
+      group(I0{}, F{}, g);
+      group(I1{}, F{}, g + 1);
+    }
+    group(I0{}, T_{}, ngroups - 1);
+  } else {
+    for (int g = 0; g < ngroups - 2; g += 2) {
+      group(I0{}, F{}, g);
+      group(I1{}, F{}, g + 1);
+    }
+    group(I0{}, F{}, ngroups - 2);
+    group(I1{}, T_{}, ngroups - 1);
   }
-  group(I0{}, F{}, ngroups - 2);
-  group(I1{}, T_{}, ngroups - 1);
   if constexpr (X2) {
     // the fused 1x1 downsample (x2 != NULL: D-22 layer4.0 / 5.0 / 6.0 conv2) as cin2 / 64 more K
     // steps after the taps, in conv_stag_x2's order (so the same bits): step e reads weight
@@ -659,6 +670,11 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 conv_w1_i8_seg_kernel(const W1SegArgs a) {
   conv_w1_body<int8_t, 128, 8, true>(a.p, a.sf);
 }
+// the int8 128 x 128 tile (D-22 layer4.1 in int8 nets: cin 128 = 9 K steps, an odd tap-group count)
+__global__ void __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2)))
+conv_w1h_i8_kernel(const drnmi_conv_args p) {
+  conv_w1_body<int8_t, 64, 4, false, false, true>(p, W1Seg{nullptr, 0, nullptr});
+}
 
 }  // namespace
 
@@ -673,7 +689,8 @@ static hipError_t w1_attrs() {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_w1_x2_kernel),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, W1::LDS);
     if (e != hipSuccess) return e;
-    for (const void* f : {reinterpret_cast<const void*>(&conv_w1h_kernel), reinterpret_cast<const void*>(&conv_w1h_x2_kernel)}) {
+    for (const void* f : {reinterpret_cast<const void*>(&conv_w1h_kernel), reinterpret_cast<const void*>(&conv_w1h_x2_kernel),
+                          reinterpret_cast<const void*>(&conv_w1h_i8_kernel)}) {
       const hipError_t e2 = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, W1H::LDS);
       if (e2 != hipSuccess) return e2;
     }
@@ -711,7 +728,8 @@ hipError_t launch_w1h(const drnmi_conv_args& p, hipStream_t s) {
   if (e0 != hipSuccess) return e0;
   const int64_t M = static_cast<int64_t>(p.n) * p.ho * p.wo;
   const dim3 grid(static_cast<unsigned>((M / W1H::TPX) * ((p.cout + 127) / 128)));
-  if (p.x2 != nullptr) hipLaunchKernelGGL(conv_w1h_x2_kernel, grid, dim3(256), W1H::LDS, s, p);
+  if (p.dtype == DRNMI_I8) hipLaunchKernelGGL(conv_w1h_i8_kernel, grid, dim3(256), W1H::LDS, s, p);
+  else if (p.x2 != nullptr) hipLaunchKernelGGL(conv_w1h_x2_kernel, grid, dim3(256), W1H::LDS, s, p);
   else hipLaunchKernelGGL(conv_w1h_kernel, grid, dim3(256), W1H::LDS, s, p);
   return hipGetLastError();
 }

@@ -41,11 +41,14 @@ TORCH_OF_CODE = {_lib.DRNMI_F32: torch.float32, _lib.DRNMI_BF16: torch.bfloat16,
 # (conv_i8_kernel: K steps of 64/128 int8 channels); the full-resolution small-channel layers
 # (stem, layer1-3: ~5 % of D-22's FLOPs) stay bf16.
 INT8_MIN_CIN = 64
-# ... and whose output has at least this many channels.  256: D-22's 128-channel layer4 stays on
+# ... and whose output has at least this many channels.  256: D-22's 128-channel layer4.0 stays on
 # the bf16 row / staggered kernels (s2row, stag128 with the downsample folded in), which beat the
-# int8 tiles there (cin 128 gives the int8 staggered tile an odd tap-group count): 1786-1788 vs
-# 1750-1755 fps interleaved (profiles/r6_int8_fusions).
+# int8 tiles there: 1786-1788 vs 1750-1755 fps interleaved (profiles/r6_int8_fusions).
 INT8_MIN_COUT = 256
+# ... except the 128 -> 128 3x3 stride-1 convs without a folded downsample (D-22 layer4.1): the
+# int8 128 x 128 tile (conv_w1h_i8_kernel, odd tap-group counts) serves them (INT8_LAYER4 = False
+# keeps them bf16)
+INT8_LAYER4 = True
 
 # (cin_stride, cout, ks, stride, dil) served by the LDS-patch kernel (bf16 only; include/drnmi.h)
 # (32 -> 64 stride 2 runs faster on the K-32 LDS-DMA implicit GEMM: 67 vs 108 us per 4 frames)
@@ -222,9 +225,18 @@ class PackedNet:
         g = self.graph
         # (cout >= 128 too: the int8 tiles are 128 channels wide; the 64-channel layer3 convs keep
         # the bf16 halo kernel)
+        producer = {nd.dst: i for i, nd in enumerate(g.nodes)}
+
+        def layer4_shape(nd):
+            c = nd.conv
+            if not INT8_LAYER4 or (c.in_channels, c.out_channels, c.kernel_size[0], c.stride[0], c.groups) != \
+                    (128, 128, 3, 1, 1) or self.cstride[nd.src] != 128:
+                return False
+            # a block conv2 whose residual is a downsample keeps the bf16 tile with it folded in
+            return not (nd.res and nd.res in producer and g.nodes[producer[nd.res]].name.endswith("downsample.0"))
         elig = {i for i, nd in enumerate(g.nodes)
                 if self.cstride[nd.src] >= INT8_MIN_CIN and nd.conv.kernel_size[0] in (1, 3)
-                and (nd.conv.out_channels >= INT8_MIN_COUT or nd.out_fp32_nchw)}
+                and (nd.conv.out_channels >= INT8_MIN_COUT or nd.out_fp32_nchw or layer4_shape(nd))}
         readers = {}
         for i, nd in enumerate(g.nodes):
             for v in (nd.src, nd.res):
@@ -234,7 +246,6 @@ class PackedNet:
             nd = g.nodes[i]
             if not nd.out_fp32_nchw and readers.get(nd.dst) and all(j in elig for j in readers[nd.dst]):
                 self.vcode[nd.dst] = _lib.DRNMI_I8
-        producer = {nd.dst: i for i, nd in enumerate(g.nodes)}
         need = {v for i in elig for v in (g.nodes[i].src, g.nodes[i].res) if v}
         missing = sorted(v for v in need | set(self.vcode) if v not in self.act_scales)
         if missing:
