@@ -122,7 +122,9 @@ def test_conv_i8_matches_oracle(case):
     a.res_scale, a.out_scale = res_scale, out_scale
     name = lib.drnmi_conv_kernel_name(ctypes.byref(a)).decode()
     strip = wo % 256 == 0 and ks == 3 and st == 1 and cin >= 128 and cout % 256 == 0
-    w1h = wo % 256 == 0 and ks == 3 and st == 1 and cin % 128 == 0 and cout == 128 and out == "i8"
+    # conv_w1h_i8_kernel: whole rows, int8 out, cin / cout <= 256 (D-22 layer4.1, layer5)
+    w1h = wo % 256 == 0 and ks == 3 and st == 1 and cin % 128 == 0 and cout % 128 == 0 and out == "i8" and \
+        cin <= 256 and cout <= 256
     assert name.startswith("conv_w1h_i8_kernel" if w1h else
                            ("conv_i8_stag_kernel" if cin % 256 == 0 else "conv_i8_strip_kernel") if strip
                            else ("conv_i8_kernel<", "conv_i8_occ2_kernel<")), name
@@ -148,7 +150,7 @@ def test_conv_i8_matches_oracle(case):
     if (strip and cin % 256 == 0) or w1h:
         # the int8 strip tiles, forced: tile 19 (conv_i8_stag_kernel) and, with an int8 output,
         # tiles 22 (conv_w1_i8_kernel) and 23 (conv_w1h_i8_kernel) -- the same oracle bits
-        for t in (23,) if w1h else (19, 22, 23) if out == "i8" else (19,):
+        for t in ((19, 22, 23) if cin % 256 == 0 and cout % 256 == 0 else (23,)) if out == "i8" else (19,):
             a.tile = t
             y.fill_(0)
             L.check(lib.drnmi_conv2d_bn_act(ctypes.byref(a), _stream()), f"conv i8 tile {t}")
