@@ -117,3 +117,17 @@ def test_fused_second_input_never_routes_to_halo():
     a.scale = ctypes.cast(sc, ctypes.c_void_p).value      # an unfolded scale: not the halo x2 form
     name = lib.drnmi_conv_kernel_name(ctypes.byref(a))
     assert name is None or not name.decode().startswith("conv_halo")
+
+
+def test_kernel_peak_by_name():
+    """bench.py prices the dominant kernel at the peak of the arithmetic it runs: every int8 kernel
+    name the library reports (conv_i8_*, conv_w1_i8_*, conv_w1h_i8_*) at the int8 peak, even in
+    int8 nets whose base precision is bf16."""
+    from drnmi.roofline import MFMA_PEAK, kernel_peak
+    for n in ("conv_i8_stag_kernel", "conv_i8_stag_seg_kernel", "conv_w1_i8_kernel", "conv_w1_i8_seg_kernel",
+              "conv_w1h_i8_kernel", "conv_i8_occ2_kernel<1, 128, 1, 2, 64>"):
+        assert kernel_peak(n, "bf16") == MFMA_PEAK["int8"], n
+    for n in ("conv_stag_kernel", "conv_w1_kernel", "conv_w1h_kernel", "conv_w1_seg_kernel", "front3_kernel"):
+        assert kernel_peak(n, "bf16") == MFMA_PEAK["bf16"], n
+    assert kernel_peak("conv_x6_kernel<3, 128, 2, 4>", "fp32x") == MFMA_PEAK["fp32x"]
+    assert kernel_peak("patch_f32_kernel<0, 16, 7, 1, 4, 64>", "fp32x") == MFMA_PEAK["fp32"]

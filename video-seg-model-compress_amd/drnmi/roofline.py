@@ -18,7 +18,7 @@ MFMA_PEAK = {"bf16": 2.5e15, "fp32": 157.3e12, "int8": 5.0e15, "fp32x": 2.5e15 /
 
 def kernel_peak(kernel_name: str, base: str) -> float:
     """MFMA peak of the arithmetic a kernel (named as rocprofv3 names it) runs."""
-    if kernel_name.startswith("conv_i8"):
+    if kernel_name.startswith("conv_i8") or "_i8_" in kernel_name:   # conv_i8_*, conv_w1_i8_*, conv_w1h_i8_*
         return MFMA_PEAK["int8"]
     if kernel_name.startswith("conv_x6"):
         return MFMA_PEAK["fp32x"]
