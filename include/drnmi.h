@@ -136,7 +136,13 @@ typedef struct drnmi_conv_args {
  *                    fp32).  tile -1 picks the bf16 LDS-DMA kernel (tiles 4..7: 128/256/64/64
  *                    output channels x 256 pixels, tile 6 with 32-channel K steps, tile 7 with
  *                    64; cin >= 64, ks 1 or 3) when it applies, else a
- *                    register-staged tile 0..3 by cout.
+ *                    register-staged tile 0..3 by cout.  Whole 256-pixel output rows (3x3, stride
+ *                    1, cin % 128 == 0) route to the strip tiles: 19 conv_stag (256 / 128
+ *                    channels, 8 waves with staggered SIMD partners), 22 conv_w1 (the same tile
+ *                    as 4 waves of 128 x 128, one per SIMD; auto at cin >= 512 without residual),
+ *                    23 conv_w1h (128 x 128 tiles, two workgroups per CU; auto at cout 128) --
+ *                    all with the same K order, so bit-identical.  int8 (dtype DRNMI_I8) takes
+ *                    19 / 22 / 23 as its int8 forms (auto: 23 at cin, cout <= 256, else 19).
  *  DRNMI_ALGO_PATCH  bf16-only small-channel direct conv for the full-resolution layers
  *                    (lmodels/drn.py:132-137 layer0, :201-211 layer1/layer2): the input tile
  *                    plus halo is staged once in LDS and reused by all ks*ks taps; weights stay
@@ -287,7 +293,8 @@ int drnmi_up8_labels_nhwc(const float* logits, int32_t cs, const float* up_w, vo
  * 256-channel block's partial logits go to partials[cout / 256][n*ho*wo][20] (fp32, 16-B aligned):
  * partial_b[m][k] = sum over the block's channels c of seg_w[k][c] * bf16(relu(conv)[m][c]).
  * seg_w: packed bf16 [seg_rows >= 32][seg_k_pad] (rows 19.. zero).  DRNMI_ENOTSUP if the conv does
- * not take the staggered tile.
+ * not take the staggered tile.  It runs on the one-wave-per-SIMD tile (conv_w1_seg_kernel /
+ * conv_w1_i8_seg_kernel); a->tile == 19 forces the staggered one (the same partials, bit for bit).
  * int8 nets (a->dtype DRNMI_I8, out_dtype DRNMI_I8, the W8A8 epilogue of drnmi_conv2d_bn_act, no
  * residual): seg_w is the int8 seg conv's packed weights and the partials are int32,
  * partial_b[m][k] = sum over the block's channels c of seg_w[k][c] * q8[m][c], q8 = the int8 value
