@@ -813,9 +813,9 @@ def test_conv_fused_downsample(case):
     name = _lib.load().drnmi_conv_kernel_name(ctypes.byref(a)).decode()
     stag = ks == 3 and wo % 256 == 0 and cin % 128 == 0 and kp == k1 + cin2
     s1x2 = halo and cin == 64 and cout == 64 and cin2 == 32 and s2 == 2 and dil == 1   # conv_s1x2row_kernel
-    # whole-row strip shapes: the staggered x2 tiles (the conv_w1 / conv_w1h x2 forms, bit-identical,
-    # measured slower inside the network: profiles/r11_w1h)
-    assert name.startswith("conv_stag128_x2_kernel" if stag and cout <= 128 else "conv_stag_x2_kernel" if stag
+    # whole-row strip shapes: conv_w1h_x2 at 128 channels (layer4.0), else the staggered x2 tile (the
+    # conv_w1 / 256-channel conv_w1h x2 forms measured slower inside the network: profiles/r11_w1h)
+    assert name.startswith("conv_w1h_x2_kernel" if stag and cout <= 128 else "conv_stag_x2_kernel" if stag
                            else "conv_s1x2row_kernel" if s1x2 else "conv_halo_kernel" if halo else "conv_big_kernel"), name
     _lib.check(_lib.load().drnmi_conv2d_bn_act(ctypes.byref(a), ctypes.c_void_p(_lib.stream_ptr())), "fused ds")
     torch.cuda.synchronize()

@@ -732,7 +732,7 @@ bool w1h_ok(const drnmi_conv_args& p) {
   return stag_ok(p) && p.cout % 128 == 0 && p.scale == nullptr && p.out_dtype == DRNMI_BF16 &&
          p.y_sc == 1 && p.y_sp == p.cout && p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
 }
-bool w1h_auto(const drnmi_conv_args& p) { return w1h_ok(p) && p.x2 == nullptr && p.cout <= 128; }
+bool w1h_auto(const drnmi_conv_args& p) { return w1h_ok(p) && p.cout <= 128; }
 
 template <int KS, bool PERSIST>
 hipError_t launch_base(const drnmi_conv_args& p, int base, hipStream_t s) {
