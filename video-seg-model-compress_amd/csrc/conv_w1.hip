@@ -1,10 +1,11 @@
-// One-wave-per-SIMD strip conv (bf16): conv_w1_kernel.  Own translation unit (its 400-register
-// allocation must not be perturbed by the other tiles, cdna_hip_programming.md §5.4 rule 19).
+// One-wave-per-SIMD strip convs: conv_w1_kernel and the forms of the same template (below).  Own
+// translation unit (their 400-512-register allocations must not be perturbed by the other tiles,
+// cdna_hip_programming.md §5.4 rule 19).
 //
-// Same tile (256 output channels x one 256-pixel run of an output row, 3x3 stride 1, cin % 128 ==
-// 0), same LDS image (two 32-KB weight stages, two 33-KB input strips; DMA'd as in conv_stag), same
-// K order and per-accumulator MFMA order as conv_stag_kernel -- so the output is bit-identical to
-// it -- but 4 waves of 128 channels x 128 pixels instead of 8 waves of 128 x 64:
+// conv_w1: the same tile (256 output channels x one 256-pixel run of an output row, 3x3 stride 1,
+// cin % 128 == 0), LDS image (two 32-KB weight stages, two 33-KB input strips; DMA'd as in
+// conv_stag), K order and per-accumulator MFMA order as conv_stag_kernel -- so the output is
+// bit-identical to it -- but 4 waves of 128 channels x 128 pixels instead of 8 waves of 128 x 64:
 //
 //   * per 32-deep substep a wave reads 8 A + 8 B fragments (16 KB) for 64 MFMAs; the 8-wave tile
 //     reads 8 A + 4 B per wave for 32 MFMAs, so the LDS read bytes per MFMA drop by a third (the
@@ -17,17 +18,24 @@
 //     lgkmcnt), every DMA piece issued a whole K step before the barrier that publishes it.
 //
 // Schedule of K step t (stage t & 1, strip buffer g & 1, t = 3 g + kw), B_t = the barrier that
-// publishes step t's weights (and, for kw = 0, group g's strip):
-//   X  groups 0..7 (substep 0): wait for a0[fm] (all b0 landed), issue 2 reads of substep 1
-//      (b1[0..7] first, then a1[0..7]), 8 MFMAs acc[fm][*] += a0[fm] x b0[*];
-//   Y  groups 0..3 (substep 1): wait for a1[fm], 8 MFMAs;
-//      vmcnt(0) lgkmcnt(0) s_barrier = B_{t+1}: every wave's DMA for step t + 1 has landed and
+// publishes step t's weights (and, for kw = 0, group g's strip); FM x FN fragments per wave
+// (conv_w1: 8 x 8):
+//   X  groups 0..FM-1 (substep 0): wait for a0[fm] (all b0 landed), issue FM+FN / FM reads of
+//      substep 1 (b1 first, then a1), FN MFMAs acc[fm][*] += a0[fm] x b0[*];
+//   Y  groups 0..FM/2-1 (substep 1): wait for a1[fm], FN MFMAs;
+//      vmcnt lgkmcnt(0) s_barrier = B_{t+1}: every wave's DMA for step t + 1 has landed and
 //      every wave has finished reading stage t & 1 and (kw = 2) strip g;
-//   Y  groups 4..7: issue the 16 reads of step t + 1's substep 0 (b0 first) and the DMA of step
+//   Y  groups FM/2..FM-1: issue the reads of step t + 1's substep 0 (b0 first) and the DMA of step
 //      t + 2's weights (into stage t & 1, just released; past the last step a re-fetch) and of one
-//      third of the next strip
-//      (group g' + 1 for t + 1 = 3 g' + k': its buffer was last read in step 3 g' - 1, before
-//      B_{3 g'}); 8 MFMAs each.
+//      third of the next strip (group g' + 1 for t + 1 = 3 g' + k': its buffer was last read in
+//      step 3 g' - 1, before B_{3 g'}), spread over the groups' MFMA gaps; FN MFMAs each.
+//
+// Forms (W1Cfg<WCO, FN> derives the counts above from the tile geometry): conv_w1 (WCO 128, FN 8,
+// one workgroup per CU), conv_w1h (WCO 64, FN 4: 128 x 128 tiles, 67 KB of LDS, two workgroups per
+// CU, so one tile's prologue and epilogue overlap the other's MFMAs), their x2 forms (the folded
+// 1x1 downsample as extra K steps after the taps, as conv_stag_x2), the seg-fused form (the seg
+// classifier in the epilogue) and the int8 forms (T = int8_t: the same 128-B rows of 128 channels,
+// v_mfma_i32_16x16x64_i8, the W8A8 epilogues; ODDOK walks an odd tap-group count).
 // Reference: lmodels/drn.py:27-29 (conv3x3, dilation = padding), :49-65 (BasicBlock convs).
 #include "common.h"
 #include "conv_tile.h"
