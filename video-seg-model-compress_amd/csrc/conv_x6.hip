@@ -249,17 +249,25 @@ conv_x6_kernel(const drnmi_conv_args p) {
     ds_rd<2 * C::A_PLANE>(a3, va);                     // fragment 0's planes, then the B rows
     ds_rd<C::A_PLANE>(a2, va);
     ds_rd<0>(a1, va);
-    float4 blo[C::FN], bhi[C::FN];                     // (hipcc waits for these: lgkmcnt(0))
-#pragma unroll
-    for (int fn = 0; fn < C::FN; ++fn) {
-      blo[fn] = *reinterpret_cast<const float4*>(smem + vb0 + C::A_BYTES + fn * 2048);
-      bhi[fn] = *reinterpret_cast<const float4*>(smem + vb1 + C::A_BYTES + fn * 2048);
-    }
+    // the B rows as inline-asm reads too, so fragment fn's pair is waited for alone (fm 0's first
+    // three groups run interleaved with the splits below, on each pair as it lands, instead of
+    // after an lgkmcnt(0) for all eleven reads: the step's opening burst of LDS reads no longer
+    // idles the matrix pipe until its last read returns)
+    f32x4 blo[C::FN], bhi[C::FN];
+    static_assert(C::FN == 4, "four B fragments");
+    ds_rd<C::A_BYTES + 0 * 2048>(blo[0], vb0);
+    ds_rd<C::A_BYTES + 0 * 2048>(bhi[0], vb1);
+    ds_rd<C::A_BYTES + 1 * 2048>(blo[1], vb0);
+    ds_rd<C::A_BYTES + 1 * 2048>(bhi[1], vb1);
+    ds_rd<C::A_BYTES + 2 * 2048>(blo[2], vb0);
+    ds_rd<C::A_BYTES + 2 * 2048>(bhi[2], vb1);
+    ds_rd<C::A_BYTES + 3 * 2048>(blo[3], vb0);
+    ds_rd<C::A_BYTES + 3 * 2048>(bhi[3], vb1);
     __builtin_amdgcn_sched_barrier(0);
     // split passes: u1 = bf16(x), u2 = bf16(x - u1), u3 = bf16(x - u1 - u2) (common.h split3)
     bf16x8 b1[C::FN], b2[C::FN], b3[C::FN];
     auto pairs = [&](int fn, int i) {
-      const float4& v = i < 2 ? blo[fn] : bhi[fn];
+      const f32x4& v = i < 2 ? blo[fn] : bhi[fn];
       return (i & 1) ? f32x2_t{v.z, v.w} : f32x2_t{v.x, v.y};
     };
     auto split_b1 = [&](int fn) {
@@ -286,20 +294,38 @@ conv_x6_kernel(const drnmi_conv_args p) {
       for (int i = 0; i < 4; ++i) u[i] = pk_bf16x2((pairs(fn, i) - widen_bf16x2(v1[i])) - widen_bf16x2(v2[i]));
       b3[fn] = __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
     };
-#pragma unroll
-    for (int fn = 0; fn < C::FN; ++fn) { split_b1(fn); split_b2(fn); split_b3(fn); }
     auto grp = [&](int fm, const bf16x8& a, const bf16x8 (&b)[C::FN]) {
 #pragma unroll
       for (int fn = 0; fn < C::FN; ++fn) acc[fm][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[fn], acc[fm][fn], 0, 0, 0);
+    };
+    // fm 0's group 1 on each B pair as it lands (the reads return in issue order: a3 a2 a1, then
+    // the pairs), then its groups 2 / 3 with the b2 / b3 splits of each fragment just ahead of
+    // its MFMA; every accumulator keeps its product order
+    auto b_wait = [&](auto fn_c) {
+      constexpr int FNI = decltype(fn_c)::value;
+      // the wait redefines the pair (an asm output): no use of it can be hoisted above the wait
+      // (a plain asm wait let the compiler convert all four pairs right after the first one)
+      asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(blo[FNI]), "+v"(bhi[FNI]) : "n"(2 * (C::FN - 1 - FNI)) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      split_b1(FNI);
+      acc[0][FNI] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3, b1[FNI], acc[0][FNI], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);               // the MFMA goes out before the next wait
     };
 #pragma unroll
     for (int fm = 0; fm < C::FM; ++fm) {
       // read order per fragment: a3(fm) after group 1 of fm - 1, a2(fm) after its group 4, a1(fm)
       // after its group 6 (each into the registers that group retired); before group 1 the
       // newer reads in flight are a2(fm), a1(fm)
-      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      grp(fm, a3, b1);                                   // 1: a3 b1
+      if (fm == 0) {
+        b_wait(std::integral_constant<int, 0>{});
+        b_wait(std::integral_constant<int, 1>{});
+        b_wait(std::integral_constant<int, 2>{});
+        b_wait(std::integral_constant<int, 3>{});       // 1: a3 b1, every B read landed
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        grp(fm, a3, b1);                                 // 1: a3 b1
+      }
       if (fm + 1 < C::FM) ds_rd_fm(a3, va, fm + 1, 2);
       // branch-free (a branch here let the reads above sink past it, next to their MFMAs): the
       // last step re-fetches its own K step into the stage step t - 1 used, which nobody reads
@@ -310,12 +336,28 @@ conv_x6_kernel(const drnmi_conv_args p) {
       if (fm + 1 < C::FM) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
       else asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      grp(fm, a2, b2);                                   // 2: a2 b2
+      if (fm == 0) {
+#pragma unroll
+        for (int fn = 0; fn < C::FN; ++fn) {             // 2: a2 b2
+          split_b2(fn);
+          acc[0][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b2[fn], acc[0][fn], 0, 0, 0);
+        }
+      } else {
+        grp(fm, a2, b2);                                 // 2: a2 b2
+      }
       // a1(fm) landed: newer in flight a3(fm + 1)
       if (fm + 1 < C::FM) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      grp(fm, a1, b3);                                   // 3: a1 b3
+      if (fm == 0) {
+#pragma unroll
+        for (int fn = 0; fn < C::FN; ++fn) {             // 3: a1 b3
+          split_b3(fn);
+          acc[0][fn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b3[fn], acc[0][fn], 0, 0, 0);
+        }
+      } else {
+        grp(fm, a1, b3);                                 // 3: a1 b3
+      }
       __builtin_amdgcn_sched_barrier(0);
       grp(fm, a2, b1);                                   // 4: a2 b1
       if (fm + 1 < C::FM) ds_rd_fm(a2, va, fm + 1, 1);
