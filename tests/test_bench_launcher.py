@@ -94,3 +94,51 @@ def test_finetune_world_mismatch_refused():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench_finetune.py"), "--gpus", "1", *FT_SMALL],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+class _Ev:
+    """a stand-in for torch.cuda.Event: elapsed_time between two host-side stamps (ms)"""
+    def __init__(self, t):
+        self.t = t
+
+    def elapsed_time(self, other):
+        return other.t - self.t
+
+
+def test_step_spread_reports_one_off_stall():
+    """bench.step_spread: per-step min / median / max from the step-boundary events, the slowest
+    step's index and the time spent beyond 1.5x the median (a one-off stall, not a steady cost)."""
+    import bench
+    steps = [5.0] * 9 + [40.0] + [5.0] * 10            # a 35-ms stall in step 9
+    t, marks = 0.0, [_Ev(0.0)]
+    for d in steps:
+        t += d
+        marks.append(_Ev(t))
+    s = bench.step_spread(marks)
+    assert s["steps"] == 20 and s["min"] == 5.0 and s["median"] == 5.0 and s["max"] == 40.0
+    assert s["max_at_step"] == 9 and s["stall_ms"] == 35.0
+    assert bench.step_spread(marks[:1]) is None
+
+
+def test_newest_first_orders_rounds_numerically(tmp_path):
+    """bench.newest_first: r11s_ > r11p_ > r10p_ > r9zz_ (string order would put r9zz first)."""
+    import bench
+    for n in ("r9zz_bf16_pmc_mfma.json", "r10p_bf16_pmc_mfma.json", "r11p_bf16_pmc_mfma.json",
+              "r11s_bf16_pmc_mfma.json", "misc_pmc_mfma.json"):
+        (tmp_path / n).write_text("{}")
+    got = [os.path.basename(f) for f in bench.newest_first(str(tmp_path / "*_pmc_mfma.json"))]
+    assert got == ["r11s_bf16_pmc_mfma.json", "r11p_bf16_pmc_mfma.json", "r10p_bf16_pmc_mfma.json",
+                   "r9zz_bf16_pmc_mfma.json", "misc_pmc_mfma.json"]
+
+
+def test_committed_mfma_captures_cover_every_precision_line():
+    """Every precision the default bench line reports has a committed MFMA-busy capture of its exact
+    workload (roofline.mfma_busy comes from it; the driver's GPU box has no rocprofv3 run)."""
+    import types
+    import bench
+    args = types.SimpleNamespace(arch="drn_d_22", height=1024, width=2048, batch=8, precision="bf16")
+    for prec in ("bf16", "fp32x", "fp32", "int8"):
+        m = bench.pmc_mfma(args, prec)
+        assert m.get("kernels"), prec
+        busy = [v["mfma_busy"] for v in m["kernels"].values() if v.get("mfma_busy") is not None]
+        assert busy and all(0.0 <= b <= 1.0 for b in busy), prec
