@@ -917,7 +917,6 @@ bool i8_w1_ok(const drnmi_conv_args& p) {
   return i8_stag_ok(p) && p.cout % 256 == 0 && p.out_dtype == DRNMI_I8 && p.y_sc == 1 && p.y_sp == p.cout &&
          p.y_sn == static_cast<int64_t>(p.ho) * p.wo * p.cout;
 }
-bool i8_w1_auto(const drnmi_conv_args& p) { return false && i8_w1_ok(p); }
 // int8 conv_w1h (conv_w1h_i8_kernel: 128 x 128 tiles, two workgroups per CU, odd tap-group counts
 // too): whole-row strip geometry, cin % 128 == 0, 128-channel blocks, dense int8 NHWC output;
 // auto-routed at cin, cout <= 256 (D-22 layer4.1, layer5 in int8 nets: profiles/r11_int8_layer4)
@@ -928,10 +927,8 @@ bool i8_w1h_ok(const drnmi_conv_args& p) {
 bool i8_w1h_pick(const drnmi_conv_args& p) {
   return p.tile == 4 + kW1H || (p.tile < 0 && i8_w1h_ok(p) && (p.cout <= 128 || p.cin == 128 || (p.cin <= 256 && p.cout <= 256)));
 }
-// tile ids 19 / 22 force the staggered / one-wave-per-SIMD int8 tile (the bit-identity tests)
-bool i8_w1_pick(const drnmi_conv_args& p) {
-  return p.tile == 4 + kW1 ? true : p.tile == 4 + kStag ? false : i8_w1_auto(p);
-}
+// tile id 22 forces the one-wave-per-SIMD int8 tile (the bit-identity tests); else the staggered one
+bool i8_w1_pick(const drnmi_conv_args& p) { return p.tile == 4 + kW1; }
 
 int i8_conv_dispatch(const drnmi_conv_args& p, hipStream_t s) {
   if (!i8_conv_supported(p)) return DRNMI_ENOTSUP;
