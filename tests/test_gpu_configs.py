@@ -94,14 +94,16 @@ def test_headline_1024x2048_exact_modes_vs_oracle(precision):
     if precision == "fp32":
         assert int(diff.sum()) == 0
     else:
-        assert int(diff.sum()) <= 4 and not np.any(diff & (margin > 1e-5))
+        # fp32x: measured 1 flip of 2,097,152 (an fp32 accumulation-order tie, oracle margin 4.8e-7)
+        assert int(diff.sum()) <= 2 and not np.any(diff & (margin > 1e-5))
 
 
 def test_headline_1024x2048_bf16_vs_oracle():
     """Config C2, the headline path itself: bf16 DRNSeg.segment (the seg_video loop bench.py times:
     uint8 frames -> labels, seg_video_old_no_plot.py:157-169, semantic_seg.py:445) on bench.py's
-    seed-0 weights and both of its 1024x2048 parity frames vs the fp32 oracle.  Gates just below
-    the measured values (round 4 bench: 99.945 % of 4,194,304 labels, mIoU vs ref 96.5)."""
+    seed-0 weights and both of its 1024x2048 parity frames vs the fp32 oracle.  Gates just above
+    the measured flips (rounds 4-6: 2,309 of 4,194,304 labels differ, 99.945 %, mIoU vs ref 96.53;
+    every bf16 tile change since is bit-identical, so a real regression shows as more flips)."""
     from drnmi import metrics
     from drnmi.drnseg import build
     from drnmi.weights import synth_frames
@@ -121,7 +123,7 @@ def test_headline_1024x2048_bf16_vs_oracle():
     miou = float(metrics.miou(hist.cpu().numpy()))
     print(f"headline D-22 2x1024x2048 bf16 segment: labels agree {agree:.6f} "
           f"({int((lab != ref).sum())} of {lab.numel()} differ), mIoU vs ref {miou:.2f}")
-    assert agree >= 0.999 and miou >= 96.0
+    assert int((lab != ref).sum()) <= 2600 and miou >= 96.3
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp32x"])
